@@ -1,0 +1,177 @@
+/*
+ * vlp_hip.h — C ABI of libvlp_hip.so, the MI355X (gfx950) implementation of the
+ * CLIP-style contrastive pretraining step of
+ * schusterbenjamin/Vision-Language-Pretraining-for-Bone-Tumor-Detection.
+ *
+ * The reference is pure Python: its hot path is VisionLanguageModule
+ * (src/models/pretrain/VisionLanguageModule.py) whose arithmetic is delegated to
+ * timm resnet34 (:30-35), HF BertModel/TinyBERT (:38-60), the head in forward
+ * (:441-461), _compute_loss (:532-554) and torch.optim.AdamW (:130-184).  Each
+ * entry point below replaces one of the device operations those calls dispatch
+ * to; the Python host layer (vlp_amd/, src/models/pretrain/VisionLanguageModule.py
+ * in this package) binds them with ctypes exactly as INTEGRATION.md shows.
+ *
+ * Conventions
+ *  - All tensor arguments are DEVICE pointers (caller-allocated, e.g. by the
+ *    PyTorch caching allocator); `stream` is a hipStream_t passed as void*.
+ *    Every call only enqueues work on `stream`; none synchronises.
+ *  - `dtype`: 0 = fp32 (parity mode), 1 = bf16 (throughput mode) storage of
+ *    activations/gradients.  Weight gradients, BN statistics, and optimizer
+ *    state are always fp32 (fp64 for BN sums).
+ *  - Activations are NHWC ([N][H][W][C], C innermost); token hidden states are
+ *    row-major [B*T][D].
+ *  - Return value: 0 on success, otherwise a hipError_t code.
+ *  - Stateless and re-entrant; "accumulate" outputs require the caller to zero
+ *    them first (documented per call).
+ */
+#ifndef VLP_HIP_H
+#define VLP_HIP_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int vlp_abi_version(void);
+
+/* ---------------- image tower: convolutions ----------------
+ * Replace the cuDNN conv fwd/dgrad/wgrad calls made by timm resnet34
+ * (VisionLanguageModule.py:30-35 -> ImageEncoder.forward).
+ * Weight operands are produced by vlp_pack_conv:
+ *   wp = [Co][KH][KW][C]   (forward),  wt = [C][KH][KW][Co]   (data gradient).
+ */
+/* y[N][Ho][Wo][Co] = conv(x, w); optionally x := relu(in_scale*x + in_shift)
+ * per input channel on load (previous BN+ReLU); accumulates per-channel
+ * sum / sum of squares of y into stat_sum / stat_sumsq (fp64, zeroed by caller). */
+int vlp_conv_fwd(int dtype, const void* x, const void* wp, void* y, int N, int H, int W, int C,
+                 int Co, int KH, int KW, int S, int P, const float* in_scale,
+                 const float* in_shift, double* stat_sum, double* stat_sumsq, void* stream);
+/* dx[N][H][W][C] = conv^T(dy, w).  If y_bn != NULL: dx := dx * (bn_scale*y_bn +
+ * bn_shift > 0) (ReLU mask of the producing BN+ReLU) and stat1 += sum(dx),
+ * stat2 += sum(dx * (y_bn - bn_mean) * bn_invstd); else if addend != NULL:
+ * dx += addend (residual-branch gradient). */
+int vlp_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, int N, int H, int W, int C,
+                   int Co, int KH, int KW, int S, int P, const void* addend, const void* y_bn,
+                   const float* bn_scale, const float* bn_shift, const float* bn_mean,
+                   const float* bn_invstd, double* stat1, double* stat2, void* stream);
+/* dw_ws[Co][KH][KW][C] += sum over pixels dy x_patch (fp32 atomics; zero first).
+ * Optional BN+ReLU-on-load of x as in vlp_conv_fwd. */
+int vlp_conv_wgrad(int dtype, const void* dy, const void* x, float* dw_ws, int N, int H, int W,
+                   int C, int Co, int KH, int KW, int S, int P, const float* in_scale,
+                   const float* in_shift, void* stream);
+
+/* stem conv 7x7/2 pad 3, 3 -> 64 channels, on a zero-padded NHWC4 image xp of
+ * size [N][Hp][Wp][4] (vlp_stem_geom); the caller zeroes xp once. */
+void vlp_stem_geom(int H, int W, int* Ho, int* Wo, int* Hp, int* Wp);
+int vlp_stem_prep(int dtype, const float* x_nchw, void* xp, int N, int H, int W, void* stream);
+int vlp_stem_prep_u8(int dtype, const uint8_t* x_u8, void* xp, int N, int H, int W, float mean,
+                     float std, void* stream);
+int vlp_stem_fwd(int dtype, const void* xp, const void* wp, void* y, int N, int H, int W,
+                 double* stat_sum, double* stat_sumsq, void* stream);
+int vlp_stem_wgrad(int dtype, const void* dy, const void* xp, float* dw_ws, int N, int H, int W,
+                   void* stream);
+
+/* ---------------- image tower: BatchNorm / residual / pooling ---------------- */
+int vlp_bn_finalize(int C, double count, const double* sum, const double* sumsq,
+                    const float* gamma, const float* beta, float eps, float momentum,
+                    float* running_mean, float* running_var, float* scale, float* shift,
+                    float* mean, float* invstd, void* stream);
+int vlp_bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* running_mean,
+                       const float* running_var, float eps, float* scale, float* shift,
+                       void* stream);
+/* out = relu(sc*y + sh + idt'), idt' = idt (scd == NULL) or scd*idt + shd */
+int vlp_bn_add_relu(int dtype, long long M, int C, const void* y, const float* sc, const float* sh,
+                    const void* idt, const float* scd, const float* shd, void* out, void* stream);
+/* g = dout * (mask > 0) (dout may be a broadcast [N][C]/HW gradient `dbc`);
+ * sum_g += sum g, sum_ga += sum g*xhat(ya), sum_gb += sum g*xhat(yb) */
+int vlp_bn_bwd_reduce(int dtype, long long M, int C, const void* dout, const float* dbc, int HW,
+                      const void* mask, const void* ya, const float* mean_a, const float* istd_a,
+                      const void* yb, const float* mean_b, const float* istd_b, double* sum_g,
+                      double* sum_ga, double* sum_gb, void* stream);
+/* dy_s = gamma_s*istd_s*(g - mean(g) - xhat_s*mean(g*xhat_s)) for sides a, b; g_out = g */
+int vlp_bn_bwd_apply(int dtype, long long M, int C, const void* dout, const float* dbc, int HW,
+                     const void* mask, const void* ya, const float* mean_a, const float* istd_a,
+                     const float* gamma_a, const double* sum_g_a, const double* sum_gx_a,
+                     void* dy_a, const void* yb, const float* mean_b, const float* istd_b,
+                     const float* gamma_b, const double* sum_g_b, const double* sum_gx_b,
+                     void* dy_b, void* g_out, void* stream);
+int vlp_bn_param_grad(int C, const double* sum_g, const double* sum_gx, float* dgamma,
+                      float* dbeta, void* stream);
+int vlp_maxpool_fwd(int dtype, int N, int H, int W, int C, const void* y, const float* sc,
+                    const float* sh, void* out, uint8_t* idx, void* stream);
+int vlp_maxpool_bwd(int dtype, int N, int H, int W, int C, const void* dp, const uint8_t* idx,
+                    const void* y, const float* sc, const float* sh, const float* mean,
+                    const float* istd, void* g_out, double* sum_g, double* sum_gx, void* stream);
+int vlp_avgpool_fwd(int dtype, int N, int HW, int C, const void* x, void* feat, void* stream);
+
+/* ---------------- text tower (TinyBERT) ----------------
+ * Replace the cuBLAS/ATen kernels of HF BertModel (VisionLanguageModule.py:45, :57-60). */
+/* y = x W^T + bias; mode 0 plain, 1 aux = pre-activation & y = gelu(aux),
+ * 2 y = dropout_p(x W^T + bias) + res */
+int vlp_linear_fwd(int dtype, int M, int N, int K, const void* x, int ldx, const void* w,
+                   const float* bias, void* y, int ldy, int mode, void* aux, const void* res,
+                   int ldr, float p, unsigned long long seed, void* stream);
+/* dx = dy W; mode 1: dx *= gelu'(aux); mode 0: dx += addend (if non-NULL) */
+int vlp_linear_dgrad(int dtype, int M, int Kin, int Nout, const void* dy, int lddy, const void* w,
+                     void* dx, int lddx, int mode, const void* aux, int ldaux, const void* addend,
+                     int ldad, void* stream);
+/* dw[Nout][Kin] += dy^T x (fp32 atomics; zero first) */
+int vlp_linear_wgrad(int dtype, int M, int Nout, int Kin, const void* dy, int lddy, const void* x,
+                     int ldx, float* dw, void* stream);
+/* out[n] += sum_m x[m][n] (bias gradients; fp32 atomics) */
+int vlp_colsum(int dtype, int M, int N, const void* x, int ld, float* out, void* stream);
+int vlp_layernorm_fwd(int dtype, int M, int D, const void* x, const float* gamma,
+                      const float* beta, float eps, void* y, float* mean, float* rstd, float p,
+                      unsigned long long seed, void* stream);
+int vlp_layernorm_bwd(int dtype, int M, int D, const void* dy, float p_out,
+                      unsigned long long seed_out, const void* x, const float* mean,
+                      const float* rstd, const float* gamma, void* dx, void* dxd, float p_in,
+                      unsigned long long seed_in, float* dgamma, float* dbeta, void* stream);
+int vlp_attn_fwd(int dtype, int B, int T, int H, int dh, const void* qkv, const long long* amask,
+                 void* ctx, float* P, float scale, float p, unsigned long long seed, void* stream);
+int vlp_attn_bwd(int dtype, int B, int T, int H, int dh, const void* qkv, const float* P,
+                 const void* dctx, void* dqkv, float scale, float p, unsigned long long seed,
+                 void* stream);
+int vlp_embed_fwd(int dtype, int M, int T, int D, const long long* ids, const long long* tt,
+                  const float* wemb, const float* pemb, const float* temb, void* e_out,
+                  void* stream);
+int vlp_embed_bwd(int dtype, int M, int T, int D, const long long* ids, const long long* tt,
+                  const void* de, float* dwemb, float* dpemb, float* dtemb, void* stream);
+int vlp_scatter_rows(int dtype, int R, int D, const void* in, int ldi, void* out, int ldo,
+                     void* stream);
+
+/* ---------------- contrastive head ----------------
+ * Replace forward (:441-461) and _compute_loss (:532-554). */
+int vlp_l2norm_fwd(int R, int E, const float* x, float* y, float* norm, void* stream);
+int vlp_l2norm_bwd(int dtype, int R, int E, const float* y, const float* norm, const float* dy,
+                   float* dx, void* dx_t, void* stream);
+/* Fused global-batch symmetric InfoNCE, forward + backward.  img_all/txt_all:
+ * [N][E] gathered normalised embeddings; this rank owns rows [offset, offset+B).
+ * g_img_all/g_txt_all (+=, zero first): d loss / d embeddings for all N rows;
+ * d_logit_scale (+=); loss_parts[0] (+=) sum of image->text CE terms of the
+ * local rows, loss_parts[1] text->image; lse_out (optional) [2][B]. */
+int vlp_clip_loss_fused(int B, int N, int E, int offset, const float* img_all,
+                        const float* txt_all, const float* logit_scale, float* g_img_all,
+                        float* g_txt_all, float* d_logit_scale, float* loss_parts,
+                        float* lse_out, void* stream);
+/* symmetric CE over explicit logits [B][B]: out = {loss, image_loss, text_loss} (+=);
+ * dlogits (+=, optional) */
+int vlp_ce_sym(int B, const float* logits, float* out, float* dlogits, void* stream);
+int vlp_matmul(int dtype, int M, int N, int K, const void* A, int lda, int a_kc, const void* B,
+               int ldb, int b_kc, void* C, int ldc, int out_f32, float alpha, int accumulate,
+               void* stream);
+int vlp_cast(int dtype, long long n, const float* x, void* y, void* stream);
+
+/* ---------------- optimizer / packing ----------------
+ * Replace torch.optim.AdamW (configs/optimizer/adamw.yaml). */
+int vlp_adamw(long long n, float* p, const float* g, float* m, float* v, float lr, float beta1,
+              float beta2, float eps, float wd, float step_size, float bc2_sqrt, void* stream);
+int vlp_pack_conv(int dtype, int Co, int C, int KH, int KW, const float* w, void* wp, void* wt,
+                  void* stream);
+int vlp_pack_stem(int dtype, const float* w, void* wp, void* stream);
+int vlp_unpack_conv_grad(int Co, int C, int KH, int KW, const float* ws, float* g, void* stream);
+int vlp_unpack_stem_grad(const float* ws, float* g, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VLP_HIP_H */

@@ -1,0 +1,169 @@
+"""Op-level parity of the HIP kernels against the CPU fp32 oracle ops.
+
+fp32 storage mode must match torch fp32 to ~1e-5 relative; bf16 mode is
+compared against fp32 math on the SAME bf16-rounded inputs, tolerance 2e-2
+relative (bf16 output rounding + fp32 accumulation order).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DT = [torch.float32, torch.bfloat16]
+
+
+def rel(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def tol(dt):
+    return 2e-5 if dt == torch.float32 else 1.5e-2
+
+
+@pytest.fixture(scope="module")
+def ops():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vlp_amd import ops as o
+    return o
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("akc,bkc", [(1, 1), (1, 0), (0, 1), (0, 0)])
+def test_matmul_layouts(ops, dt, akc, bkc):
+    torch.manual_seed(0)
+    M, N, K = 208, 136, 328
+    A = torch.randn(M, K).to(dt).float()
+    B = torch.randn(N, K).to(dt).float()
+    ref = A @ B.T
+    Ad = (A if akc else A.T.contiguous()).to(dt).cuda()
+    Bd = (B if bkc else B.T.contiguous()).to(dt).cuda()
+    C = torch.empty(M, N, device="cuda", dtype=torch.float32)
+    ops.matmul(Ad, Bd, C, M, N, K, K if akc else M, akc, K if bkc else N, bkc, N)
+    torch.cuda.synchronize()
+    assert rel(C, ref) < tol(dt) / 4
+
+
+CONV_CASES = [
+    # N, H, W, C, Co, KH, KW, S, P
+    (2, 12, 12, 64, 64, 3, 3, 1, 1),
+    (2, 12, 12, 64, 128, 3, 3, 2, 1),
+    (2, 12, 12, 64, 128, 1, 1, 2, 0),
+    (3, 7, 9, 128, 64, 3, 3, 1, 1),
+]
+
+
+def nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def nchw(t):
+    return t.permute(0, 3, 1, 2).contiguous()
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("case", CONV_CASES)
+@pytest.mark.parametrize("xform", [False, True])
+def test_conv_fwd(ops, dt, case, xform):
+    N, H, W, C, Co, KH, KW, S, P = case
+    torch.manual_seed(1)
+    x = torch.randn(N, C, H, W).to(dt).float()
+    w = (torch.randn(Co, C, KH, KW) * (C * KH * KW) ** -0.5).to(dt).float()
+    sc = torch.rand(C) + 0.5
+    sh = torch.randn(C) * 0.3
+    xin = torch.relu(x * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1)) if xform else x
+    if xform and dt == torch.bfloat16:
+        xin = xin.to(dt).float()
+    ref = F.conv2d(xin, w, stride=S, padding=P)
+    wp = torch.empty(Co, KH, KW, C, dtype=dt, device="cuda")
+    ops.pack_conv(w.cuda(), wp, None)
+    s1 = torch.zeros(Co, dtype=torch.float64, device="cuda")
+    s2 = torch.zeros_like(s1)
+    y = ops.conv_fwd(nhwc(x).to(dt).cuda(), wp, Co, KH, KW, S, P,
+                     sc.cuda() if xform else None, sh.cuda() if xform else None, s1, s2)
+    torch.cuda.synchronize()
+    assert rel(nchw(y.float().cpu()), ref) < tol(dt)
+    assert rel(s1.cpu(), ref.sum((0, 2, 3))) < 1e-4
+    assert rel(s2.cpu(), (ref * ref).sum((0, 2, 3))) < 1e-4
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_dgrad_wgrad(ops, dt, case):
+    N, H, W, C, Co, KH, KW, S, P = case
+    torch.manual_seed(2)
+    x = torch.randn(N, C, H, W).to(dt).float().requires_grad_()
+    w = (torch.randn(Co, C, KH, KW) * (C * KH * KW) ** -0.5).to(dt).float().requires_grad_()
+    y = F.conv2d(x, w, stride=S, padding=P)
+    dy = torch.randn_like(y).to(dt).float()
+    y.backward(dy)
+    wt = torch.empty(C, KH, KW, Co, dtype=dt, device="cuda")
+    ops.pack_conv(w.detach().cuda(), None, wt)
+    add = torch.randn(N, C, H, W).to(dt).float()
+    dx = ops.conv_dgrad(nhwc(dy).to(dt).cuda(), wt, H, W, C, KH, KW, S, P,
+                        addend=nhwc(add).to(dt).cuda())
+    ws = torch.zeros(Co, KH, KW, C, device="cuda")
+    ops.conv_wgrad(nhwc(dy).to(dt).cuda(), nhwc(x.detach()).to(dt).cuda(), KH, KW, S, P, ws)
+    g = torch.empty(Co, C, KH, KW, device="cuda")
+    ops.unpack_conv_grad(ws, g)
+    torch.cuda.synchronize()
+    assert rel(nchw(dx.float().cpu()), x.grad + add) < tol(dt)
+    assert rel(g.cpu(), w.grad) < tol(dt) / 2
+
+
+@pytest.mark.parametrize("dt", DT)
+def test_conv_dgrad_bn_epilogue(ops, dt):
+    N, H, W, C, Co, KH, KW, S, P = 2, 10, 10, 64, 64, 3, 3, 1, 1
+    torch.manual_seed(3)
+    dy = torch.randn(N, Co, H, W).to(dt).float()
+    w = (torch.randn(Co, C, KH, KW) * 0.05).to(dt).float()
+    ybn = torch.randn(N, C, H, W).to(dt).float()
+    sc, sh = torch.rand(C) + 0.5, torch.randn(C) * 0.2
+    mu, ist = torch.randn(C) * 0.1, torch.rand(C) + 0.5
+    dxr = torch.nn.grad.conv2d_input(ybn.shape, w, dy, stride=S, padding=P)
+    if dt == torch.bfloat16:
+        dxr = dxr.to(dt).float()
+    mask = (ybn * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1)) > 0
+    gref = dxr * mask
+    xh = (ybn - mu.view(1, -1, 1, 1)) * ist.view(1, -1, 1, 1)
+    wt = torch.empty(C, KH, KW, Co, dtype=dt, device="cuda")
+    ops.pack_conv(w.cuda(), None, wt)
+    s1 = torch.zeros(C, dtype=torch.float64, device="cuda")
+    s2 = torch.zeros_like(s1)
+    g = ops.conv_dgrad(nhwc(dy).to(dt).cuda(), wt, H, W, C, KH, KW, S, P, y_bn=nhwc(ybn).to(dt).cuda(),
+                       bn=(sc.cuda(), sh.cuda(), mu.cuda(), ist.cuda()), stat1=s1, stat2=s2)
+    torch.cuda.synchronize()
+    assert rel(nchw(g.float().cpu()), gref) < tol(dt)
+    assert rel(s1.cpu(), gref.sum((0, 2, 3))) < tol(dt)
+    assert rel(s2.cpu(), (gref * xh).sum((0, 2, 3))) < tol(dt)
+
+
+@pytest.mark.parametrize("dt", DT)
+def test_stem_fwd_wgrad(ops, dt):
+    N, H, W = 2, 32, 30
+    torch.manual_seed(4)
+    x = torch.randn(N, 3, H, W).to(dt).float()
+    w = (torch.randn(64, 3, 7, 7) * 0.1).to(dt).float().requires_grad_()
+    y = F.conv2d(x, w, stride=2, padding=3)
+    dy = torch.randn_like(y).to(dt).float()
+    y.backward(dy)
+    Ho, Wo, Hp, Wp = ops.stem_geom(H, W)
+    assert (Ho, Wo) == tuple(y.shape[2:])
+    xp = torch.zeros(N, Hp, Wp, 4, dtype=dt, device="cuda")
+    ops.stem_prep(x.cuda(), xp)
+    wp = torch.empty(64, 256, dtype=dt, device="cuda")
+    ops.pack_stem(w.detach().cuda(), wp)
+    yd = torch.empty(N, Ho, Wo, 64, dtype=dt, device="cuda")
+    s1 = torch.zeros(64, dtype=torch.float64, device="cuda")
+    s2 = torch.zeros_like(s1)
+    ops.stem_fwd(xp, wp, N, H, W, yd, s1, s2)
+    ws = torch.zeros(64, 256, device="cuda")
+    ops.stem_wgrad(nhwc(dy).to(dt).cuda(), xp, N, H, W, ws)
+    g = torch.empty(64, 3, 7, 7, device="cuda")
+    ops.unpack_stem_grad(ws, g)
+    torch.cuda.synchronize()
+    assert rel(nchw(yd.float().cpu()), y.detach()) < tol(dt)
+    assert rel(g.cpu(), w.grad) < tol(dt) / 2

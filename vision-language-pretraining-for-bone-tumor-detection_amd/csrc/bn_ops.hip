@@ -1,0 +1,464 @@
+// Train-mode BatchNorm2d, residual add + ReLU, max/avg pooling for the ResNet34
+// tower (timm BasicBlock semantics: conv-bn-relu-conv-bn (+shortcut) relu;
+// stem conv-bn-relu-maxpool3x3/2; global average pool), NHWC layout.
+//
+// Batch statistics come from the conv epilogues (fp64 sums); everything here
+// is an HBM-bound streaming pass over [M = N*H*W][C] tensors in 16-byte chunks.
+#include "common.h"
+
+namespace vlp {
+
+constexpr int kEwThreads = 256;
+
+static inline int ew_blocks(size_t work, int per_block = kEwThreads, int cap = 8192) {
+  size_t b = (work + per_block - 1) / per_block;
+  if (b > (size_t)cap) b = cap;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+// ---- finalize batch statistics -> affine coefficients, running stats ----
+__global__ void bn_finalize_kernel(int C, double count, const double* __restrict__ sum,
+                                   const double* __restrict__ sumsq, const float* __restrict__ gamma,
+                                   const float* __restrict__ beta, float eps, float momentum,
+                                   float* running_mean, float* running_var, float* scale,
+                                   float* shift, float* mean_out, float* invstd_out) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double mean = sum[c] / count;
+  double var = sumsq[c] / count - mean * mean;
+  if (var < 0) var = 0;
+  float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  float sc = gamma[c] * invstd;
+  scale[c] = sc;
+  shift[c] = beta[c] - (float)mean * sc;
+  mean_out[c] = (float)mean;
+  invstd_out[c] = invstd;
+  if (running_mean) {
+    float unbiased = (float)(count > 1 ? var * count / (count - 1) : var);
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
+  }
+}
+
+// eval-mode coefficients from running statistics
+__global__ void bn_eval_kernel(int C, const float* gamma, const float* beta, const float* rm,
+                               const float* rv, float eps, float* scale, float* shift) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float invstd = 1.f / sqrtf(rv[c] + eps);
+  scale[c] = gamma[c] * invstd;
+  shift[c] = beta[c] - rm[c] * gamma[c] * invstd;
+}
+
+// ---- out = relu(sc*y + sh + identity), identity = idt or (scd*idt + shd) ----
+template <typename T>
+__global__ void bn_add_relu_kernel(size_t nchunks, int C, const T* __restrict__ y,
+                                   const float* __restrict__ sc, const float* __restrict__ sh,
+                                   const T* __restrict__ idt, const float* __restrict__ scd,
+                                   const float* __restrict__ shd, T* __restrict__ out) {
+  constexpr int E = Chunk<T>::N;
+  const int cpr = C / E;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nchunks;
+       i += (size_t)gridDim.x * blockDim.x) {
+    int c0 = (int)(i % cpr) * E;
+    float a[E], b[E];
+    Chunk<T>::unpack(ldg16(y + i * E), a);
+    if (idt) Chunk<T>::unpack(ldg16(idt + i * E), b);
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      float v = fmaf(a[j], sc[c0 + j], sh[c0 + j]);
+      if (idt) v += scd ? fmaf(b[j], scd[c0 + j], shd[c0 + j]) : b[j];
+      a[j] = fmaxf(v, 0.f);
+    }
+    stg16(out + i * E, Chunk<T>::pack(a));
+  }
+}
+
+// ---- backward reduction: g = dout * (out > 0); sums of g, g*xhat_a, g*xhat_b ----
+// dout may instead be a broadcast [N][C] gradient divided by HW (global avg pool).
+template <typename T>
+__global__ void __launch_bounds__(256)
+bn_bwd_reduce_kernel(int M, int C, const T* __restrict__ dout, const float* __restrict__ dbc,
+                     int HW, const T* __restrict__ mask, const T* __restrict__ ya,
+                     const float* __restrict__ mean_a, const float* __restrict__ istd_a,
+                     const T* __restrict__ yb, const float* __restrict__ mean_b,
+                     const float* __restrict__ istd_b, double* sum_g, double* sum_ga,
+                     double* sum_gb) {
+  constexpr int E = Chunk<T>::N;
+  const int cpr = C / E;
+  const int rows_per_iter = 256 / cpr;
+  const int t = threadIdx.x;
+  const int cc = t % cpr, rr = t / cpr;
+  const int c0 = cc * E;
+  float ag[E], aa[E], ab[E];
+  float ma[E], ia[E], mb[E], ib[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    ag[j] = aa[j] = ab[j] = 0.f;
+    ma[j] = mean_a[c0 + j]; ia[j] = istd_a[c0 + j];
+    mb[j] = yb ? mean_b[c0 + j] : 0.f; ib[j] = yb ? istd_b[c0 + j] : 0.f;
+  }
+  if (rr < rows_per_iter) {
+    for (int m = blockIdx.x * rows_per_iter + rr; m < M; m += gridDim.x * rows_per_iter) {
+      size_t o = (size_t)m * C + c0;
+      float g[E], mk[E], y1[E], y2[E];
+      if (dbc) {
+        int n = m / HW;
+#pragma unroll
+        for (int j = 0; j < E; ++j) g[j] = dbc[(size_t)n * C + c0 + j] / (float)HW;
+      } else {
+        Chunk<T>::unpack(ldg16(dout + o), g);
+      }
+      if (mask) {
+        Chunk<T>::unpack(ldg16(mask + o), mk);
+#pragma unroll
+        for (int j = 0; j < E; ++j) g[j] = mk[j] > 0.f ? g[j] : 0.f;
+      }
+      Chunk<T>::unpack(ldg16(ya + o), y1);
+      if (yb) Chunk<T>::unpack(ldg16(yb + o), y2);
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        ag[j] += g[j];
+        aa[j] += g[j] * ((y1[j] - ma[j]) * ia[j]);
+        if (yb) ab[j] += g[j] * ((y2[j] - mb[j]) * ib[j]);
+      }
+    }
+  }
+  // reduce across the rows handled by this block
+  __shared__ float red[3][256][E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) { red[0][t][j] = ag[j]; red[1][t][j] = aa[j]; red[2][t][j] = ab[j]; }
+  __syncthreads();
+  if (t < cpr) {
+    for (int r = 1; r < rows_per_iter; ++r)
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        ag[j] += red[0][t + r * cpr][j];
+        aa[j] += red[1][t + r * cpr][j];
+        ab[j] += red[2][t + r * cpr][j];
+      }
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      atomicAdd(sum_g + c0 + j, (double)ag[j]);
+      atomicAdd(sum_ga + c0 + j, (double)aa[j]);
+      if (yb) atomicAdd(sum_gb + c0 + j, (double)ab[j]);
+    }
+  }
+}
+
+// ---- backward apply: dy_a = k_a*(g - mean(g) - xhat_a*mean(g xhat_a)), same for b ----
+struct BnBwdSide {
+  const void* y; const float* mean; const float* istd; const float* gamma;
+  const double* sum_g; const double* sum_gx; void* dy;
+};
+template <typename T>
+__global__ void bn_bwd_apply_kernel(size_t nchunks, int C, double count, const T* __restrict__ dout,
+                                    const float* __restrict__ dbc, int HW, const T* __restrict__ mask,
+                                    BnBwdSide A, BnBwdSide B, T* __restrict__ g_out) {
+  constexpr int E = Chunk<T>::N;
+  const int cpr = C / E;
+  const float inv_count = (float)(1.0 / count);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nchunks;
+       i += (size_t)gridDim.x * blockDim.x) {
+    int c0 = (int)(i % cpr) * E;
+    size_t m = i / cpr;
+    float g[E], mk[E], y[E], d[E];
+    if (dbc) {
+      int n = (int)(m / HW);
+#pragma unroll
+      for (int j = 0; j < E; ++j) g[j] = dbc[(size_t)n * C + c0 + j] / (float)HW;
+    } else {
+      Chunk<T>::unpack(ldg16(dout + i * E), g);
+    }
+    if (mask) {
+      Chunk<T>::unpack(ldg16(mask + i * E), mk);
+#pragma unroll
+      for (int j = 0; j < E; ++j) g[j] = mk[j] > 0.f ? g[j] : 0.f;
+    }
+    if (g_out) stg16(g_out + i * E, Chunk<T>::pack(g));
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      const BnBwdSide& S = side ? B : A;
+      if (!S.dy) continue;
+      Chunk<T>::unpack(ldg16((const T*)S.y + i * E), y);
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        int c = c0 + j;
+        float is = S.istd[c];
+        float xh = (y[j] - S.mean[c]) * is;
+        float mg = (float)S.sum_g[c] * inv_count;
+        float mgx = (float)S.sum_gx[c] * inv_count;
+        d[j] = S.gamma[c] * is * (g[j] - mg - xh * mgx);
+      }
+      stg16((T*)S.dy + i * E, Chunk<T>::pack(d));
+    }
+  }
+}
+
+// dgamma = sum(g*xhat), dbeta = sum(g)
+__global__ void bn_param_grad_kernel(int C, const double* sum_g, const double* sum_gx, float* dgamma,
+                                     float* dbeta) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  dgamma[c] = (float)sum_gx[c];
+  dbeta[c] = (float)sum_g[c];
+}
+
+// ---- stem: maxpool 3x3/2 pad 1 over relu(sc*y + sh); records the argmax tap ----
+template <typename T>
+__global__ void maxpool_fwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const T* __restrict__ y,
+                                   const float* __restrict__ sc, const float* __restrict__ sh,
+                                   T* __restrict__ out, uint8_t* __restrict__ idx) {
+  constexpr int E = Chunk<T>::N;
+  const int cpr = C / E;
+  size_t total = (size_t)N * Ho * Wo * cpr;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    int cc = (int)(i % cpr);
+    size_t p = i / cpr;
+    int wo = (int)(p % Wo);
+    size_t t = p / Wo;
+    int ho = (int)(t % Ho);
+    int n = (int)(t / Ho);
+    int c0 = cc * E;
+    float best[E], v[E];
+    uint8_t bi[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    for (int kh = 0; kh < 3; ++kh) {
+      int h = ho * 2 - 1 + kh;
+      if ((unsigned)h >= (unsigned)H) continue;
+      for (int kw = 0; kw < 3; ++kw) {
+        int w = wo * 2 - 1 + kw;
+        if ((unsigned)w >= (unsigned)W) continue;
+        Chunk<T>::unpack(ldg16(y + (((size_t)n * H + h) * W + w) * C + c0), v);
+#pragma unroll
+        for (int j = 0; j < E; ++j) {
+          float a = fmaxf(fmaf(v[j], sc[c0 + j], sh[c0 + j]), 0.f);
+          if (a > best[j]) { best[j] = a; bi[j] = (uint8_t)(kh * 3 + kw); }
+        }
+      }
+    }
+    stg16(out + p * C + c0, Chunk<T>::pack(best));
+#pragma unroll
+    for (int j = 0; j < E; ++j) idx[p * C + c0 + j] = bi[j];
+  }
+}
+
+// ---- stem backward: route pooled gradient to argmax, ReLU mask, BN stats ----
+template <typename T>
+__global__ void __launch_bounds__(256)
+maxpool_bwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const T* __restrict__ dp,
+                   const uint8_t* __restrict__ idx, const T* __restrict__ y,
+                   const float* __restrict__ sc, const float* __restrict__ sh,
+                   const float* __restrict__ mean, const float* __restrict__ istd,
+                   T* __restrict__ g_out, double* sum_g, double* sum_gx) {
+  constexpr int E = Chunk<T>::N;
+  const int cpr = C / E;
+  const int rows_per_iter = 256 / cpr;
+  const int t = threadIdx.x;
+  const int cc = t % cpr, rr = t / cpr;
+  const int c0 = cc * E;
+  const int M = N * H * W;
+  float ag[E], ax[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) ag[j] = ax[j] = 0.f;
+  for (int m = blockIdx.x * rows_per_iter + rr; m < M; m += gridDim.x * rows_per_iter) {
+    int w = m % W;
+    int tt = m / W;
+    int h = tt % H;
+    int n = tt / H;
+    float g[E], v[E], yv[E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) g[j] = 0.f;
+    for (int dh = 0; dh < 3; ++dh) {
+      int th = h + 1 - dh;
+      if (th < 0 || (th & 1)) continue;
+      int ho = th >> 1;
+      if (ho >= Ho) continue;
+      for (int dw = 0; dw < 3; ++dw) {
+        int tw = w + 1 - dw;
+        if (tw < 0 || (tw & 1)) continue;
+        int wo = tw >> 1;
+        if (wo >= Wo) continue;
+        size_t po = (((size_t)n * Ho + ho) * Wo + wo) * C + c0;
+        Chunk<T>::unpack(ldg16(dp + po), v);
+        const uint8_t tap = (uint8_t)(dh * 3 + dw);
+#pragma unroll
+        for (int j = 0; j < E; ++j)
+          if (idx[po + j] == tap) g[j] += v[j];
+      }
+    }
+    size_t o = (size_t)m * C + c0;
+    Chunk<T>::unpack(ldg16(y + o), yv);
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      if (!(fmaf(yv[j], sc[c0 + j], sh[c0 + j]) > 0.f)) g[j] = 0.f;
+      ag[j] += g[j];
+      ax[j] += g[j] * ((yv[j] - mean[c0 + j]) * istd[c0 + j]);
+    }
+    stg16(g_out + o, Chunk<T>::pack(g));
+  }
+  __shared__ float red[2][256][E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) { red[0][t][j] = ag[j]; red[1][t][j] = ax[j]; }
+  __syncthreads();
+  if (t < cpr) {
+    for (int r = 1; r < rows_per_iter; ++r)
+#pragma unroll
+      for (int j = 0; j < E; ++j) { ag[j] += red[0][t + r * cpr][j]; ax[j] += red[1][t + r * cpr][j]; }
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      atomicAdd(sum_g + c0 + j, (double)ag[j]);
+      atomicAdd(sum_gx + c0 + j, (double)ax[j]);
+    }
+  }
+}
+
+// ---- global average pool: feat[n][c] = mean_hw x[n][hw][c] ----
+template <typename T>
+__global__ void avgpool_fwd_kernel(int N, int HW, int C, const T* __restrict__ x, T* __restrict__ feat) {
+  int n = blockIdx.x;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float s = 0.f;
+    for (int p = 0; p < HW; ++p) s += to_f(x[((size_t)n * HW + p) * C + c]);
+    feat[(size_t)n * C + c] = from_f<T>(s / (float)HW);
+  }
+}
+
+}  // namespace vlp
+
+using namespace vlp;
+
+VLP_EXPORT int vlp_bn_finalize(int C, double count, const double* sum, const double* sumsq,
+                               const float* gamma, const float* beta, float eps, float momentum,
+                               float* running_mean, float* running_var, float* scale, float* shift,
+                               float* mean, float* invstd, void* stream) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, C,
+                     count, sum, sumsq, gamma, beta, eps, momentum, running_mean, running_var, scale,
+                     shift, mean, invstd);
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* rm,
+                                  const float* rv, float eps, float* scale, float* shift,
+                                  void* stream) {
+  hipLaunchKernelGGL(bn_eval_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, C,
+                     gamma, beta, rm, rv, eps, scale, shift);
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_bn_add_relu(int dtype, long long M, int C, const void* y, const float* sc,
+                               const float* sh, const void* idt, const float* scd, const float* shd,
+                               void* out, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == VLP_BF16) {
+    size_t n = (size_t)M * C / 8;
+    hipLaunchKernelGGL(bn_add_relu_kernel<bf16>, dim3(ew_blocks(n)), dim3(256), 0, st, n, C,
+                       (const bf16*)y, sc, sh, (const bf16*)idt, scd, shd, (bf16*)out);
+  } else {
+    size_t n = (size_t)M * C / 4;
+    hipLaunchKernelGGL(bn_add_relu_kernel<float>, dim3(ew_blocks(n)), dim3(256), 0, st, n, C,
+                       (const float*)y, sc, sh, (const float*)idt, scd, shd, (float*)out);
+  }
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_bn_bwd_reduce(int dtype, long long M, int C, const void* dout, const float* dbc,
+                                 int HW, const void* mask, const void* ya, const float* mean_a,
+                                 const float* istd_a, const void* yb, const float* mean_b,
+                                 const float* istd_b, double* sum_g, double* sum_ga, double* sum_gb,
+                                 void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int epc = dtype == VLP_BF16 ? 8 : 4;
+  int rows_per_iter = 256 / (C / epc);
+  int blocks = ew_blocks((size_t)M, rows_per_iter * 16, 2048);
+  if (dtype == VLP_BF16)
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<bf16>, dim3(blocks), dim3(256), 0, st, (int)M, C,
+                       (const bf16*)dout, dbc, HW, (const bf16*)mask, (const bf16*)ya, mean_a, istd_a,
+                       (const bf16*)yb, mean_b, istd_b, sum_g, sum_ga, sum_gb);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, dim3(blocks), dim3(256), 0, st, (int)M, C,
+                       (const float*)dout, dbc, HW, (const float*)mask, (const float*)ya, mean_a,
+                       istd_a, (const float*)yb, mean_b, istd_b, sum_g, sum_ga, sum_gb);
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_bn_bwd_apply(int dtype, long long M, int C, const void* dout, const float* dbc,
+                                int HW, const void* mask,
+                                const void* ya, const float* mean_a, const float* istd_a,
+                                const float* gamma_a, const double* sum_g_a, const double* sum_gx_a,
+                                void* dy_a,
+                                const void* yb, const float* mean_b, const float* istd_b,
+                                const float* gamma_b, const double* sum_g_b, const double* sum_gx_b,
+                                void* dy_b, void* g_out, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  BnBwdSide A{ya, mean_a, istd_a, gamma_a, sum_g_a, sum_gx_a, dy_a};
+  BnBwdSide B{yb, mean_b, istd_b, gamma_b, sum_g_b, sum_gx_b, dy_b};
+  if (dtype == VLP_BF16) {
+    size_t n = (size_t)M * C / 8;
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16>, dim3(ew_blocks(n)), dim3(256), 0, st, n, C,
+                       (double)M, (const bf16*)dout, dbc, HW, (const bf16*)mask, A, B, (bf16*)g_out);
+  } else {
+    size_t n = (size_t)M * C / 4;
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(ew_blocks(n)), dim3(256), 0, st, n, C,
+                       (double)M, (const float*)dout, dbc, HW, (const float*)mask, A, B,
+                       (float*)g_out);
+  }
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_bn_param_grad(int C, const double* sum_g, const double* sum_gx, float* dgamma,
+                                 float* dbeta, void* stream) {
+  hipLaunchKernelGGL(bn_param_grad_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     C, sum_g, sum_gx, dgamma, dbeta);
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_maxpool_fwd(int dtype, int N, int H, int W, int C, const void* y, const float* sc,
+                               const float* sh, void* out, uint8_t* idx, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  int epc = dtype == VLP_BF16 ? 8 : 4;
+  size_t n = (size_t)N * Ho * Wo * (C / epc);
+  if (dtype == VLP_BF16)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<bf16>, dim3(ew_blocks(n)), dim3(256), 0, st, N, H, W, C, Ho,
+                       Wo, (const bf16*)y, sc, sh, (bf16*)out, idx);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(ew_blocks(n)), dim3(256), 0, st, N, H, W, C, Ho,
+                       Wo, (const float*)y, sc, sh, (float*)out, idx);
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_maxpool_bwd(int dtype, int N, int H, int W, int C, const void* dp,
+                               const uint8_t* idx, const void* y, const float* sc, const float* sh,
+                               const float* mean, const float* istd, void* g_out, double* sum_g,
+                               double* sum_gx, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  int epc = dtype == VLP_BF16 ? 8 : 4;
+  int rows_per_iter = 256 / (C / epc);
+  int blocks = ew_blocks((size_t)N * H * W, rows_per_iter * 16, 2048);
+  if (dtype == VLP_BF16)
+    hipLaunchKernelGGL(maxpool_bwd_kernel<bf16>, dim3(blocks), dim3(256), 0, st, N, H, W, C, Ho, Wo,
+                       (const bf16*)dp, idx, (const bf16*)y, sc, sh, mean, istd, (bf16*)g_out, sum_g,
+                       sum_gx);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, dim3(blocks), dim3(256), 0, st, N, H, W, C, Ho, Wo,
+                       (const float*)dp, idx, (const float*)y, sc, sh, mean, istd, (float*)g_out,
+                       sum_g, sum_gx);
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_avgpool_fwd(int dtype, int N, int HW, int C, const void* x, void* feat,
+                               void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == VLP_BF16)
+    hipLaunchKernelGGL(avgpool_fwd_kernel<bf16>, dim3(N), dim3(256), 0, st, N, HW, C, (const bf16*)x,
+                       (bf16*)feat);
+  else
+    hipLaunchKernelGGL(avgpool_fwd_kernel<float>, dim3(N), dim3(256), 0, st, N, HW, C,
+                       (const float*)x, (float*)feat);
+  return (int)hipGetLastError();
+}

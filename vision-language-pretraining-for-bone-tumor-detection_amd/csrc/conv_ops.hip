@@ -1,0 +1,478 @@
+// Implicit-GEMM convolutions for the ResNet34 image tower (timm `resnet34`,
+// called from the reference at src/models/pretrain/VisionLanguageModule.py:30-35).
+//
+// Layout: activations NHWC (channels innermost), weights packed per step from
+// the fp32 master tensors (timm [Co][C][KH][KW]) into
+//   Wp[Co][KH][KW][C]  (forward operand, K-contiguous)
+//   Wt[C][KH][KW][Co]  (data-gradient operand, K-contiguous)
+// so every operand streams as 16-byte chunks along the channel dimension.
+//
+//   fwd   : y[m=(n,ho,wo)][co]  = sum_{kh,kw,ci} x[n][ho*S-P+kh][wo*S-P+kw][ci] Wp[co][kh][kw][ci]
+//   dgrad : dx[m=(n,h,w)][ci]   = sum_{kh,kw,co} dy[n][(h+P-kh)/S][(w+P-kw)/S][co] Wt[ci][kh][kw][co]
+//   wgrad : dW[co][(kh,kw,ci)]  = sum_{m} dy[m][co] * x_patch[m][(kh,kw,ci)]     (split-K over m)
+//
+// Fusions: the forward epilogue accumulates train-mode BatchNorm batch
+// statistics (sum, sum of squares per channel, fp64 atomics); the forward and
+// weight-gradient loaders can apply the previous layer's BN+ReLU on load, so
+// the post-activation tensor is never materialised; the data-gradient epilogue
+// can apply the ReLU mask of the producer layer and accumulate that BN's
+// backward statistics, or add a residual-branch gradient.
+#include "gemm.h"
+
+namespace vlp {
+
+struct ConvGeom {
+  int N, H, W, C, Co, KH, KW, S, P, Ho, Wo;
+  int M;      // rows of the GEMM
+  int K;      // reduction length
+  FastDiv fd_howo, fd_wo, fd_hw, fd_w, fd_c, fd_co, fd_kw;
+};
+
+static ConvGeom make_geom(int N, int H, int W, int C, int Co, int KH, int KW, int S, int P) {
+  ConvGeom g;
+  g.N = N; g.H = H; g.W = W; g.C = C; g.Co = Co; g.KH = KH; g.KW = KW; g.S = S; g.P = P;
+  g.Ho = (H + 2 * P - KH) / S + 1;
+  g.Wo = (W + 2 * P - KW) / S + 1;
+  g.M = 0; g.K = 0;
+  g.fd_howo = make_fastdiv(g.Ho * g.Wo);
+  g.fd_wo = make_fastdiv(g.Wo);
+  g.fd_hw = make_fastdiv(H * W);
+  g.fd_w = make_fastdiv(W);
+  g.fd_c = make_fastdiv(C);
+  g.fd_co = make_fastdiv(Co);
+  g.fd_kw = make_fastdiv(KW);
+  return g;
+}
+
+// Optional per-channel affine + ReLU applied to a loaded chunk (BN-apply on load).
+template <typename T>
+__device__ __forceinline__ uint4 xform_chunk(uint4 v, const float* sc, const float* sh, int c) {
+  constexpr int E = Chunk<T>::N;
+  float f[E];
+  Chunk<T>::unpack(v, f);
+#pragma unroll
+  for (int j = 0; j < E; ++j) f[j] = fmaxf(fmaf(f[j], sc[c + j], sh[c + j]), 0.f);
+  return Chunk<T>::pack(f);
+}
+
+// ---- forward A operand: input patches, K-contiguous ----
+template <typename T, bool XF>
+struct ConvFwdA {
+  static constexpr bool kKContig = true;
+  struct State { const T* base; int hi0, wi0; bool ok; };
+  ConvGeom g; const T* x; const float* sc; const float* sh;
+  __device__ State fixed(int m) const {
+    State s;
+    s.ok = m < g.M;
+    int mm = s.ok ? m : 0;
+    int n = fdiv(mm, g.fd_howo);
+    int r = mm - n * g.Ho * g.Wo;
+    int ho = fdiv(r, g.fd_wo);
+    int wo = r - ho * g.Wo;
+    s.base = x + (size_t)n * g.H * g.W * g.C;
+    s.hi0 = ho * g.S - g.P;
+    s.wi0 = wo * g.S - g.P;
+    return s;
+  }
+  __device__ uint4 load(const State& s, int k) const {
+    if (!s.ok || k >= g.K) return zero4();
+    int tap = fdiv(k, g.fd_c);
+    int ci = k - tap * g.C;
+    int kh = fdiv(tap, g.fd_kw);
+    int kw = tap - kh * g.KW;
+    int hi = s.hi0 + kh, wi = s.wi0 + kw;
+    if ((unsigned)hi >= (unsigned)g.H || (unsigned)wi >= (unsigned)g.W) return zero4();
+    uint4 v = ldg16(s.base + ((size_t)hi * g.W + wi) * g.C + ci);
+    if constexpr (XF) v = xform_chunk<T>(v, sc, sh, ci);
+    return v;
+  }
+};
+
+// ---- data-gradient A operand: output-gradient "patches", K-contiguous ----
+template <typename T>
+struct ConvDgradA {
+  static constexpr bool kKContig = true;
+  struct State { const T* base; int hp, wp; bool ok; };
+  ConvGeom g; const T* dy;
+  __device__ State fixed(int m) const {
+    State s;
+    s.ok = m < g.M;
+    int mm = s.ok ? m : 0;
+    int n = fdiv(mm, g.fd_hw);
+    int r = mm - n * g.H * g.W;
+    int h = fdiv(r, g.fd_w);
+    int w = r - h * g.W;
+    s.base = dy + (size_t)n * g.Ho * g.Wo * g.Co;
+    s.hp = h + g.P;
+    s.wp = w + g.P;
+    return s;
+  }
+  __device__ uint4 load(const State& s, int k) const {
+    if (!s.ok || k >= g.K) return zero4();
+    int tap = fdiv(k, g.fd_co);
+    int co = k - tap * g.Co;
+    int kh = fdiv(tap, g.fd_kw);
+    int kw = tap - kh * g.KW;
+    int th = s.hp - kh, tw = s.wp - kw;
+    if (th < 0 || tw < 0) return zero4();
+    int ho = th, wo = tw;
+    if (g.S != 1) {
+      if ((th % g.S) | (tw % g.S)) return zero4();
+      ho = th / g.S; wo = tw / g.S;
+    }
+    if (ho >= g.Ho || wo >= g.Wo) return zero4();
+    return ldg16(s.base + ((size_t)ho * g.Wo + wo) * g.Co + co);
+  }
+};
+
+// ---- weight-gradient B operand: input patches, MN-contiguous over (kh,kw,ci) ----
+template <typename T, bool XF>
+struct ConvWgradB {
+  static constexpr bool kKContig = false;
+  struct State { int kh, kw, ci; bool ok; };
+  ConvGeom g; const T* x; const float* sc; const float* sh; int Kcols;
+  __device__ State fixed(int col) const {
+    State s;
+    s.ok = col < Kcols;
+    int c = s.ok ? col : 0;
+    int tap = fdiv(c, g.fd_c);
+    s.ci = c - tap * g.C;
+    s.kh = fdiv(tap, g.fd_kw);
+    s.kw = tap - s.kh * g.KW;
+    return s;
+  }
+  __device__ uint4 load(const State& s, int m) const {
+    if (!s.ok || m >= g.M) return zero4();
+    int n = fdiv(m, g.fd_howo);
+    int r = m - n * g.Ho * g.Wo;
+    int ho = fdiv(r, g.fd_wo);
+    int wo = r - ho * g.Wo;
+    int hi = ho * g.S - g.P + s.kh, wi = wo * g.S - g.P + s.kw;
+    if ((unsigned)hi >= (unsigned)g.H || (unsigned)wi >= (unsigned)g.W) return zero4();
+    uint4 v = ldg16(x + (((size_t)n * g.H + hi) * g.W + wi) * g.C + s.ci);
+    if constexpr (XF) v = xform_chunk<T>(v, sc, sh, s.ci);
+    return v;
+  }
+};
+
+// ---- stem (7x7/2, 3 input channels) on a zero-padded NHWC4 image ----
+// Xp[n][Hp][Wp][4] with the 3-pixel top/left padding materialised; K layout
+// (kh:8, kw:8, c:4) = 256, of which kh<7, kw<7, c<3 carry weights.
+struct StemGeom {
+  int N, Ho, Wo, Hp, Wp, M;
+  FastDiv fd_howo, fd_wo;
+};
+template <typename T>
+struct StemA {
+  static constexpr bool kKContig = true;
+  struct State { const T* base; bool ok; };
+  StemGeom g; const T* xp;
+  __device__ State fixed(int m) const {
+    State s;
+    s.ok = m < g.M;
+    int mm = s.ok ? m : 0;
+    int n = fdiv(mm, g.fd_howo);
+    int r = mm - n * g.Ho * g.Wo;
+    int ho = fdiv(r, g.fd_wo);
+    int wo = r - ho * g.Wo;
+    s.base = xp + (((size_t)n * g.Hp + 2 * ho) * g.Wp + 2 * wo) * 4;
+    return s;
+  }
+  __device__ uint4 load(const State& s, int k) const {
+    int kh = k >> 5, kw = (k & 31) >> 2;
+    if (!s.ok || kh >= 7) return zero4();
+    return ldg16(s.base + ((size_t)kh * g.Wp + kw) * 4);
+  }
+};
+template <typename T>
+struct StemWgradB {
+  static constexpr bool kKContig = false;
+  struct State { int off; bool ok; };
+  StemGeom g; const T* xp;
+  __device__ State fixed(int col) const {
+    int kh = col >> 5, kw = (col & 31) >> 2;
+    return State{(kh * g.Wp + kw) * 4, kh < 7};
+  }
+  __device__ uint4 load(const State& s, int m) const {
+    if (!s.ok || m >= g.M) return zero4();
+    int n = fdiv(m, g.fd_howo);
+    int r = m - n * g.Ho * g.Wo;
+    int ho = fdiv(r, g.fd_wo);
+    int wo = r - ho * g.Wo;
+    return ldg16(xp + (((size_t)n * g.Hp + 2 * ho) * g.Wp + 2 * wo) * 4 + s.off);
+  }
+};
+
+// ---------------- epilogues ----------------
+// raw conv output + BN batch statistics (sum, sum of squares)
+template <typename T>
+struct EpiConvFwd {
+  static constexpr bool kStats = true;
+  double* stat1; double* stat2;
+  T* y; int Co;
+  __device__ void operator()(int row, int col, v4f v, v4f& s1, v4f& s2) const {
+    store4(y + (size_t)row * Co + col, v);
+    s1 = v;
+    s2 = v * v;
+  }
+};
+// data gradient through the producer's ReLU (mask from BN-applied y), plus
+// that BN's backward statistics: sum(g), sum(g * xhat).
+template <typename T>
+struct EpiDgradBN {
+  static constexpr bool kStats = true;
+  double* stat1; double* stat2;
+  T* g_out; int C;
+  const T* y; const float* sc; const float* sh; const float* mean; const float* invstd;
+  __device__ void operator()(int row, int col, v4f v, v4f& s1, v4f& s2) const {
+    v4f yv = load4(y + (size_t)row * C + col);
+    v4f sc4 = *reinterpret_cast<const v4f*>(sc + col);
+    v4f sh4 = *reinterpret_cast<const v4f*>(sh + col);
+    v4f mu = *reinterpret_cast<const v4f*>(mean + col);
+    v4f is = *reinterpret_cast<const v4f*>(invstd + col);
+    v4f g;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) g[j] = (fmaf(yv[j], sc4[j], sh4[j]) > 0.f) ? v[j] : 0.f;
+    store4(g_out + (size_t)row * C + col, g);
+    s1 = g;
+    s2 = g * ((yv - mu) * is);
+  }
+};
+// data gradient plus a residual-branch gradient
+template <typename T>
+struct EpiDgradAdd {
+  static constexpr bool kStats = false;
+  double* stat1 = nullptr; double* stat2 = nullptr;
+  T* dx; const T* addend; int C;
+  __device__ void operator()(int row, int col, v4f v, v4f&, v4f&) const {
+    size_t o = (size_t)row * C + col;
+    if (addend) v += load4(addend + o);
+    store4(dx + o, v);
+  }
+};
+
+// ---------------- tile-config dispatch ----------------
+template <typename T, class LA, class LB, class EP>
+static int gemm_auto(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
+                     hipStream_t st) {
+  if (N <= 64)
+    return launch_gemm<T, 256, 64, 4>(M, N, K, ksplit, la, lb, ep, st);
+  return launch_gemm<T, 128, 128, 2>(M, N, K, ksplit, la, lb, ep, st);
+}
+// weight-gradient GEMMs: rows = Co, cols = KH*KW*C, reduction = pixels
+template <typename T, class LA, class LB, class EP>
+static int gemm_wgrad(int M, int N, int K, const LA& la, const LB& lb, const EP& ep, hipStream_t st) {
+  int tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  int ksplit = (2048 + tiles - 1) / tiles;
+  int maxsplit = (K + 4095) / 4096;     // at least 4096 pixels per split
+  if (ksplit > maxsplit) ksplit = maxsplit;
+  if (M <= 64) {
+    tiles = (N + 255) / 256;
+    ksplit = (2048 + tiles - 1) / tiles;
+    if (ksplit > maxsplit) ksplit = maxsplit;
+    return launch_gemm<T, 64, 256, 1>(M, N, K, ksplit, la, lb, ep, st);
+  }
+  return launch_gemm<T, 128, 128, 2>(M, N, K, ksplit, la, lb, ep, st);
+}
+
+template <typename T>
+static int conv_fwd_t(const void* x, const void* wp, void* y, ConvGeom g, const float* sc,
+                      const float* sh, double* s1, double* s2, hipStream_t st) {
+  g.M = g.N * g.Ho * g.Wo;
+  g.K = g.KH * g.KW * g.C;
+  KMat<T> lb{(const T*)wp, g.K, g.Co, g.K};
+  EpiConvFwd<T> ep{s1, s2, (T*)y, g.Co};
+  if (sc) {
+    ConvFwdA<T, true> la{g, (const T*)x, sc, sh};
+    return gemm_auto<T>(g.M, g.Co, g.K, 1, la, lb, ep, st);
+  }
+  ConvFwdA<T, false> la{g, (const T*)x, nullptr, nullptr};
+  return gemm_auto<T>(g.M, g.Co, g.K, 1, la, lb, ep, st);
+}
+
+template <typename T>
+static int conv_dgrad_t(const void* dy, const void* wt, void* dx, ConvGeom g, const void* addend,
+                        const void* ybn, const float* sc, const float* sh, const float* mean,
+                        const float* invstd, double* s1, double* s2, hipStream_t st) {
+  g.M = g.N * g.H * g.W;
+  g.K = g.KH * g.KW * g.Co;
+  ConvDgradA<T> la{g, (const T*)dy};
+  KMat<T> lb{(const T*)wt, g.K, g.C, g.K};
+  if (ybn) {
+    EpiDgradBN<T> ep{s1, s2, (T*)dx, g.C, (const T*)ybn, sc, sh, mean, invstd};
+    return gemm_auto<T>(g.M, g.C, g.K, 1, la, lb, ep, st);
+  }
+  EpiDgradAdd<T> ep{nullptr, nullptr, (T*)dx, (const T*)addend, g.C};
+  return gemm_auto<T>(g.M, g.C, g.K, 1, la, lb, ep, st);
+}
+
+template <typename T>
+static int conv_wgrad_t(const void* dy, const void* x, float* dw, ConvGeom g, const float* sc,
+                        const float* sh, hipStream_t st) {
+  g.M = g.N * g.Ho * g.Wo;        // pixels (reduction)
+  g.K = g.KH * g.KW * g.C;        // columns
+  MNMat<T> la{(const T*)dy, g.Co, g.Co, g.M};
+  EpiAtomic ep{nullptr, nullptr, dw, g.K, 1.0f};
+  if (sc) {
+    ConvWgradB<T, true> lb{g, (const T*)x, sc, sh, g.K};
+    return gemm_wgrad<T>(g.Co, g.K, g.M, la, lb, ep, st);
+  }
+  ConvWgradB<T, false> lb{g, (const T*)x, nullptr, nullptr, g.K};
+  return gemm_wgrad<T>(g.Co, g.K, g.M, la, lb, ep, st);
+}
+
+static StemGeom make_stem(int N, int H, int W) {
+  StemGeom g;
+  g.N = N;
+  g.Ho = (H + 6 - 7) / 2 + 1;
+  g.Wo = (W + 6 - 7) / 2 + 1;
+  g.Hp = 2 * g.Ho + 6;
+  g.Wp = 2 * g.Wo + 6;
+  g.M = N * g.Ho * g.Wo;
+  g.fd_howo = make_fastdiv(g.Ho * g.Wo);
+  g.fd_wo = make_fastdiv(g.Wo);
+  return g;
+}
+
+// NCHW (3 ch, fp32) -> padded NHWC4 image of type T (interior only; the
+// caller zeroes the buffer once so the padding stays zero).
+template <typename T>
+__global__ void stem_prep_kernel(const float* __restrict__ x, T* __restrict__ xp, int N, int H, int W,
+                                 int Hp, int Wp) {
+  size_t total = (size_t)N * H * W;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    int w = (int)(i % W);
+    size_t t = i / W;
+    int h = (int)(t % H);
+    int n = (int)(t / H);
+    const float* src = x + (size_t)n * 3 * H * W + (size_t)h * W + w;
+    T* dst = xp + (((size_t)n * Hp + h + 3) * Wp + w + 3) * 4;
+    dst[0] = from_f<T>(src[0]);
+    dst[1] = from_f<T>(src[(size_t)H * W]);
+    dst[2] = from_f<T>(src[(size_t)2 * H * W]);
+    dst[3] = from_f<T>(0.f);
+  }
+}
+// 1-channel uint8 radiograph -> normalised, replicated padded NHWC4 image
+// (the on-device half of the pinned-uint8 collation path).
+template <typename T>
+__global__ void stem_prep_u8_kernel(const uint8_t* __restrict__ x, T* __restrict__ xp, int N, int H,
+                                    int W, int Hp, int Wp, float mean, float inv_std) {
+  size_t total = (size_t)N * H * W;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
+       i += (size_t)gridDim.x * blockDim.x) {
+    int w = (int)(i % W);
+    size_t t = i / W;
+    int h = (int)(t % H);
+    int n = (int)(t / H);
+    float v = ((float)x[i] - mean) * inv_std;
+    T* dst = xp + (((size_t)n * Hp + h + 3) * Wp + w + 3) * 4;
+    T tv = from_f<T>(v);
+    dst[0] = tv; dst[1] = tv; dst[2] = tv; dst[3] = from_f<T>(0.f);
+  }
+}
+
+}  // namespace vlp
+
+using namespace vlp;
+
+VLP_EXPORT int vlp_conv_fwd(int dtype, const void* x, const void* wp, void* y, int N, int H, int W,
+                            int C, int Co, int KH, int KW, int S, int P, const float* in_scale,
+                            const float* in_shift, double* stat_sum, double* stat_sumsq,
+                            void* stream) {
+  ConvGeom g = make_geom(N, H, W, C, Co, KH, KW, S, P);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == VLP_BF16)
+    return conv_fwd_t<bf16>(x, wp, y, g, in_scale, in_shift, stat_sum, stat_sumsq, st);
+  return conv_fwd_t<float>(x, wp, y, g, in_scale, in_shift, stat_sum, stat_sumsq, st);
+}
+
+VLP_EXPORT int vlp_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, int N, int H,
+                              int W, int C, int Co, int KH, int KW, int S, int P,
+                              const void* addend, const void* y_bn, const float* bn_scale,
+                              const float* bn_shift, const float* bn_mean,
+                              const float* bn_invstd, double* stat1, double* stat2,
+                              void* stream) {
+  ConvGeom g = make_geom(N, H, W, C, Co, KH, KW, S, P);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == VLP_BF16)
+    return conv_dgrad_t<bf16>(dy, wt, dx, g, addend, y_bn, bn_scale, bn_shift, bn_mean, bn_invstd,
+                              stat1, stat2, st);
+  return conv_dgrad_t<float>(dy, wt, dx, g, addend, y_bn, bn_scale, bn_shift, bn_mean, bn_invstd,
+                             stat1, stat2, st);
+}
+
+VLP_EXPORT int vlp_conv_wgrad(int dtype, const void* dy, const void* x, float* dw_ws, int N, int H,
+                              int W, int C, int Co, int KH, int KW, int S, int P,
+                              const float* in_scale, const float* in_shift, void* stream) {
+  ConvGeom g = make_geom(N, H, W, C, Co, KH, KW, S, P);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == VLP_BF16) return conv_wgrad_t<bf16>(dy, x, dw_ws, g, in_scale, in_shift, st);
+  return conv_wgrad_t<float>(dy, x, dw_ws, g, in_scale, in_shift, st);
+}
+
+VLP_EXPORT int vlp_stem_prep(int dtype, const float* x, void* xp, int N, int H, int W, void* stream) {
+  StemGeom g = make_stem(N, H, W);
+  hipStream_t st = (hipStream_t)stream;
+  size_t total = (size_t)N * H * W;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 65536) blocks = 65536;
+  if (dtype == VLP_BF16)
+    hipLaunchKernelGGL(stem_prep_kernel<bf16>, dim3(blocks), dim3(256), 0, st, x, (bf16*)xp, N, H, W, g.Hp, g.Wp);
+  else
+    hipLaunchKernelGGL(stem_prep_kernel<float>, dim3(blocks), dim3(256), 0, st, x, (float*)xp, N, H, W, g.Hp, g.Wp);
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_stem_prep_u8(int dtype, const uint8_t* x, void* xp, int N, int H, int W,
+                                float mean, float std, void* stream) {
+  StemGeom g = make_stem(N, H, W);
+  hipStream_t st = (hipStream_t)stream;
+  size_t total = (size_t)N * H * W;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 65536) blocks = 65536;
+  if (dtype == VLP_BF16)
+    hipLaunchKernelGGL(stem_prep_u8_kernel<bf16>, dim3(blocks), dim3(256), 0, st, x, (bf16*)xp, N, H, W, g.Hp, g.Wp, mean, 1.f / std);
+  else
+    hipLaunchKernelGGL(stem_prep_u8_kernel<float>, dim3(blocks), dim3(256), 0, st, x, (float*)xp, N, H, W, g.Hp, g.Wp, mean, 1.f / std);
+  return (int)hipGetLastError();
+}
+
+// Padded-image geometry for the host (so Python allocates the right buffer).
+VLP_EXPORT void vlp_stem_geom(int H, int W, int* Ho, int* Wo, int* Hp, int* Wp) {
+  StemGeom g = make_stem(1, H, W);
+  *Ho = g.Ho; *Wo = g.Wo; *Hp = g.Hp; *Wp = g.Wp;
+}
+
+VLP_EXPORT int vlp_stem_fwd(int dtype, const void* xp, const void* wp, void* y, int N, int H, int W,
+                            double* stat_sum, double* stat_sumsq, void* stream) {
+  StemGeom g = make_stem(N, H, W);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == VLP_BF16) {
+    StemA<bf16> la{g, (const bf16*)xp};
+    KMat<bf16> lb{(const bf16*)wp, 256, 64, 256};
+    EpiConvFwd<bf16> ep{stat_sum, stat_sumsq, (bf16*)y, 64};
+    return launch_gemm<bf16, 256, 64, 4>(g.M, 64, 256, 1, la, lb, ep, st);
+  }
+  StemA<float> la{g, (const float*)xp};
+  KMat<float> lb{(const float*)wp, 256, 64, 256};
+  EpiConvFwd<float> ep{stat_sum, stat_sumsq, (float*)y, 64};
+  return launch_gemm<float, 256, 64, 4>(g.M, 64, 256, 1, la, lb, ep, st);
+}
+
+// dW_ws[64][256] (kh:8, kw:8, c:4 layout), fp32, accumulated atomically.
+VLP_EXPORT int vlp_stem_wgrad(int dtype, const void* dy, const void* xp, float* dw_ws, int N, int H,
+                              int W, void* stream) {
+  StemGeom g = make_stem(N, H, W);
+  hipStream_t st = (hipStream_t)stream;
+  EpiAtomic ep{nullptr, nullptr, dw_ws, 256, 1.0f};
+  if (dtype == VLP_BF16) {
+    MNMat<bf16> la{(const bf16*)dy, 64, 64, g.M};
+    StemWgradB<bf16> lb{g, (const bf16*)xp};
+    return gemm_wgrad<bf16>(64, 224, g.M, la, lb, ep, st);
+  }
+  MNMat<float> la{(const float*)dy, 64, 64, g.M};
+  StemWgradB<float> lb{g, (const float*)xp};
+  return gemm_wgrad<float>(64, 224, g.M, la, lb, ep, st);
+}

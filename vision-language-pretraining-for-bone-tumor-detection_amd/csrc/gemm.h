@@ -1,0 +1,380 @@
+// MFMA GEMM engine for gfx950 (CDNA4), shared by every contraction on the
+// hot path: implicit-GEMM convolutions (fwd / dgrad / wgrad), TinyBERT linear
+// layers, and the CLIP projections.
+//
+//   C[m][n] = sum_k A(m, k) * B(n, k)
+//
+// A and B are supplied by *loader* functors that return 16-byte chunks
+// (8 bf16 / 4 fp32 values).  A loader is either
+//   K-contiguous  (kKContig = true):  chunk = A(m, k .. k+EPC-1)
+//   MN-contiguous (kKContig = false): chunk = A(m .. m+EPC-1, k)
+// so NHWC activations, torch [out][in] weights, and "transposed" operands
+// (wgrad / weight-gradient products) all stream with 16-B coalesced loads and
+// no explicit transpose pass.  Chunks are staged through a double-buffered,
+// XOR-swizzled LDS image; MN-contiguous bf16 images are read with the gfx950
+// ds_read_b64_tr_b16 transposing read.
+//
+// bf16: v_mfma_f32_16x16x32_bf16, BK = 64.  fp32 (parity mode):
+// v_mfma_f32_16x16x4_f32 (exact fp32 fma chain), BK = 32.  In both cases one
+// LDS row is 128 bytes, so the LDS geometry and swizzles are identical.
+//
+// The MFMA is issued "swapped" (MFMA-A = B tile, MFMA-B = A tile) so each lane
+// owns four consecutive output COLUMNS of one row: epilogues store 8/16-byte
+// vectors along the NHWC channel dimension.
+//
+// 4 waves (256 threads) per workgroup in a WGM x WGN wave grid; the grid is
+// remapped so that consecutive tile ids share an XCD (L2 reuse of the A panel).
+// Split-K over grid.y for reductions over pixels (weight gradients).
+#pragma once
+#include "common.h"
+
+namespace vlp {
+
+typedef __attribute__((address_space(3))) v4bf lds_v4bf;
+
+struct GemmShape {
+  int M, N, K;
+  int kchunk;   // K range per split (multiple of BK); == K rounded up when no split
+  int tiles_m, tiles_n;
+};
+
+// ---------------- LDS image addressing (bytes) ----------------
+// K-contig image: [rows][128 B]; 16-B chunk c of row r -> c ^ ((r>>1)&7).
+__device__ __forceinline__ int kc_off(int r, int c) {
+  return r * 128 + ((c ^ ((r >> 1) & 7)) << 4);
+}
+// MN-contig image: [k-rows][RB bytes]; 32-B blocks XOR-swizzled by k.
+template <int RB>
+__device__ __forceinline__ int mn_off(int k, int byte_in_row) {
+  const int sw = (RB >= 256) ? (k & 7) : ((k >> 1) & 3);
+  return k * RB + ((((byte_in_row >> 5) ^ sw) << 5) | (byte_in_row & 31));
+}
+
+template <typename T, int BM, bool KC>
+struct TileGeom {
+  static constexpr int EPC = Elem<T>::EPC;
+  static constexpr int BK = Elem<T>::BK;
+  static constexpr int BYTES = BM * 128;            // one stage of this operand
+  static constexpr int NCH = BYTES / 16 / 256;      // chunks per thread
+  static constexpr int RB = BM * (int)sizeof(T);    // MN image row bytes
+  static constexpr int CPR = RB / 16;               // MN chunks per k-row
+  static_assert(NCH >= 1, "tile too small");
+  static_assert(KC || (256 % CPR == 0), "MN tile geometry");
+};
+
+// Per-thread staging of one operand tile into registers and then LDS.
+template <typename T, int BM, class L>
+struct Stager {
+  using G = TileGeom<T, BM, L::kKContig>;
+  typename L::State st[L::kKContig ? G::NCH : 1];
+  uint4 r[G::NCH];
+
+  __device__ __forceinline__ void init(const L& ld, int row0) {
+    const int t = threadIdx.x;
+    if constexpr (L::kKContig) {
+#pragma unroll
+      for (int i = 0; i < G::NCH; ++i) st[i] = ld.fixed(row0 + (t >> 3) + 32 * i);
+    } else {
+      st[0] = ld.fixed(row0 + (t % G::CPR) * G::EPC);
+    }
+  }
+  __device__ __forceinline__ void load(const L& ld, int k0) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < G::NCH; ++i) {
+      if constexpr (L::kKContig) {
+        r[i] = ld.load(st[i], k0 + (t & 7) * G::EPC);
+      } else {
+        r[i] = ld.load(st[0], k0 + t / G::CPR + (256 / G::CPR) * i);
+      }
+    }
+  }
+  __device__ __forceinline__ void store(char* lds) const {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < G::NCH; ++i) {
+      int off;
+      if constexpr (L::kKContig) {
+        off = kc_off((t >> 3) + 32 * i, t & 7);
+      } else {
+        off = mn_off<G::RB>(t / G::CPR + (256 / G::CPR) * i, (t % G::CPR) * 16);
+      }
+      *reinterpret_cast<uint4*>(lds + off) = r[i];
+    }
+  }
+};
+
+// ---------------- fragment reads ----------------
+// bf16 fragment for MFMA 16x16x32, k-step s (0/1) within a BK=64 stage.
+// Lane l = 16g + i holds operand row (rb + i) at k in {32s+4g..+3} U {32s+16+4g..+3}
+// (a k-permutation shared by both operands, chosen so the reads are conflict-free).
+template <bool KC, int RB>
+__device__ __forceinline__ v8bf frag_bf16(const char* lds, int rb, int s) {
+  const int l = threadIdx.x & 63;
+  const int i = l & 15, g = l >> 4;
+  v4bf lo, hi;
+  if constexpr (KC) {
+    const int r = rb + i;
+    const int c1 = 4 * s + (g >> 1), c2 = 4 * s + 2 + (g >> 1);
+    lo = *reinterpret_cast<const v4bf*>(lds + kc_off(r, c1) + 8 * (g & 1));
+    hi = *reinterpret_cast<const v4bf*>(lds + kc_off(r, c2) + 8 * (g & 1));
+  } else {
+    const int q = i >> 2, p = i & 3;
+    const int k1 = 32 * s + 4 * g + q;
+    const int by = (rb + 4 * p) * 2;
+    lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(lds + mn_off<RB>(k1, by)));
+    hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(lds + mn_off<RB>(k1 + 16, by)));
+  }
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// fp32 fragment for 4 x MFMA 16x16x4f32 over a 16-k sub-step s (0/1) of BK=32.
+// Lane l = 16g + i holds row (rb + i) at k = 16s + 4g + j in element j (MFMA j).
+template <bool KC, int RB>
+__device__ __forceinline__ v4f frag_f32(const char* lds, int rb, int s) {
+  const int l = threadIdx.x & 63;
+  const int i = l & 15, g = l >> 4;
+  if constexpr (KC) {
+    return *reinterpret_cast<const v4f*>(lds + kc_off(rb + i, 4 * s + g));
+  } else {
+    v4f v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      v[j] = *reinterpret_cast<const float*>(lds + mn_off<RB>(16 * s + 4 * g + j, (rb + i) * 4));
+    return v;
+  }
+}
+
+// ---------------- the kernel ----------------
+// Epilogue contract:
+//   static constexpr bool kStats;  // accumulate two per-column sums
+//   __device__ void operator()(int row, int col, v4f v, v4f& s1, v4f& s2) const;
+//      called only for row < M (col < N, N % 4 == 0); s1/s2 start at 0.
+//   double* stat1, *stat2;          // per-column sums (only when kStats)
+template <typename T, int BM, int BN, int WGM, class LA, class LB, class EP>
+__global__ void __launch_bounds__(256)
+gemm_kernel(GemmShape sh, LA la, LB lb, EP ep) {
+  constexpr int WGN = 4 / WGM;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;   // wave tile
+  constexpr int MB = WTM / 16, NB = WTN / 16;
+  constexpr int BK = Elem<T>::BK;
+  using GA = TileGeom<T, BM, LA::kKContig>;
+  using GB = TileGeom<T, BN, LB::kKContig>;
+  constexpr int STAGE = GA::BYTES + GB::BYTES;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  // XCD-aware bijective remap of the tile id (consecutive ids -> same XCD).
+  const int nwg = sh.tiles_m * sh.tiles_n;
+  const int bid = blockIdx.x;
+  int wid = bid;
+  if (nwg >= 16) {
+    const int xcd = bid & 7, idx = bid >> 3, q = nwg >> 3, rr = nwg & 7;
+    wid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
+  }
+  const int tm = wid / sh.tiles_n, tn = wid - tm * sh.tiles_n;
+  const int row0 = tm * BM, col0 = tn * BN;
+
+  const int kb = blockIdx.y * sh.kchunk;
+  int ke = kb + sh.kchunk;
+  if (ke > sh.K) ke = sh.K;
+  const int nk = (ke - kb + BK - 1) / BK;
+
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave / WGN, wn = wave - wm * WGN;
+
+  Stager<T, BM, LA> sa;
+  Stager<T, BN, LB> sb;
+  sa.init(la, row0);
+  sb.init(lb, col0);
+
+  v4f acc[MB][NB];
+#pragma unroll
+  for (int a = 0; a < MB; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[a][b] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    sa.load(la, kb);
+    sb.load(lb, kb);
+    sa.store(smem);
+    sb.store(smem + GA::BYTES);
+  }
+  __syncthreads();
+
+  for (int t = 0; t < nk; ++t) {
+    const bool more = (t + 1) < nk;
+    if (more) {
+      sa.load(la, kb + (t + 1) * BK);
+      sb.load(lb, kb + (t + 1) * BK);
+    }
+    const char* ia = smem + (t & 1) * STAGE;
+    const char* ib = ia + GA::BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      if constexpr (sizeof(T) == 2) {
+        v8bf fa[MB], fb[NB];
+#pragma unroll
+        for (int a = 0; a < MB; ++a) fa[a] = frag_bf16<LA::kKContig, GA::RB>(ia, wm * WTM + a * 16, s);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) fb[b] = frag_bf16<LB::kKContig, GB::RB>(ib, wn * WTN + b * 16, s);
+#pragma unroll
+        for (int a = 0; a < MB; ++a)
+#pragma unroll
+          for (int b = 0; b < NB; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], acc[a][b], 0, 0, 0);
+      } else {
+        v4f fa[MB], fb[NB];
+#pragma unroll
+        for (int a = 0; a < MB; ++a) fa[a] = frag_f32<LA::kKContig, GA::RB>(ia, wm * WTM + a * 16, s);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) fb[b] = frag_f32<LB::kKContig, GB::RB>(ib, wn * WTN + b * 16, s);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int a = 0; a < MB; ++a)
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+              acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(fb[b][j], fa[a][j], acc[a][b], 0, 0, 0);
+      }
+    }
+    if (more) {
+      char* nxt = smem + ((t + 1) & 1) * STAGE;
+      sa.store(nxt);
+      sb.store(nxt + GA::BYTES);
+    }
+    __syncthreads();
+  }
+
+  // ---------------- epilogue ----------------
+  // lane l = 16g + i owns C[row = rbase + i][col = cbase + 4g .. 4g+3]
+  const int l = threadIdx.x & 63;
+  const int li = l & 15, lg = l >> 4;
+  v4f s1[NB], s2[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) { s1[b] = v4f{0.f, 0.f, 0.f, 0.f}; s2[b] = s1[b]; }
+#pragma unroll
+  for (int a = 0; a < MB; ++a) {
+    const int row = row0 + wm * WTM + a * 16 + li;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int col = col0 + wn * WTN + b * 16 + 4 * lg;
+      if (row < sh.M && col < sh.N) {
+        v4f c1 = v4f{0.f, 0.f, 0.f, 0.f}, c2 = c1;
+        ep(row, col, acc[a][b], c1, c2);
+        if constexpr (EP::kStats) { s1[b] += c1; s2[b] += c2; }
+      }
+    }
+  }
+  if constexpr (EP::kStats) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float x = s1[b][j], y = s2[b][j];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          x += __shfl_xor(x, o, 64);
+          y += __shfl_xor(y, o, 64);
+        }
+        s1[b][j] = x; s2[b][j] = y;
+      }
+      const int col = col0 + wn * WTN + b * 16 + 4 * lg;
+      if (li == 0 && col < sh.N) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          atomicAdd(ep.stat1 + col + j, (double)s1[b][j]);
+          atomicAdd(ep.stat2 + col + j, (double)s2[b][j]);
+        }
+      }
+    }
+  }
+}
+
+template <typename T, int BM, int BN>
+constexpr int gemm_lds_bytes() { return 2 * (BM + BN) * 128; }
+
+// Host-side launcher.  ksplit > 1 splits the reduction over grid.y (the
+// epilogue must then accumulate atomically).
+template <typename T, int BM, int BN, int WGM, class LA, class LB, class EP>
+inline int launch_gemm(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
+                       hipStream_t stream) {
+  constexpr int BK = Elem<T>::BK;
+  if (M <= 0 || N <= 0) return 0;
+  GemmShape sh;
+  sh.M = M; sh.N = N; sh.K = K;
+  sh.tiles_m = (M + BM - 1) / BM;
+  sh.tiles_n = (N + BN - 1) / BN;
+  if (ksplit < 1) ksplit = 1;
+  int kc = (K + ksplit - 1) / ksplit;
+  kc = ((kc + BK - 1) / BK) * BK;
+  if (kc < BK) kc = BK;
+  ksplit = (K + kc - 1) / kc;
+  if (ksplit < 1) ksplit = 1;
+  sh.kchunk = kc;
+  dim3 grid(sh.tiles_m * sh.tiles_n, ksplit, 1);
+  constexpr int lds = gemm_lds_bytes<T, BM, BN>();
+  if constexpr (lds > 65536) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)&gemm_kernel<T, BM, BN, WGM, LA, LB, EP>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      attr_set = true;
+    }
+  }
+  hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WGM, LA, LB, EP>), grid, dim3(256), lds, stream, sh, la, lb, ep);
+  return (int)hipGetLastError();
+}
+
+// ---------------- generic loaders ----------------
+// Row-major matrix, K contiguous: A(m,k) = p[m*ld + k].  Zero outside [M) x [K).
+template <typename T>
+struct KMat {
+  static constexpr bool kKContig = true;
+  struct State { const T* p; bool ok; };
+  const T* p; int ld, M, K;
+  __device__ State fixed(int m) const { return State{p + (size_t)m * ld, m < M}; }
+  __device__ uint4 load(const State& s, int k) const {
+    return (s.ok && k < K) ? ldg16(s.p + k) : zero4();
+  }
+};
+// MN contiguous: A(m,k) = p[k*ld + m].  Requires M % EPC == 0.
+template <typename T>
+struct MNMat {
+  static constexpr bool kKContig = false;
+  struct State { const T* p; bool ok; };
+  const T* p; int ld, M, K;
+  __device__ State fixed(int m) const { return State{p + m, m < M}; }
+  __device__ uint4 load(const State& s, int k) const {
+    return (s.ok && k < K) ? ldg16(s.p + (size_t)k * ld) : zero4();
+  }
+};
+
+// ---------------- generic epilogues ----------------
+// out[row*ldo + col] = alpha*v (+ bias[col]) (+ res[row*ldr+col]); optional GELU(erf).
+template <typename TO>
+struct EpiStore {
+  static constexpr bool kStats = false;
+  double* stat1 = nullptr; double* stat2 = nullptr;
+  TO* out; int ldo;
+  const float* bias;      // may be null
+  float alpha;
+  __device__ void operator()(int row, int col, v4f v, v4f&, v4f&) const {
+    v = v * alpha;
+    if (bias) v += *reinterpret_cast<const v4f*>(bias + col);
+    store4(out + (size_t)row * ldo + col, v);
+  }
+};
+// fp32 atomic accumulation (split-K / weight gradients)
+struct EpiAtomic {
+  static constexpr bool kStats = false;
+  double* stat1 = nullptr; double* stat2 = nullptr;
+  float* out; int ldo; float alpha;
+  __device__ void operator()(int row, int col, v4f v, v4f&, v4f&) const {
+    float* p = out + (size_t)row * ldo + col;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) atomicAdd(p + j, v[j] * alpha);
+  }
+};
+
+}  // namespace vlp

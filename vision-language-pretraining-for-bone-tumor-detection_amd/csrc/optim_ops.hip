@@ -1,0 +1,138 @@
+// Optimizer step and per-step weight packing.
+//
+// AdamW follows torch.optim.AdamW (reference optimizer: configs/optimizer/adamw.yaml,
+// built in VisionLanguageModule.configure_optimizers :130-184) element-for-element:
+//   p *= 1 - lr*wd;  m = b1 m + (1-b1) g;  v = b2 v + (1-b2) g^2
+//   p -= (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
+// over flat fp32 parameter / gradient / state arenas (one launch per group).
+//
+// Packing turns the fp32 master conv weights (timm [Co][C][KH][KW]) into the
+// GEMM operand layouts of conv_ops.hip, and the weight-gradient workspaces back.
+#include "common.h"
+
+namespace vlp {
+
+__global__ void adamw_kernel(size_t n, float* __restrict__ p, const float* __restrict__ g,
+                             float* __restrict__ m, float* __restrict__ v, float lr, float b1,
+                             float b2, float eps, float wd, float step_size, float bc2_sqrt) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    float pi = p[i] * (1.f - lr * wd);
+    float gi = g[i];
+    float mi = fmaf(1.f - b1, gi - m[i], m[i]);   // torch exp_avg.lerp_(grad, 1-beta1)
+    float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = pi - step_size * (mi / denom);
+  }
+}
+
+template <typename T>
+__global__ void pack_conv_kernel(int Co, int C, int KH, int KW, const float* __restrict__ w,
+                                 T* __restrict__ wp, T* __restrict__ wt) {
+  size_t total = (size_t)Co * C * KH * KW;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    int kw = (int)(i % KW);
+    size_t t = i / KW;
+    int kh = (int)(t % KH);
+    t /= KH;
+    int c = (int)(t % C);
+    int co = (int)(t / C);
+    T v = from_f<T>(w[i]);
+    if (wp) wp[(((size_t)co * KH + kh) * KW + kw) * C + c] = v;
+    if (wt) wt[(((size_t)c * KH + kh) * KW + kw) * Co + co] = v;
+  }
+}
+
+// stem [64][3][7][7] -> Wp[64][kh:8][kw:8][c:4] (zeros outside)
+template <typename T>
+__global__ void pack_stem_kernel(const float* __restrict__ w, T* __restrict__ wp) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 64 * 256) return;
+  int co = i >> 8, k = i & 255;
+  int kh = k >> 5, kw = (k >> 2) & 7, c = k & 3;
+  float v = 0.f;
+  if (kh < 7 && kw < 7 && c < 3) v = w[((co * 3 + c) * 7 + kh) * 7 + kw];
+  wp[i] = from_f<T>(v);
+}
+
+// ws[Co][KH][KW][C] -> g[Co][C][KH][KW]
+__global__ void unpack_conv_grad_kernel(int Co, int C, int KH, int KW, const float* __restrict__ ws,
+                                        float* __restrict__ g) {
+  size_t total = (size_t)Co * C * KH * KW;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    int kw = (int)(i % KW);
+    size_t t = i / KW;
+    int kh = (int)(t % KH);
+    t /= KH;
+    int c = (int)(t % C);
+    int co = (int)(t / C);
+    g[i] = ws[(((size_t)co * KH + kh) * KW + kw) * C + c];
+  }
+}
+
+__global__ void unpack_stem_grad_kernel(const float* __restrict__ ws, float* __restrict__ g) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 64 * 3 * 49) return;
+  int kw = i % 7, kh = (i / 7) % 7, c = (i / 49) % 3, co = i / 147;
+  g[i] = ws[co * 256 + kh * 32 + kw * 4 + c];
+}
+
+static inline int grid_for(size_t n) {
+  size_t b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace vlp
+
+using namespace vlp;
+
+// step_size = lr / (1 - beta1^t), bc2_sqrt = sqrt(1 - beta2^t), computed in fp64 on the host
+VLP_EXPORT int vlp_adamw(long long n, float* p, const float* g, float* m, float* v, float lr,
+                         float beta1, float beta2, float eps, float wd, float step_size,
+                         float bc2_sqrt, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (size_t)n, p, g,
+                     m, v, lr, beta1, beta2, eps, wd, step_size, bc2_sqrt);
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_pack_conv(int dtype, int Co, int C, int KH, int KW, const float* w, void* wp,
+                             void* wt, void* stream) {
+  size_t n = (size_t)Co * C * KH * KW;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == VLP_BF16)
+    hipLaunchKernelGGL(pack_conv_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, st, Co, C, KH, KW, w,
+                       (bf16*)wp, (bf16*)wt);
+  else
+    hipLaunchKernelGGL(pack_conv_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, Co, C, KH, KW, w,
+                       (float*)wp, (float*)wt);
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_pack_stem(int dtype, const float* w, void* wp, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == VLP_BF16)
+    hipLaunchKernelGGL(pack_stem_kernel<bf16>, dim3(64), dim3(256), 0, st, w, (bf16*)wp);
+  else
+    hipLaunchKernelGGL(pack_stem_kernel<float>, dim3(64), dim3(256), 0, st, w, (float*)wp);
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_unpack_conv_grad(int Co, int C, int KH, int KW, const float* ws, float* g,
+                                    void* stream) {
+  size_t n = (size_t)Co * C * KH * KW;
+  hipLaunchKernelGGL(unpack_conv_grad_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, Co,
+                     C, KH, KW, ws, g);
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_unpack_stem_grad(const float* ws, float* g, void* stream) {
+  hipLaunchKernelGGL(unpack_stem_grad_kernel, dim3((64 * 147 + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, ws, g);
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_abi_version() { return 1; }

@@ -1,0 +1,264 @@
+"""Tensor-level wrappers over the C ABI (libvlp_hip.so).
+
+PyTorch provides only device memory (caching allocator), the current stream,
+and zero-fills; every arithmetic operation below is a hand-written HIP kernel.
+All functions enqueue on torch's current stream and never synchronise.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._lib import BF16, F32, lib, ptr, stream_of
+
+
+def dcode(t: torch.Tensor) -> int:
+    if t.dtype == torch.bfloat16:
+        return BF16
+    if t.dtype == torch.float32:
+        return F32
+    raise TypeError(f"unsupported storage dtype {t.dtype}")
+
+
+def _s():
+    return stream_of()
+
+
+def conv_out_hw(H, W, KH, KW, S, P):
+    return (H + 2 * P - KH) // S + 1, (W + 2 * P - KW) // S + 1
+
+
+# ---------------- convolutions ----------------
+def conv_fwd(x, wp, Co, KH, KW, S, P, in_scale=None, in_shift=None, stat_sum=None, stat_sumsq=None,
+             out=None):
+    N, H, W, C = x.shape
+    Ho, Wo = conv_out_hw(H, W, KH, KW, S, P)
+    y = out if out is not None else torch.empty((N, Ho, Wo, Co), dtype=x.dtype, device=x.device)
+    if stat_sum is None:
+        stat_sum = torch.zeros(Co, dtype=torch.float64, device=x.device)
+        stat_sumsq = torch.zeros(Co, dtype=torch.float64, device=x.device)
+    lib().vlp_conv_fwd(dcode(x), ptr(x), ptr(wp), ptr(y), N, H, W, C, Co, KH, KW, S, P,
+                       ptr(in_scale), ptr(in_shift), ptr(stat_sum), ptr(stat_sumsq), _s())
+    return y
+
+
+def conv_dgrad(dy, wt, H, W, C, KH, KW, S, P, addend=None, y_bn=None, bn=None, stat1=None,
+               stat2=None, out=None):
+    """bn = (scale, shift, mean, invstd) of the BN+ReLU producing the conv input."""
+    N, Ho, Wo, Co = dy.shape
+    dx = out if out is not None else torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
+    sc = sh = mu = ist = None
+    if y_bn is not None:
+        sc, sh, mu, ist = bn
+    lib().vlp_conv_dgrad(dcode(dy), ptr(dy), ptr(wt), ptr(dx), N, H, W, C, Co, KH, KW, S, P,
+                         ptr(addend), ptr(y_bn), ptr(sc), ptr(sh), ptr(mu), ptr(ist), ptr(stat1),
+                         ptr(stat2), _s())
+    return dx
+
+
+def conv_wgrad(dy, x, KH, KW, S, P, dw_ws, in_scale=None, in_shift=None):
+    N, H, W, C = x.shape
+    Co = dy.shape[-1]
+    lib().vlp_conv_wgrad(dcode(dy), ptr(dy), ptr(x), ptr(dw_ws), N, H, W, C, Co, KH, KW, S, P,
+                         ptr(in_scale), ptr(in_shift), _s())
+    return dw_ws
+
+
+def stem_geom(H, W):
+    import ctypes
+    a, b, c, d = (ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int())
+    lib()._dll.vlp_stem_geom(H, W, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c),
+                             ctypes.byref(d))
+    return a.value, b.value, c.value, d.value
+
+
+def stem_prep(x_nchw, xp):
+    N, _, H, W = x_nchw.shape
+    lib().vlp_stem_prep(dcode(xp), ptr(x_nchw), ptr(xp), N, H, W, _s())
+
+
+def stem_prep_u8(x_u8, xp, mean, std):
+    N, H, W = x_u8.shape[0], x_u8.shape[-2], x_u8.shape[-1]
+    lib().vlp_stem_prep_u8(dcode(xp), ptr(x_u8), ptr(xp), N, H, W, float(mean), float(std), _s())
+
+
+def stem_fwd(xp, wp, N, H, W, y, stat_sum, stat_sumsq):
+    lib().vlp_stem_fwd(dcode(xp), ptr(xp), ptr(wp), ptr(y), N, H, W, ptr(stat_sum),
+                       ptr(stat_sumsq), _s())
+
+
+def stem_wgrad(dy, xp, N, H, W, dw_ws):
+    lib().vlp_stem_wgrad(dcode(dy), ptr(dy), ptr(xp), ptr(dw_ws), N, H, W, _s())
+
+
+# ---------------- BN / pooling ----------------
+def bn_finalize(count, s, ss, gamma, beta, eps, momentum, running_mean, running_var, scale, shift,
+                mean, invstd):
+    lib().vlp_bn_finalize(gamma.numel(), float(count), ptr(s), ptr(ss), ptr(gamma), ptr(beta),
+                          float(eps), float(momentum), ptr(running_mean), ptr(running_var),
+                          ptr(scale), ptr(shift), ptr(mean), ptr(invstd), _s())
+
+
+def bn_eval_coeffs(gamma, beta, rm, rv, eps, scale, shift):
+    lib().vlp_bn_eval_coeffs(gamma.numel(), ptr(gamma), ptr(beta), ptr(rm), ptr(rv), float(eps),
+                             ptr(scale), ptr(shift), _s())
+
+
+def bn_add_relu(y, sc, sh, idt, scd, shd, out):
+    C = y.shape[-1]
+    M = y.numel() // C
+    lib().vlp_bn_add_relu(dcode(y), M, C, ptr(y), ptr(sc), ptr(sh), ptr(idt), ptr(scd), ptr(shd),
+                          ptr(out), _s())
+
+
+def bn_bwd_reduce(M, C, dout, dbc, HW, mask, ya, mean_a, istd_a, yb, mean_b, istd_b, sum_g, sum_ga,
+                  sum_gb, dtype_ref):
+    lib().vlp_bn_bwd_reduce(dcode(dtype_ref), M, C, ptr(dout), ptr(dbc), HW, ptr(mask), ptr(ya),
+                            ptr(mean_a), ptr(istd_a), ptr(yb), ptr(mean_b), ptr(istd_b), ptr(sum_g),
+                            ptr(sum_ga), ptr(sum_gb), _s())
+
+
+def bn_bwd_apply(M, C, dout, dbc, HW, mask, A, B, g_out, dtype_ref):
+    """A/B = (y, mean, istd, gamma, sum_g, sum_gx, dy_out) or None."""
+    a = A if A is not None else (None,) * 7
+    b = B if B is not None else (None,) * 7
+    lib().vlp_bn_bwd_apply(dcode(dtype_ref), M, C, ptr(dout), ptr(dbc), HW, ptr(mask),
+                           *[ptr(t) for t in a], *[ptr(t) for t in b], ptr(g_out), _s())
+
+
+def bn_param_grad(sum_g, sum_gx, dgamma, dbeta):
+    lib().vlp_bn_param_grad(dgamma.numel(), ptr(sum_g), ptr(sum_gx), ptr(dgamma), ptr(dbeta), _s())
+
+
+def maxpool_fwd(y, sc, sh, out, idx):
+    N, H, W, C = y.shape
+    lib().vlp_maxpool_fwd(dcode(y), N, H, W, C, ptr(y), ptr(sc), ptr(sh), ptr(out), ptr(idx), _s())
+
+
+def maxpool_bwd(dp, idx, y, sc, sh, mean, istd, g_out, sum_g, sum_gx):
+    N, H, W, C = y.shape
+    lib().vlp_maxpool_bwd(dcode(y), N, H, W, C, ptr(dp), ptr(idx), ptr(y), ptr(sc), ptr(sh),
+                          ptr(mean), ptr(istd), ptr(g_out), ptr(sum_g), ptr(sum_gx), _s())
+
+
+def avgpool_fwd(x, feat):
+    N, H, W, C = x.shape
+    lib().vlp_avgpool_fwd(dcode(x), N, H * W, C, ptr(x), ptr(feat), _s())
+
+
+# ---------------- text tower ----------------
+def linear_fwd(x, w, bias, y, M, N, K, ldx=None, ldy=None, mode=0, aux=None, res=None, ldr=None,
+               p=0.0, seed=0):
+    lib().vlp_linear_fwd(dcode(x), M, N, K, ptr(x), ldx or K, ptr(w), ptr(bias), ptr(y), ldy or N,
+                         mode, ptr(aux), ptr(res), ldr or N, float(p), int(seed), _s())
+
+
+def linear_dgrad(dy, w, dx, M, Kin, Nout, lddy=None, lddx=None, mode=0, aux=None, ldaux=None,
+                 addend=None, ldad=None):
+    lib().vlp_linear_dgrad(dcode(dy), M, Kin, Nout, ptr(dy), lddy or Nout, ptr(w), ptr(dx),
+                           lddx or Kin, mode, ptr(aux), ldaux or Kin, ptr(addend), ldad or Kin, _s())
+
+
+def linear_wgrad(dy, x, dw, M, Nout, Kin, lddy=None, ldx=None):
+    lib().vlp_linear_wgrad(dcode(dy), M, Nout, Kin, ptr(dy), lddy or Nout, ptr(x), ldx or Kin,
+                           ptr(dw), _s())
+
+
+def colsum(x, out, M, N, ld=None):
+    lib().vlp_colsum(dcode(x), M, N, ptr(x), ld or N, ptr(out), _s())
+
+
+def layernorm_fwd(x, gamma, beta, eps, y, mean, rstd, M, D, p=0.0, seed=0):
+    lib().vlp_layernorm_fwd(dcode(x), M, D, ptr(x), ptr(gamma), ptr(beta), float(eps), ptr(y),
+                            ptr(mean), ptr(rstd), float(p), int(seed), _s())
+
+
+def layernorm_bwd(dy, x, mean, rstd, gamma, dx, dxd, dgamma, dbeta, M, D, p_out=0.0, seed_out=0,
+                  p_in=0.0, seed_in=0):
+    lib().vlp_layernorm_bwd(dcode(dy), M, D, ptr(dy), float(p_out), int(seed_out), ptr(x),
+                            ptr(mean), ptr(rstd), ptr(gamma), ptr(dx), ptr(dxd), float(p_in),
+                            int(seed_in), ptr(dgamma), ptr(dbeta), _s())
+
+
+def attn_fwd(qkv, amask, ctx, P, B, T, H, dh, scale, p=0.0, seed=0):
+    lib().vlp_attn_fwd(dcode(qkv), B, T, H, dh, ptr(qkv), ptr(amask), ptr(ctx), ptr(P),
+                       float(scale), float(p), int(seed), _s())
+
+
+def attn_bwd(qkv, P, dctx, dqkv, B, T, H, dh, scale, p=0.0, seed=0):
+    lib().vlp_attn_bwd(dcode(qkv), B, T, H, dh, ptr(qkv), ptr(P), ptr(dctx), ptr(dqkv),
+                       float(scale), float(p), int(seed), _s())
+
+
+def embed_fwd(ids, tt, wemb, pemb, temb, e_out, M, T, D):
+    lib().vlp_embed_fwd(dcode(e_out), M, T, D, ptr(ids), ptr(tt), ptr(wemb), ptr(pemb), ptr(temb),
+                        ptr(e_out), _s())
+
+
+def embed_bwd(ids, tt, de, dwemb, dpemb, dtemb, M, T, D):
+    lib().vlp_embed_bwd(dcode(de), M, T, D, ptr(ids), ptr(tt), ptr(de), ptr(dwemb), ptr(dpemb),
+                        ptr(dtemb), _s())
+
+
+def scatter_rows(src, dst, R, D, ldi, ldo):
+    lib().vlp_scatter_rows(dcode(src), R, D, ptr(src), ldi, ptr(dst), ldo, _s())
+
+
+# ---------------- head ----------------
+def l2norm_fwd(x, y, norm):
+    R, E = x.shape
+    lib().vlp_l2norm_fwd(R, E, ptr(x), ptr(y), ptr(norm), _s())
+
+
+def l2norm_bwd(y, norm, dy, dx=None, dx_t=None):
+    R, E = y.shape
+    code = dcode(dx_t) if dx_t is not None else F32
+    lib().vlp_l2norm_bwd(code, R, E, ptr(y), ptr(norm), ptr(dy), ptr(dx), ptr(dx_t), _s())
+
+
+def clip_loss_fused(B, N, E, offset, img_all, txt_all, logit_scale, g_img_all, g_txt_all, d_ls,
+                    loss_parts, lse_out=None):
+    lib().vlp_clip_loss_fused(B, N, E, offset, ptr(img_all), ptr(txt_all), ptr(logit_scale),
+                              ptr(g_img_all), ptr(g_txt_all), ptr(d_ls), ptr(loss_parts),
+                              ptr(lse_out), _s())
+
+
+def ce_sym(logits, out, dlogits=None):
+    lib().vlp_ce_sym(logits.shape[0], ptr(logits), ptr(out), ptr(dlogits), _s())
+
+
+def matmul(A, B, C, M, N, K, lda, a_kc, ldb, b_kc, ldc, alpha=1.0, accumulate=False, dtype_ref=None):
+    ref = dtype_ref if dtype_ref is not None else A
+    out_f32 = 1 if C.dtype == torch.float32 else 0
+    lib().vlp_matmul(dcode(ref), M, N, K, ptr(A), lda, int(a_kc), ptr(B), ldb, int(b_kc), ptr(C),
+                     ldc, out_f32, float(alpha), int(accumulate), _s())
+
+
+def cast(x, y):
+    lib().vlp_cast(dcode(y), x.numel(), ptr(x), ptr(y), _s())
+
+
+# ---------------- optimizer / packing ----------------
+def adamw(p, g, m, v, lr, beta1, beta2, eps, wd, step):
+    bc1 = 1.0 - beta1 ** step
+    bc2 = 1.0 - beta2 ** step
+    lib().vlp_adamw(p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), float(lr), float(beta1),
+                    float(beta2), float(eps), float(wd), float(lr / bc1), float(bc2 ** 0.5), _s())
+
+
+def pack_conv(w, wp, wt):
+    Co, C, KH, KW = w.shape
+    ref = wp if wp is not None else wt
+    lib().vlp_pack_conv(dcode(ref), Co, C, KH, KW, ptr(w), ptr(wp), ptr(wt), _s())
+
+
+def pack_stem(w, wp):
+    lib().vlp_pack_stem(dcode(wp), ptr(w), ptr(wp), _s())
+
+
+def unpack_conv_grad(ws, g):
+    Co, C, KH, KW = g.shape
+    lib().vlp_unpack_conv_grad(Co, C, KH, KW, ptr(ws), ptr(g), _s())
+
+
+def unpack_stem_grad(ws, g):
+    lib().vlp_unpack_stem_grad(ptr(ws), ptr(g), _s())
