@@ -142,8 +142,13 @@ int vlp_scatter_rows(int dtype, int R, int D, const void* in, int ldi, void* out
 /* ---------------- contrastive head ----------------
  * Replace forward (:441-461) and _compute_loss (:532-554). */
 int vlp_l2norm_fwd(int R, int E, const float* x, float* y, float* norm, void* stream);
+/* dx = gscale[0] * d normalize(x) (gscale may be NULL = 1); optional compute-dtype copy */
 int vlp_l2norm_bwd(int dtype, int R, int E, const float* y, const float* norm, const float* dy,
-                   float* dx, void* dx_t, void* stream);
+                   const float* gscale, float* dx, void* dx_t, void* stream);
+/* y = x * s[0] (+ y if accumulate); s may be NULL (= 1) */
+int vlp_scale(int n, const float* x, const float* s, float* y, int accumulate, void* stream);
+/* out[3] = {(parts0 + parts1) / (2N), parts0 / N, parts1 / N} */
+int vlp_clip_loss_finish(const float* parts, int N, float* out, void* stream);
 /* Fused global-batch symmetric InfoNCE, forward + backward.  img_all/txt_all:
  * [N][E] gathered normalised embeddings; this rank owns rows [offset, offset+B).
  * g_img_all/g_txt_all (+=, zero first): d loss / d embeddings for all N rows;

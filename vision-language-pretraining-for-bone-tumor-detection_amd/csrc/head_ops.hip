@@ -184,17 +184,19 @@ __global__ void l2norm_fwd_kernel(int R, int E, const float* __restrict__ x, flo
 // dx = (dy - y * <y, dy>) / n   (n > eps),   dy / eps otherwise; optional T copy
 template <typename T>
 __global__ void l2norm_bwd_kernel(int R, int E, const float* __restrict__ y, const float* __restrict__ norm,
-                                  const float* __restrict__ dy, float* __restrict__ dx, T* __restrict__ dxT) {
+                                  const float* __restrict__ dy, const float* __restrict__ gscale,
+                                  float* __restrict__ dx, T* __restrict__ dxT) {
   int r = blockIdx.x * 4 + (threadIdx.x >> 6);
   int l = threadIdx.x & 63;
   if (r >= R) return;
+  const float gs = gscale ? gscale[0] : 1.f;
   float n = norm[r];
   float dot = 0.f;
   for (int d = l; d < E; d += 64) dot += y[(size_t)r * E + d] * dy[(size_t)r * E + d];
   dot = warp_sum(dot);
   for (int d = l; d < E; d += 64) {
     float g = dy[(size_t)r * E + d];
-    float v = n > 1e-12f ? (g - y[(size_t)r * E + d] * dot) / n : g / 1e-12f;
+    float v = gs * (n > 1e-12f ? (g - y[(size_t)r * E + d] * dot) / n : g / 1e-12f);
     if (dx) dx[(size_t)r * E + d] = v;
     if (dxT) dxT[(size_t)r * E + d] = from_f<T>(v);
   }
@@ -230,6 +232,22 @@ __global__ void ce_sym_kernel(int B, const float* __restrict__ logits, float* __
   }
 }
 
+// y[i] = x[i] * s[0] (+ y[i] if accumulate)
+__global__ void scale_kernel(int n, const float* __restrict__ x, const float* __restrict__ s,
+                             float* __restrict__ y, int accumulate) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = (accumulate ? y[i] : 0.f) + x[i] * (s ? s[0] : 1.f);
+}
+
+// loss outputs from the fused kernel's parts: out = {(p0+p1)/(2N), p0/N, p1/N}
+__global__ void clip_loss_finish_kernel(const float* parts, float inv_n, float* out) {
+  if (threadIdx.x == 0) {
+    out[0] = 0.5f * (parts[0] + parts[1]) * inv_n;
+    out[1] = parts[0] * inv_n;
+    out[2] = parts[1] * inv_n;
+  }
+}
+
 template <typename T>
 __global__ void cast_kernel(size_t n, const float* __restrict__ x, T* __restrict__ y) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
@@ -259,14 +277,28 @@ VLP_EXPORT int vlp_l2norm_fwd(int R, int E, const float* x, float* y, float* nor
 }
 
 VLP_EXPORT int vlp_l2norm_bwd(int dtype, int R, int E, const float* y, const float* norm,
-                              const float* dy, float* dx, void* dxT, void* stream) {
+                              const float* dy, const float* gscale, float* dx, void* dxT,
+                              void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (dtype == VLP_BF16)
     hipLaunchKernelGGL(l2norm_bwd_kernel<bf16>, dim3((R + 3) / 4), dim3(256), 0, st, R, E, y, norm, dy,
-                       dx, (bf16*)dxT);
+                       gscale, dx, (bf16*)dxT);
   else
     hipLaunchKernelGGL(l2norm_bwd_kernel<float>, dim3((R + 3) / 4), dim3(256), 0, st, R, E, y, norm,
-                       dy, dx, (float*)dxT);
+                       dy, gscale, dx, (float*)dxT);
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_scale(int n, const float* x, const float* s, float* y, int accumulate,
+                         void* stream) {
+  hipLaunchKernelGGL(scale_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, n, x, s, y,
+                     accumulate);
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_clip_loss_finish(const float* parts, int N, float* out, void* stream) {
+  hipLaunchKernelGGL(clip_loss_finish_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, parts,
+                     1.f / (float)N, out);
   return (int)hipGetLastError();
 }
 

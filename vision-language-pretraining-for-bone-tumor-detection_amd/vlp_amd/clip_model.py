@@ -1,0 +1,151 @@
+"""CLIP-style model assembled from the HIP towers and the fused contrastive head.
+
+Mirrors VisionLanguageModule's compute (src/models/pretrain/VisionLanguageModule.py):
+  __init__ :98-111   image/text projections ~ N(0, dim^-1/2), logit_scale = ln(1/0.07)
+  forward  :441-461  normalize(f @ P), s = min(exp(logit_scale), 100), logits = s * img @ txt^T
+  _compute_loss :532-554  symmetric cross-entropy over the batch
+
+Two entry points:
+  * `ClipStepFn` — the training hot path: image tower + text tower + projections
+    + L2-norm + (data-parallel all-gather) + fused loss/gradient kernel as ONE
+    autograd node, so `loss.backward()` runs the explicit HIP backward of the
+    whole model and hands autograd views of the flat gradient arenas.
+  * `embeddings()/logits()` — the API path used by `forward(batch)`: returns
+    logits/embeddings with autograd support through `EmbedFn`/`LogitsFn`.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from . import dist as vdist
+from . import ops
+from .arena import ArenaModule
+
+
+class ClipHead(ArenaModule):
+    def __init__(self, image_dim=512, text_dim=312, embedding_dim=256, compute_dtype="bf16",
+                 device=None):
+        super().__init__()
+        self.image_dim, self.text_dim, self.embedding_dim = image_dim, text_dim, embedding_dim
+        self.compute_dtype = compute_dtype
+        self._init_arena([("image_projection", (image_dim, embedding_dim)),
+                          ("text_projection", (text_dim, embedding_dim)),
+                          ("logit_scale", (1,))], device=device)
+        self._ws = {}
+        self.reset_parameters()
+
+    @torch.no_grad()
+    def reset_parameters(self):
+        nn.init.normal_(self.arena.view("image_projection"), std=self.image_dim ** -0.5)   # :105
+        nn.init.normal_(self.arena.view("text_projection"), std=self.text_dim ** -0.5)     # :109
+        self.arena.view("logit_scale").fill_(math.log(1 / 0.07))                           # :111
+
+    def _after_apply(self):
+        self._ws = {}
+
+    @property
+    def tdtype(self):
+        return torch.bfloat16 if self.compute_dtype == "bf16" else torch.float32
+
+    def wcopy(self):
+        if self.compute_dtype == "fp32":
+            return self.arena.data
+        buf = self._ws.get("wT")
+        if buf is None:
+            buf = torch.empty(self.arena.numel, dtype=self.tdtype, device=self.arena.data.device)
+            self._ws["wT"] = buf
+        ops.cast(self.arena.data, buf)
+        return buf
+
+
+def _project_normalize(head, wT, feat, ld, dim, proj_name, E):
+    """emb = normalize(feat @ P) (fp32 out); feat rows with leading dim `ld`."""
+    B = feat.shape[0] if ld == dim else feat.numel() // ld
+    raw = torch.empty(B, E, dtype=torch.float32, device=feat.device)
+    P = head.arena.view(proj_name, wT)
+    # C[b][e] = sum_i feat[b][i] P[i][e]: A = feat (K-contig), B(n=e, k=i) = P[i][e] (MN-contig)
+    ops.matmul(feat, P, raw, B, E, dim, ld, 1, E, 0, E, dtype_ref=feat)
+    emb = torch.empty_like(raw)
+    norm = torch.empty(B, dtype=torch.float32, device=feat.device)
+    ops.l2norm_fwd(raw, emb, norm)
+    return emb, norm
+
+
+def _project_backward(head, wT, feat, ld, dim, proj_name, E, emb, norm, g_emb, gscale):
+    """Returns d feat [B, dim] (compute dtype); writes d P into the head grad arena."""
+    B = emb.shape[0]
+    T = head.tdtype
+    draw = torch.empty(B, E, dtype=torch.float32, device=emb.device)
+    draw_t = draw if T == torch.float32 else torch.empty(B, E, dtype=T, device=emb.device)
+    ops.l2norm_bwd(emb, norm, g_emb, draw, None if T == torch.float32 else draw_t, gscale=gscale)
+    P = head.arena.view(proj_name, wT)
+    # dP[i][e] = sum_b feat[b][i] draw[b][e]: A(m=i,k=b) = feat[b][i] (MN), B(n=e,k=b) = draw[b][e] (MN)
+    ops.matmul(feat, draw_t, head.arena.gview(proj_name), dim, E, B, ld, 0, E, 0, E, dtype_ref=feat)
+    # dfeat[b][i] = sum_e draw[b][e] P[i][e]: A = draw (K-contig), B(n=i,k=e) = P[i][e] (K-contig)
+    dfeat = torch.empty(B, dim, dtype=T, device=emb.device)
+    ops.matmul(draw_t, P, dfeat, B, dim, E, E, 1, E, 1, dim, dtype_ref=draw_t)
+    return dfeat
+
+
+class ClipStepFn(torch.autograd.Function):
+    """loss, image_loss, text_loss, img_emb, txt_emb = f(batch; all parameters)."""
+
+    @staticmethod
+    def forward(ctx, model, x, x_u8, input_ids, attention_mask, token_type_ids, *params):
+        img_t, txt_t, head = model.image_tower, model.text_tower, model.head
+        training = model.training
+        feat_img, sv_img = img_t.run_forward(x, training, x_u8=x_u8)
+        h_last, sv_txt = txt_t.run_forward(input_ids, attention_mask, token_type_ids, training)
+        B, Tn = input_ids.shape
+        D, E = txt_t.cfg.hidden, head.embedding_dim
+        wT = head.wcopy()
+        ie, inorm = _project_normalize(head, wT, feat_img, 512, 512, "image_projection", E)
+        te, tnorm = _project_normalize(head, wT, h_last, Tn * D, D, "text_projection", E)
+        rank, world = vdist.world()
+        ie_all = vdist.all_gather_rows(ie)
+        te_all = vdist.all_gather_rows(te)
+        N = B * world
+        dev = ie.device
+        g_img_all = torch.zeros(N, E, dtype=torch.float32, device=dev)
+        g_txt_all = torch.zeros(N, E, dtype=torch.float32, device=dev)
+        small = torch.zeros(4, dtype=torch.float32, device=dev)   # parts[2], d_logit_scale
+        ls = head.arena.view("logit_scale")
+        ops.clip_loss_fused(B, N, E, rank * B, ie_all, te_all, ls, g_img_all, g_txt_all, small[2:3],
+                            small[0:2])
+        vdist.all_reduce_sum_(small[0:2])  # global loss terms (the gradient needs no collective)
+        out = torch.empty(3, dtype=torch.float32, device=dev)
+        ops.clip_loss_finish(small[0:2], N, out)
+        ctx.model = model
+        ctx.state = (sv_img, sv_txt, wT, feat_img, h_last, ie, inorm, te, tnorm, g_img_all, g_txt_all,
+                     small, B, Tn, D, E)
+        ctx.mark_non_differentiable(ie, te)
+        return out[0], out[1], out[2], ie, te
+
+    @staticmethod
+    def backward(ctx, dloss, dli, dlt, die, dte):
+        model = ctx.model
+        img_t, txt_t, head = model.image_tower, model.text_tower, model.head
+        (sv_img, sv_txt, wT, feat_img, h_last, ie, inorm, te, tnorm, g_img_all, g_txt_all, small,
+         B, Tn, D, E) = ctx.state
+        ctx.state = None
+        g_img = vdist.reduce_scatter_rows(g_img_all)
+        g_txt = vdist.reduce_scatter_rows(g_txt_all)
+        gs = dloss.reshape(1).float().contiguous()
+        head.arena.grad.zero_()
+        ops.scale(small[2:3], gs, head.arena.gview("logit_scale"))
+        dfeat_img = _project_backward(head, wT, feat_img, 512, 512, "image_projection", E, ie, inorm,
+                                      g_img, gs)
+        dcls = _project_backward(head, wT, h_last, Tn * D, D, "text_projection", E, te, tnorm,
+                                 g_txt, gs)
+        img_t.run_backward(sv_img, dfeat_img)
+        txt_t.run_backward(sv_txt, dcls)
+        grads = (head.grads_for_autograd() + img_t.grads_for_autograd() + txt_t.grads_for_autograd())
+        return (None, None, None, None, None, None, *grads)
+
+
+def model_params(model):
+    return (model.head.params_in_arena_order() + model.image_tower.params_in_arena_order()
+            + model.text_tower.params_in_arena_order())

@@ -209,10 +209,19 @@ def l2norm_fwd(x, y, norm):
     lib().vlp_l2norm_fwd(R, E, ptr(x), ptr(y), ptr(norm), _s())
 
 
-def l2norm_bwd(y, norm, dy, dx=None, dx_t=None):
+def l2norm_bwd(y, norm, dy, dx=None, dx_t=None, gscale=None):
     R, E = y.shape
     code = dcode(dx_t) if dx_t is not None else F32
-    lib().vlp_l2norm_bwd(code, R, E, ptr(y), ptr(norm), ptr(dy), ptr(dx), ptr(dx_t), _s())
+    lib().vlp_l2norm_bwd(code, R, E, ptr(y), ptr(norm), ptr(dy), ptr(gscale), ptr(dx), ptr(dx_t),
+                         _s())
+
+
+def scale(x, s, y, accumulate=False):
+    lib().vlp_scale(x.numel(), ptr(x), ptr(s), ptr(y), int(accumulate), _s())
+
+
+def clip_loss_finish(parts, N, out):
+    lib().vlp_clip_loss_finish(ptr(parts), int(N), ptr(out), _s())
 
 
 def clip_loss_fused(B, N, E, offset, img_all, txt_all, logit_scale, g_img_all, g_txt_all, d_ls,

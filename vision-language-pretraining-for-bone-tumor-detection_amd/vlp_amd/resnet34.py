@@ -1,0 +1,416 @@
+"""ResNet34 image tower on the HIP kernels (drop-in for the timm model created
+at src/models/pretrain/VisionLanguageModule.py:30-32 with num_classes=0,
+global_pool="avg").
+
+State-dict keys are timm's (conv1, bn1, layerX.Y.{conv1,bn1,conv2,bn2,
+downsample.0,downsample.1}, BN running_mean/var/num_batches_tracked), so
+checkpoints load into timm `resnet34` and the reference's finetuning modules
+(OnlyImagingModule.py:76-80, FusionModule.py:92-96) unchanged.
+
+Execution (train mode, per BasicBlock):
+  y1 = conv1(x)                       [+ BN1 batch stats in the epilogue]
+  y2 = conv2(relu(bn1(y1)))           [BN1+ReLU applied on load; + BN2 stats]
+  yd = downsample.0(x)                [+ BNd stats]            (first block of layers 2-4)
+  out = relu(bn2(y2) + (x | bnd(yd)))  one streaming pass
+Backward (explicit, no autograd inside the tower):
+  R   : sum(g), sum(g*xhat2) [, sum(g*xhatd)] with g = dout*(out>0)
+  E   : dy2 = BN2'(g), dyd = BNd'(g) | g passed on as identity gradient
+  conv2 dgrad -> g1 = (.)*(bn1(y1)>0) + BN1 backward sums in the epilogue
+  conv2 wgrad on relu(bn1(y1)) recomputed on load
+  E1  : dy1 = BN1'(g1);  conv1 dgrad (+ identity / downsample gradient) -> dout of the previous block
+Stem: conv 7x7/2 on a padded NHWC4 image, BN+ReLU+maxpool in one pass that
+records the argmax tap; backward routes through the argmax, applies the ReLU
+mask and accumulates BN sums in one pass.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .arena import ArenaModule
+
+LAYERS = (3, 4, 6, 3)
+WIDTHS = (64, 128, 256, 512)
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+
+
+class _Holder(nn.Module):
+    """Parameter/buffer container mirroring one timm submodule (no forward)."""
+
+
+class _Conv:
+    def __init__(self, key, Co, C, KH, KW, S, P):
+        self.key, self.Co, self.C, self.KH, self.KW, self.S, self.P = key, Co, C, KH, KW, S, P
+        self.numel = Co * C * KH * KW
+
+
+class _BN:
+    def __init__(self, key, C, holder):
+        self.key, self.C, self.holder = key, C, holder
+
+
+def _tower_specs():
+    convs, bns = [], []
+    convs.append(_Conv("conv1", 64, 3, 7, 7, 2, 3))
+    bns.append(("bn1", 64))
+    inpl = 64
+    for li, (n, planes) in enumerate(zip(LAYERS, WIDTHS)):
+        for b in range(n):
+            s = (1 if li == 0 else 2) if b == 0 else 1
+            pre = f"layer{li + 1}.{b}"
+            convs.append(_Conv(pre + ".conv1", planes, inpl, 3, 3, s, 1))
+            bns.append((pre + ".bn1", planes))
+            convs.append(_Conv(pre + ".conv2", planes, planes, 3, 3, 1, 1))
+            bns.append((pre + ".bn2", planes))
+            if b == 0 and (s != 1 or inpl != planes):
+                convs.append(_Conv(pre + ".downsample.0", planes, inpl, 1, 1, s, 0))
+                bns.append((pre + ".downsample.1", planes))
+            inpl = planes
+    return convs, bns
+
+
+class ResNet34Tower(ArenaModule):
+    num_features = 512
+
+    def __init__(self, drop_rate: float = 0.0, compute_dtype: str = "bf16", device=None):
+        super().__init__()
+        self.drop_rate = float(drop_rate)
+        self.compute_dtype = compute_dtype
+        convs, bns = _tower_specs()
+        self._convs = {c.key: c for c in convs}
+        specs = []
+        for c in convs:
+            specs.append((c.key + ".weight", (c.Co, c.C, c.KH, c.KW)))
+        for key, C in bns:
+            specs.append((key + ".weight", (C,)))
+            specs.append((key + ".bias", (C,)))
+        # arena order = timm order would interleave; keep convs then BN (order is internal)
+        self._init_arena(specs, device=device)
+        # module tree with timm names (registration order = timm state_dict order)
+        self._bns = {}
+        bn_c = dict(bns)
+
+        def mk_conv(parent, attr, key):
+            h = _Holder()
+            setattr(parent, attr, h)
+            self._register(h, "weight", key + ".weight")
+
+        def mk_bn(parent, attr, key):
+            h = _Holder()
+            setattr(parent, attr, h)
+            self._register(h, "weight", key + ".weight")
+            self._register(h, "bias", key + ".bias")
+            C = bn_c[key]
+            h.register_buffer("running_mean", torch.zeros(C, device=device))
+            h.register_buffer("running_var", torch.ones(C, device=device))
+            h.register_buffer("num_batches_tracked", torch.zeros((), dtype=torch.long, device=device))
+            self._bns[key] = _BN(key, C, h)
+
+        mk_conv(self, "conv1", "conv1")
+        mk_bn(self, "bn1", "bn1")
+        inpl = 64
+        for li, (n, planes) in enumerate(zip(LAYERS, WIDTHS)):
+            layer = nn.Sequential()
+            for b in range(n):
+                s = (1 if li == 0 else 2) if b == 0 else 1
+                pre = f"layer{li + 1}.{b}"
+                blk = _Holder()
+                mk_conv(blk, "conv1", pre + ".conv1")
+                mk_bn(blk, "bn1", pre + ".bn1")
+                mk_conv(blk, "conv2", pre + ".conv2")
+                mk_bn(blk, "bn2", pre + ".bn2")
+                if b == 0 and (s != 1 or inpl != planes):
+                    ds = nn.Sequential()
+                    mk_conv(ds, "0", pre + ".downsample.0")
+                    mk_bn(ds, "1", pre + ".downsample.1")
+                    blk.downsample = ds
+                layer.add_module(str(b), blk)
+                inpl = planes
+            setattr(self, f"layer{li + 1}", layer)
+        self._blocks = []
+        for li, n in enumerate(LAYERS):
+            for b in range(n):
+                pre = f"layer{li + 1}.{b}"
+                self._blocks.append((pre, (pre + ".downsample.0") in self._convs))
+        self.reset_parameters()
+        self._ws = {}  # per-device workspaces (packed weights, wgrad buffers, BN coefficients)
+
+    # ---------------- init (timm ResNet.init_weights) ----------------
+    @torch.no_grad()
+    def reset_parameters(self, zero_init_last: bool = True):
+        for c in self._convs.values():
+            nn.init.kaiming_normal_(self.arena.view(c.key + ".weight"), mode="fan_out",
+                                    nonlinearity="relu")
+        for key in self._bns:
+            self.arena.view(key + ".weight").fill_(1.0)
+            self.arena.view(key + ".bias").zero_()
+        if zero_init_last:
+            for pre, _ in self._blocks:
+                self.arena.view(pre + ".bn2.weight").zero_()
+
+    def _after_apply(self):
+        self._ws = {}
+
+    @property
+    def tdtype(self):
+        return torch.bfloat16 if self.compute_dtype == "bf16" else torch.float32
+
+    # ---------------- workspaces ----------------
+    def _workspace(self):
+        dev = self.arena.data.device
+        key = (str(dev), self.compute_dtype)
+        ws = self._ws.get(key)
+        if ws is not None:
+            return ws
+        T = self.tdtype
+        ws = {}
+        for c in self._convs.values():
+            if c.key == "conv1":
+                ws["conv1.wp"] = torch.empty(64, 256, dtype=T, device=dev)
+            else:
+                ws[c.key + ".wp"] = torch.empty(c.Co, c.KH, c.KW, c.C, dtype=T, device=dev)
+                ws[c.key + ".wt"] = torch.empty(c.C, c.KH, c.KW, c.Co, dtype=T, device=dev)
+        # wgrad workspaces (fp32, GEMM layout), one flat buffer zeroed per backward
+        off = 0
+        self._wg_off = {}
+        for c in self._convs.values():
+            n = 64 * 256 if c.key == "conv1" else c.numel
+            self._wg_off[c.key] = (off, n)
+            off += (n + 63) // 64 * 64
+        ws["wgrad"] = torch.zeros(off, dtype=torch.float32, device=dev)
+        # per-BN coefficient and statistic slices
+        nb = len(self._bns)
+        Cmax = 512
+        ws["coef"] = torch.zeros(nb, 4, Cmax, dtype=torch.float32, device=dev)   # scale, shift, mean, istd
+        ws["fstat"] = torch.zeros(nb, 2, Cmax, dtype=torch.float64, device=dev)  # sum, sumsq
+        ws["bstat"] = torch.zeros(nb, 2, Cmax, dtype=torch.float64, device=dev)  # sum_g, sum_gx
+        self._bn_idx = {k: i for i, k in enumerate(self._bns)}
+        self._ws[key] = ws
+        return ws
+
+    def _coef(self, ws, key):
+        i, C = self._bn_idx[key], self._bns[key].C
+        c = ws["coef"][i]
+        return c[0, :C], c[1, :C], c[2, :C], c[3, :C]
+
+    def _fstat(self, ws, key):
+        i, C = self._bn_idx[key], self._bns[key].C
+        return ws["fstat"][i, 0, :C], ws["fstat"][i, 1, :C]
+
+    def _bstat(self, ws, key):
+        i, C = self._bn_idx[key], self._bns[key].C
+        return ws["bstat"][i, 0, :C], ws["bstat"][i, 1, :C]
+
+    def pack_weights(self):
+        """fp32 master (timm layout) -> GEMM operand layouts in the compute dtype."""
+        ws = self._workspace()
+        for c in self._convs.values():
+            w = self.arena.view(c.key + ".weight")
+            if c.key == "conv1":
+                ops.pack_stem(w, ws["conv1.wp"])
+            else:
+                ops.pack_conv(w, ws[c.key + ".wp"], ws[c.key + ".wt"])
+        return ws
+
+    # ---------------- BN helpers ----------------
+    def _bn_finalize(self, ws, key, count, training):
+        bn = self._bns[key]
+        gamma, beta = self.arena.view(key + ".weight"), self.arena.view(key + ".bias")
+        sc, sh, mu, ist = self._coef(ws, key)
+        h = bn.holder
+        if training:
+            s, ss = self._fstat(ws, key)
+            ops.bn_finalize(count, s, ss, gamma, beta, BN_EPS, BN_MOMENTUM, h.running_mean,
+                            h.running_var, sc, sh, mu, ist)
+            h.num_batches_tracked.add_(1)
+        else:
+            ops.bn_eval_coeffs(gamma, beta, h.running_mean, h.running_var, BN_EPS, sc, sh)
+        return sc, sh
+
+    # ---------------- forward ----------------
+    def run_forward(self, x: Optional[torch.Tensor], training: bool, x_u8: Optional[torch.Tensor] = None,
+                    u8_norm=(127.5, 73.9)):
+        """x: [N,3,H,W] fp32 NCHW (reference batch["x-ray"]) or x_u8: [N,1,H,W] uint8.
+        Returns (features [N,512] in the compute dtype, saved-state dict)."""
+        ws = self.pack_weights()
+        T = self.tdtype
+        dev = self.arena.data.device
+        src = x if x is not None else x_u8
+        N, H, W = src.shape[0], src.shape[-2], src.shape[-1]
+        Ho, Wo, Hp, Wp = ops.stem_geom(H, W)
+        xp_key = ("xp", N, H, W)
+        xp = ws.get(xp_key)
+        if xp is None:
+            xp = torch.zeros(N, Hp, Wp, 4, dtype=T, device=dev)  # padding stays zero
+            ws[xp_key] = xp
+        if x is not None:
+            ops.stem_prep(x.contiguous(), xp)
+        else:
+            ops.stem_prep_u8(x_u8.contiguous(), xp, u8_norm[0], u8_norm[1])
+        ws["fstat"].zero_()
+        saved = {"N": N, "H": H, "W": W, "xp": xp, "training": training}
+        # stem
+        y0 = torch.empty(N, Ho, Wo, 64, dtype=T, device=dev)
+        s, ss = self._fstat(ws, "bn1")
+        ops.stem_fwd(xp, ws["conv1.wp"], N, H, W, y0, s, ss)
+        sc0, sh0 = self._bn_finalize(ws, "bn1", N * Ho * Wo, training)
+        Hq, Wq = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
+        p = torch.empty(N, Hq, Wq, 64, dtype=T, device=dev)
+        idx = torch.empty(N, Hq, Wq, 64, dtype=torch.uint8, device=dev)
+        ops.maxpool_fwd(y0, sc0, sh0, p, idx)
+        saved["y0"], saved["idx"] = y0, idx
+        xcur = p
+        blocks = []
+        for pre, has_ds in self._blocks:
+            c1, c2 = self._convs[pre + ".conv1"], self._convs[pre + ".conv2"]
+            s, ss = self._fstat(ws, pre + ".bn1")
+            y1 = ops.conv_fwd(xcur, ws[c1.key + ".wp"], c1.Co, 3, 3, c1.S, 1, stat_sum=s, stat_sumsq=ss)
+            Mb = y1.numel() // y1.shape[-1]
+            sc1, sh1 = self._bn_finalize(ws, pre + ".bn1", Mb, training)
+            s, ss = self._fstat(ws, pre + ".bn2")
+            y2 = ops.conv_fwd(y1, ws[c2.key + ".wp"], c2.Co, 3, 3, 1, 1, sc1, sh1, s, ss)
+            sc2, sh2 = self._bn_finalize(ws, pre + ".bn2", Mb, training)
+            yd = scd = shd = None
+            if has_ds:
+                cd = self._convs[pre + ".downsample.0"]
+                s, ss = self._fstat(ws, pre + ".downsample.1")
+                yd = ops.conv_fwd(xcur, ws[cd.key + ".wp"], cd.Co, 1, 1, cd.S, 0, stat_sum=s,
+                                  stat_sumsq=ss)
+                scd, shd = self._bn_finalize(ws, pre + ".downsample.1", Mb, training)
+            out = torch.empty_like(y2)
+            ops.bn_add_relu(y2, sc2, sh2, yd if has_ds else xcur, scd, shd, out)
+            blocks.append({"x": xcur, "y1": y1, "y2": y2, "yd": yd, "out": out})
+            xcur = out
+        feat = torch.empty(N, 512, dtype=T, device=dev)
+        ops.avgpool_fwd(xcur, feat)
+        saved["blocks"] = blocks
+        return feat, saved
+
+    # ---------------- backward ----------------
+    def run_backward(self, saved, dfeat: torch.Tensor):
+        """dfeat: [N,512] fp32 gradient of the pooled features.  Writes every
+        parameter gradient into the grad arena (overwriting)."""
+        ws = self._workspace()
+        T = self.tdtype
+        dev = self.arena.data.device
+        ws["bstat"].zero_()
+        ws["wgrad"].zero_()
+        dfeat = dfeat.float().contiguous()
+        blocks = saved["blocks"]
+        dout = None
+        for bi in range(len(self._blocks) - 1, -1, -1):
+            pre, has_ds = self._blocks[bi]
+            B = blocks[bi]
+            x, y1, y2, yd, out = B["x"], B["y1"], B["y2"], B["yd"], B["out"]
+            N, Hh, Ww, C = out.shape
+            Cin = x.shape[-1]
+            M = N * Hh * Ww
+            last = dout is None
+            dbc = dfeat if last else None
+            HW = Hh * Ww
+            c1, c2 = self._convs[pre + ".conv1"], self._convs[pre + ".conv2"]
+            k1, k2 = pre + ".bn1", pre + ".bn2"
+            _, _, mu2, is2 = self._coef(ws, k2)
+            sg2, sgx2 = self._bstat(ws, k2)
+            mud = isd = sgxd = None
+            if has_ds:
+                kd = pre + ".downsample.1"
+                _, _, mud, isd = self._coef(ws, kd)
+                sgd, sgxd = self._bstat(ws, kd)
+            ops.bn_bwd_reduce(M, C, dout, dbc, HW, out, y2, mu2, is2, yd, mud, isd, sg2, sgx2, sgxd, out)
+            ops.bn_param_grad(sg2, sgx2, self.arena.gview(k2 + ".weight"), self.arena.gview(k2 + ".bias"))
+            dy2 = torch.empty_like(y2)
+            A = (y2, mu2, is2, self.arena.view(k2 + ".weight"), sg2, sgx2, dy2)
+            Bside, g_id = None, None
+            if has_ds:
+                dyd = torch.empty_like(yd)
+                Bside = (yd, mud, isd, self.arena.view(kd + ".weight"), sg2, sgxd, dyd)
+                ops.bn_param_grad(sg2, sgxd, self.arena.gview(kd + ".weight"), self.arena.gview(kd + ".bias"))
+            else:
+                g_id = torch.empty_like(out)
+            ops.bn_bwd_apply(M, C, dout, dbc, HW, out, A, Bside, g_id, out)
+            # conv2: dgrad through relu(bn1(y1)) with BN1 backward sums; wgrad on relu(bn1(y1))
+            sc1, sh1, mu1, is1 = self._coef(ws, k1)
+            sg1, sgx1 = self._bstat(ws, k1)
+            g1 = ops.conv_dgrad(dy2, ws[c2.key + ".wt"], Hh, Ww, C, 3, 3, 1, 1, y_bn=y1,
+                                bn=(sc1, sh1, mu1, is1), stat1=sg1, stat2=sgx1)
+            self._wgrad(ws, c2, dy2, y1, sc1, sh1)
+            ops.bn_param_grad(sg1, sgx1, self.arena.gview(k1 + ".weight"), self.arena.gview(k1 + ".bias"))
+            dy1 = torch.empty_like(y1)
+            ops.bn_bwd_apply(M, C, g1, None, 1, None,
+                             (y1, mu1, is1, self.arena.view(k1 + ".weight"), sg1, sgx1, dy1), None, None, y1)
+            Hi, Wi = x.shape[1], x.shape[2]
+            addend = g_id
+            if has_ds:
+                cd = self._convs[pre + ".downsample.0"]
+                addend = ops.conv_dgrad(dyd, ws[cd.key + ".wt"], Hi, Wi, Cin, 1, 1, cd.S, 0)
+                self._wgrad(ws, cd, dyd, x)
+            dx = ops.conv_dgrad(dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, addend=addend)
+            self._wgrad(ws, c1, dy1, x)
+            dout = dx
+        # stem: maxpool -> relu -> bn1 -> conv1
+        y0, idx = saved["y0"], saved["idx"]
+        sc0, sh0, mu0, is0 = self._coef(ws, "bn1")
+        sg0, sgx0 = self._bstat(ws, "bn1")
+        g0 = torch.empty_like(y0)
+        ops.maxpool_bwd(dout, idx, y0, sc0, sh0, mu0, is0, g0, sg0, sgx0)
+        ops.bn_param_grad(sg0, sgx0, self.arena.gview("bn1.weight"), self.arena.gview("bn1.bias"))
+        dy0 = torch.empty_like(y0)
+        M0 = y0.numel() // 64
+        ops.bn_bwd_apply(M0, 64, g0, None, 1, None,
+                         (y0, mu0, is0, self.arena.view("bn1.weight"), sg0, sgx0, dy0), None, None, y0)
+        o, n = self._wg_off["conv1"]
+        wsb = ws["wgrad"][o:o + n]
+        ops.stem_wgrad(dy0, saved["xp"], saved["N"], saved["H"], saved["W"], wsb)
+        ops.unpack_stem_grad(wsb, self.arena.gview("conv1.weight"))
+
+    def _wgrad(self, ws, c, dy, x, sc=None, sh=None):
+        o, n = self._wg_off[c.key]
+        buf = ws["wgrad"][o:o + n]
+        ops.conv_wgrad(dy, x, c.KH, c.KW, c.S, c.P, buf, sc, sh)
+        ops.unpack_conv_grad(buf, self.arena.gview(c.key + ".weight"))
+
+    # ---------------- autograd entry ----------------
+    def forward(self, x):
+        """API forward: [N,3,H,W] float -> [N,512] fp32 features (timm semantics)."""
+        feat = ImageTowerFn.apply(self, x, *self.params_in_arena_order())
+        if self.drop_rate > 0.0 and self.training:
+            feat = DropoutFn.apply(feat, self.drop_rate)
+        return feat
+
+
+class ImageTowerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, tower: ResNet34Tower, x, *params):
+        feat, saved = tower.run_forward(x, tower.training)
+        ctx.tower = tower
+        ctx.saved = saved if torch.is_grad_enabled() or True else None
+        return feat.float()
+
+    @staticmethod
+    def backward(ctx, dfeat):
+        tower = ctx.tower
+        tower.run_backward(ctx.saved, dfeat)
+        ctx.saved = None
+        return (None, None, *tower.grads_for_autograd())
+
+
+class DropoutFn(torch.autograd.Function):
+    """Feature dropout of timm's head (drop_rate); mask from the HIP hash RNG is
+    not needed here: this runs on a [N,512] tensor, via the linear-fwd dropout
+    epilogue would be overkill, so it uses a precomputed keep-mask."""
+
+    @staticmethod
+    def forward(ctx, x, p):
+        keep = (torch.rand_like(x) >= p).to(x.dtype) / (1.0 - p)
+        ctx.save_for_backward(keep)
+        return x * keep
+
+    @staticmethod
+    def backward(ctx, g):
+        (keep,) = ctx.saved_tensors
+        return g * keep, None
