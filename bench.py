@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""Benchmark: image-text pairs/s of the full CLIP pretraining step
+(ResNet34 + TinyBERT forward + backward + fused global-batch InfoNCE + AdamW)
+at bs=256/GPU, 512x512, T=40, bf16 (BASELINE.json configs[1]; configs[2] for
+--gpus 8 via torch.distributed.run).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+
+One process per GPU (RCCL over xGMI for N > 1), W untimed warm-up steps, then
+exactly K timed steps bracketed by barrier + synchronize; the max over ranks is
+reported.  Inputs (the reference batch layout: x-ray [B,3,H,W] fp32, caption
+ids/masks [B,T] int64) are resident in HBM before timing starts.
+
+The JSON line also carries
+  roofline     : the dominant kernel (by total time) timed with HIP events on
+                 its launch stream during the timed steps; achieved = its
+                 algorithmic FLOPs / its summed launch duration
+  cpu_baseline : the CPU oracle (timm-layout ResNet34 + HF BertModel + the
+                 reference head/loss + torch AdamW, fp32) on this host's cores,
+                 on a bounded sample (rank 0, N=1 only)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "vision-language-pretraining-for-bone-tumor-detection_amd")
+for p in (ROOT, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_F32_TFLOPS = 157.3
+FLOP_PER_PAIR_512 = 114.72e9  # ResNet34 113.60 + TinyBERT 1.117 + head
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--image-size", type=int, default=512)
+    ap.add_argument("--seq-len", type=int, default=40)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-batch", type=int, default=4)
+    ap.add_argument("--cpu-sample-steps", type=int, default=3)
+    ap.add_argument("--roofline-kernel", default="auto")
+    ap.add_argument("--kernel-report", default="")
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws > 1:
+        lr = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(lr)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", lr))
+        return dist.get_rank(), ws, lr
+    torch.cuda.set_device(0)
+    return 0, 1, 0
+
+
+def make_batch(B, H, T, device, seed):
+    from tests.golden.synth import synth_batch
+    b = synth_batch(B, H, T, seed)
+    return {"x-ray": b["x-ray"].to(device), "label": b["label"].to(device), "caption": b["caption"],
+            "caption_tokenized": {k: v.to(device) for k, v in b["caption_tokenized"].items()}}
+
+
+def cpu_baseline(args):
+    """Oracle (reference CPU fp32 path, restated) on a bounded sample."""
+    from oracle import weights as W
+    from oracle.clip import OracleVLP, compute_loss
+    from tests.golden.synth import synth_batch
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    B, H, T = args.cpu_sample_batch, args.image_size, args.seq_len
+    model = OracleVLP(128, text_dropout=0.1)
+    W.apply_recipe(model, 0)
+    model.train()
+    opt = torch.optim.AdamW(model.param_groups(), lr=5e-5)
+    batch = synth_batch(B, H, T, 0)
+    times = []
+    for i in range(args.cpu_sample_steps + 1):
+        t0 = time.perf_counter()
+        opt.zero_grad()
+        lg, _, _ = model(batch)
+        loss = compute_loss(lg)[0]
+        loss.backward()
+        opt.step()
+        if i > 0:
+            times.append(time.perf_counter() - t0)
+    times.sort()
+    med = times[len(times) // 2]
+    return {"value": round(B / med, 3), "unit": "image-text pairs/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle fp32 CPU step (fwd+bwd+AdamW), bs={B}, {H}x{H}, T={T}, "
+                      f"median of {len(times)} steps after 1 warm-up ({med:.2f} s/step)"}
+
+
+def main():
+    args = parse()
+    rank, world, local = setup_dist(args)
+    from src.models.pretrain.VisionLanguageModule import VisionLanguageModule
+    from vlp_amd import ktimer
+    import functools
+
+    dev = torch.device("cuda", local)
+    torch.manual_seed(1234 + rank)
+    model = VisionLanguageModule("resnet34", "tinybert", functools.partial(torch.optim.AdamW, lr=5e-5),
+                                 False, False, 512, 312, 128, compute_dtype=args.dtype, device=dev)
+    model.train()
+    opt = model.configure_optimizers()["optimizer"]
+    from vlp_amd.dist import GradReducer
+    reducer = GradReducer()
+    arenas = [model._head.arena, model.image_encoder.model.arena, model.text_encoder.model.arena]
+    batch = make_batch(args.batch, args.image_size, args.seq_len, dev, seed=rank)
+
+    def step():
+        opt.zero_grad()
+        loss = model.training_step(batch)
+        loss.backward()
+        reducer.reduce(arenas)
+        reducer.wait()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # select the dominant kernel family to time (by total time in one step)
+    tk = args.roofline_kernel
+    if tk == "auto":
+        ktimer.enable(None)
+        step()
+        torch.cuda.synchronize()
+        totals = ktimer.totals()
+        ktimer.disable()
+        tk = max(totals, key=lambda k: totals[k][0]) if totals else None
+        if args.kernel_report and rank == 0:
+            with open(args.kernel_report, "w") as f:
+                json.dump({k: {"ms": v[0], "launches": v[1], "gflop": v[2] / 1e9}
+                           for k, v in sorted(totals.items(), key=lambda kv: -kv[1][0])}, f, indent=1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ktimer.enable(tk)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    ktimer.disable()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    el = elapsed.item()
+    tot = ktimer.totals().get(tk, (0.0, 0, 0.0))
+    ms_k, nl, flop_k = tot
+    if rank == 0:
+        pairs = world * args.batch * args.steps
+        value = pairs / el
+        peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
+        achieved = (flop_k / (ms_k / 1e3)) / 1e12 if ms_k > 0 else 0.0
+        res = {
+            "metric": "image-text pairs/sec (fwd+bwd) at bs=256/GPU, 1/2/4/8 MI355X",
+            "value": round(value, 2),
+            "unit": "image-text pairs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (seeded uint8 radiographs normalised to 3-ch fp32, seeded token ids; random-init weights)",
+            "config": {"workload": "ResNet34+TinyBERT CLIP pretrain step (fwd+bwd+global-batch InfoNCE+AdamW)",
+                       "global_batch": world * args.batch, "per_gpu_batch": args.batch,
+                       "image_size": args.image_size, "seq_len": args.seq_len,
+                       "parallelism": f"dp{world}"},
+            "model_flops_frac": round(value * FLOP_PER_PAIR_512 * (args.image_size / 512) ** 2 / (world * peak * 1e12), 4)
+            if args.image_size == 512 else None,
+            "roofline": {"bound": "mfma", "kernel": tk, "achieved": round(achieved, 2), "peak": peak,
+                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                         "avg_launch_us": round(ms_k * 1e3 / max(nl, 1), 2), "launches": nl,
+                         "traffic": None},
+            "loss": round(loss.item(), 5),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -44,7 +44,8 @@ int vlp_abi_version(void);
  * sum / sum of squares of y into stat_sum / stat_sumsq (fp64, zeroed by caller). */
 int vlp_conv_fwd(int dtype, const void* x, const void* wp, void* y, int N, int H, int W, int C,
                  int Co, int KH, int KW, int S, int P, const float* in_scale,
-                 const float* in_shift, double* stat_sum, double* stat_sumsq, void* stream);
+                 const float* in_shift, double* stat_sum, double* stat_sumsq, int stat_rep,
+                 void* stream);
 /* dx[N][H][W][C] = conv^T(dy, w).  If y_bn != NULL: dx := dx * (bn_scale*y_bn +
  * bn_shift > 0) (ReLU mask of the producing BN+ReLU) and stat1 += sum(dx),
  * stat2 += sum(dx * (y_bn - bn_mean) * bn_invstd); else if addend != NULL:
@@ -52,7 +53,8 @@ int vlp_conv_fwd(int dtype, const void* x, const void* wp, void* y, int N, int H
 int vlp_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, int N, int H, int W, int C,
                    int Co, int KH, int KW, int S, int P, const void* addend, const void* y_bn,
                    const float* bn_scale, const float* bn_shift, const float* bn_mean,
-                   const float* bn_invstd, double* stat1, double* stat2, void* stream);
+                   const float* bn_invstd, double* stat1, double* stat2, int stat_rep,
+                   void* stream);
 /* dw_ws[Co][KH][KW][C] += sum over pixels dy x_patch (fp32 atomics; zero first).
  * Optional BN+ReLU-on-load of x as in vlp_conv_fwd. */
 int vlp_conv_wgrad(int dtype, const void* dy, const void* x, float* dw_ws, int N, int H, int W,
@@ -66,11 +68,17 @@ int vlp_stem_prep(int dtype, const float* x_nchw, void* xp, int N, int H, int W,
 int vlp_stem_prep_u8(int dtype, const uint8_t* x_u8, void* xp, int N, int H, int W, float mean,
                      float std, void* stream);
 int vlp_stem_fwd(int dtype, const void* xp, const void* wp, void* y, int N, int H, int W,
-                 double* stat_sum, double* stat_sumsq, void* stream);
+                 double* stat_sum, double* stat_sumsq, int stat_rep, void* stream);
 int vlp_stem_wgrad(int dtype, const void* dy, const void* xp, float* dw_ws, int N, int H, int W,
                    void* stream);
 
-/* ---------------- image tower: BatchNorm / residual / pooling ---------------- */
+/* ---------------- image tower: BatchNorm / residual / pooling ----------------
+ * Per-channel statistic outputs (fp64) are REPLICATED: a producer called with
+ * stat_rep = R adds into R copies laid out [R][C] (copy = workgroup % R) so
+ * that ~1e5 workgroups do not serialise on C addresses; vlp_stat_reduce folds
+ * them into copy 0, which is what every consumer reads.  stat_rep = 1 means a
+ * plain [C] buffer. */
+int vlp_stat_reduce(int rep, int C, double* a, double* b, double* c, void* stream);
 int vlp_bn_finalize(int C, double count, const double* sum, const double* sumsq,
                     const float* gamma, const float* beta, float eps, float momentum,
                     float* running_mean, float* running_var, float* scale, float* shift,
@@ -86,7 +94,7 @@ int vlp_bn_add_relu(int dtype, long long M, int C, const void* y, const float* s
 int vlp_bn_bwd_reduce(int dtype, long long M, int C, const void* dout, const float* dbc, int HW,
                       const void* mask, const void* ya, const float* mean_a, const float* istd_a,
                       const void* yb, const float* mean_b, const float* istd_b, double* sum_g,
-                      double* sum_ga, double* sum_gb, void* stream);
+                      double* sum_ga, double* sum_gb, int stat_rep, void* stream);
 /* dy_s = gamma_s*istd_s*(g - mean(g) - xhat_s*mean(g*xhat_s)) for sides a, b; g_out = g */
 int vlp_bn_bwd_apply(int dtype, long long M, int C, const void* dout, const float* dbc, int HW,
                      const void* mask, const void* ya, const float* mean_a, const float* istd_a,
@@ -100,7 +108,8 @@ int vlp_maxpool_fwd(int dtype, int N, int H, int W, int C, const void* y, const 
                     const float* sh, void* out, uint8_t* idx, void* stream);
 int vlp_maxpool_bwd(int dtype, int N, int H, int W, int C, const void* dp, const uint8_t* idx,
                     const void* y, const float* sc, const float* sh, const float* mean,
-                    const float* istd, void* g_out, double* sum_g, double* sum_gx, void* stream);
+                    const float* istd, void* g_out, double* sum_g, double* sum_gx, int stat_rep,
+                    void* stream);
 int vlp_avgpool_fwd(int dtype, int N, int HW, int C, const void* x, void* feat, void* stream);
 
 /* ---------------- text tower (TinyBERT) ----------------

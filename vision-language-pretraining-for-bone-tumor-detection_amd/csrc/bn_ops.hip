@@ -4,6 +4,14 @@
 //
 // Batch statistics come from the conv epilogues (fp64 sums); everything here
 // is an HBM-bound streaming pass over [M = N*H*W][C] tensors in 16-byte chunks.
+// Threads own a FIXED channel chunk (grid stride is a multiple of C/EPC), so
+// per-channel coefficients are folded once into registers and the inner loop
+// is loads, FMAs and stores only.
+//
+// Reductions over M (BN backward sums) are accumulated per workgroup and then
+// added with fp64 atomics into `rep` replicas of the [C] sums (replica =
+// workgroup % rep) to avoid serialising thousands of workgroups on C
+// addresses; vlp_stat_reduce folds replicas into replica 0.
 #include "common.h"
 
 namespace vlp {
@@ -51,27 +59,45 @@ __global__ void bn_eval_kernel(int C, const float* gamma, const float* beta, con
   shift[c] = beta[c] - rm[c] * gamma[c] * invstd;
 }
 
+// fold `rep` replicas [rep][C] into replica 0, for up to 3 arrays
+__global__ void stat_reduce_kernel(int rep, int C, double* a, double* b, double* c) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  double* arr[3] = {a, b, c};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    double* p = arr[k];
+    if (!p || i >= C) continue;
+    double s = 0;
+    for (int r = 0; r < rep; ++r) s += p[(size_t)r * C + i];
+    p[i] = s;
+  }
+}
+
 // ---- out = relu(sc*y + sh + identity), identity = idt or (scd*idt + shd) ----
 template <typename T>
-__global__ void bn_add_relu_kernel(size_t nchunks, int C, const T* __restrict__ y,
-                                   const float* __restrict__ sc, const float* __restrict__ sh,
-                                   const T* __restrict__ idt, const float* __restrict__ scd,
-                                   const float* __restrict__ shd, T* __restrict__ out) {
+__global__ void __launch_bounds__(256)
+bn_add_relu_kernel(unsigned nchunks, int cpr, const T* __restrict__ y, const float* __restrict__ sc,
+                   const float* __restrict__ sh, const T* __restrict__ idt,
+                   const float* __restrict__ scd, const float* __restrict__ shd, T* __restrict__ out) {
   constexpr int E = Chunk<T>::N;
-  const int cpr = C / E;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nchunks;
-       i += (size_t)gridDim.x * blockDim.x) {
-    int c0 = (int)(i % cpr) * E;
-    float a[E], b[E];
-    Chunk<T>::unpack(ldg16(y + i * E), a);
-    if (idt) Chunk<T>::unpack(ldg16(idt + i * E), b);
+  const unsigned tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned stride = gridDim.x * blockDim.x;   // multiple of cpr
+  const int c0 = (int)(tid % (unsigned)cpr) * E;
+  float a[E], b[E], c[E], d[E];
 #pragma unroll
-    for (int j = 0; j < E; ++j) {
-      float v = fmaf(a[j], sc[c0 + j], sh[c0 + j]);
-      if (idt) v += scd ? fmaf(b[j], scd[c0 + j], shd[c0 + j]) : b[j];
-      a[j] = fmaxf(v, 0.f);
-    }
-    stg16(out + i * E, Chunk<T>::pack(a));
+  for (int j = 0; j < E; ++j) {
+    a[j] = sc[c0 + j]; b[j] = sh[c0 + j];
+    c[j] = scd ? scd[c0 + j] : 1.f;
+    d[j] = scd ? shd[c0 + j] : 0.f;
+    b[j] += d[j];
+  }
+  for (unsigned i = tid; i < nchunks; i += stride) {
+    float u[E], v[E];
+    Chunk<T>::unpack(ldg16(y + (size_t)i * E), u);
+    Chunk<T>::unpack(ldg16(idt + (size_t)i * E), v);
+#pragma unroll
+    for (int j = 0; j < E; ++j) u[j] = fmaxf(fmaf(u[j], a[j], fmaf(v[j], c[j], b[j])), 0.f);
+    stg16(out + (size_t)i * E, Chunk<T>::pack(u));
   }
 }
 
@@ -84,7 +110,7 @@ bn_bwd_reduce_kernel(int M, int C, const T* __restrict__ dout, const float* __re
                      const float* __restrict__ mean_a, const float* __restrict__ istd_a,
                      const T* __restrict__ yb, const float* __restrict__ mean_b,
                      const float* __restrict__ istd_b, double* sum_g, double* sum_ga,
-                     double* sum_gb) {
+                     double* sum_gb, int rep) {
   constexpr int E = Chunk<T>::N;
   const int cpr = C / E;
   const int rows_per_iter = 256 / cpr;
@@ -93,39 +119,34 @@ bn_bwd_reduce_kernel(int M, int C, const T* __restrict__ dout, const float* __re
   const int c0 = cc * E;
   float ag[E], aa[E], ab[E];
   float ma[E], ia[E], mb[E], ib[E];
+  const float inv_hw = 1.f / (float)HW;
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     ag[j] = aa[j] = ab[j] = 0.f;
     ma[j] = mean_a[c0 + j]; ia[j] = istd_a[c0 + j];
     mb[j] = yb ? mean_b[c0 + j] : 0.f; ib[j] = yb ? istd_b[c0 + j] : 0.f;
   }
-  if (rr < rows_per_iter) {
-    for (int m = blockIdx.x * rows_per_iter + rr; m < M; m += gridDim.x * rows_per_iter) {
-      size_t o = (size_t)m * C + c0;
-      float g[E], mk[E], y1[E], y2[E];
-      if (dbc) {
-        int n = m / HW;
+  for (int m = blockIdx.x * rows_per_iter + rr; m < M; m += gridDim.x * rows_per_iter) {
+    size_t o = (size_t)m * C + c0;
+    float g[E], mk[E], y1[E], y2[E];
+    if (dbc) {
+      int n = m / HW;
 #pragma unroll
-        for (int j = 0; j < E; ++j) g[j] = dbc[(size_t)n * C + c0 + j] / (float)HW;
-      } else {
-        Chunk<T>::unpack(ldg16(dout + o), g);
-      }
-      if (mask) {
-        Chunk<T>::unpack(ldg16(mask + o), mk);
+      for (int j = 0; j < E; ++j) g[j] = dbc[(size_t)n * C + c0 + j] * inv_hw;
+    } else {
+      Chunk<T>::unpack(ldg16(dout + o), g);
+    }
+    Chunk<T>::unpack(ldg16(mask + o), mk);
+    Chunk<T>::unpack(ldg16(ya + o), y1);
+    if (yb) Chunk<T>::unpack(ldg16(yb + o), y2);
 #pragma unroll
-        for (int j = 0; j < E; ++j) g[j] = mk[j] > 0.f ? g[j] : 0.f;
-      }
-      Chunk<T>::unpack(ldg16(ya + o), y1);
-      if (yb) Chunk<T>::unpack(ldg16(yb + o), y2);
-#pragma unroll
-      for (int j = 0; j < E; ++j) {
-        ag[j] += g[j];
-        aa[j] += g[j] * ((y1[j] - ma[j]) * ia[j]);
-        if (yb) ab[j] += g[j] * ((y2[j] - mb[j]) * ib[j]);
-      }
+    for (int j = 0; j < E; ++j) {
+      float gg = mk[j] > 0.f ? g[j] : 0.f;
+      ag[j] += gg;
+      aa[j] += gg * ((y1[j] - ma[j]) * ia[j]);
+      if (yb) ab[j] += gg * ((y2[j] - mb[j]) * ib[j]);
     }
   }
-  // reduce across the rows handled by this block
   __shared__ float red[3][256][E];
 #pragma unroll
   for (int j = 0; j < E; ++j) { red[0][t][j] = ag[j]; red[1][t][j] = aa[j]; red[2][t][j] = ab[j]; }
@@ -138,60 +159,71 @@ bn_bwd_reduce_kernel(int M, int C, const T* __restrict__ dout, const float* __re
         aa[j] += red[1][t + r * cpr][j];
         ab[j] += red[2][t + r * cpr][j];
       }
+    const size_t ro = (size_t)(blockIdx.x % rep) * C + c0;
 #pragma unroll
     for (int j = 0; j < E; ++j) {
-      atomicAdd(sum_g + c0 + j, (double)ag[j]);
-      atomicAdd(sum_ga + c0 + j, (double)aa[j]);
-      if (yb) atomicAdd(sum_gb + c0 + j, (double)ab[j]);
+      atomicAdd(sum_g + ro + j, (double)ag[j]);
+      atomicAdd(sum_ga + ro + j, (double)aa[j]);
+      if (yb) atomicAdd(sum_gb + ro + j, (double)ab[j]);
     }
   }
 }
 
-// ---- backward apply: dy_a = k_a*(g - mean(g) - xhat_a*mean(g xhat_a)), same for b ----
+// ---- backward apply: dy_s = A_s*g + B_s*y_s + C_s (folded BN backward) ----
 struct BnBwdSide {
   const void* y; const float* mean; const float* istd; const float* gamma;
   const double* sum_g; const double* sum_gx; void* dy;
 };
-template <typename T>
-__global__ void bn_bwd_apply_kernel(size_t nchunks, int C, double count, const T* __restrict__ dout,
-                                    const float* __restrict__ dbc, int HW, const T* __restrict__ mask,
-                                    BnBwdSide A, BnBwdSide B, T* __restrict__ g_out) {
+template <typename T, bool HAS_B>
+__global__ void __launch_bounds__(256)
+bn_bwd_apply_kernel(unsigned nchunks, int cpr, double count, const T* __restrict__ dout,
+                    const float* __restrict__ dbc, int HW, const T* __restrict__ mask, BnBwdSide A,
+                    BnBwdSide B, T* __restrict__ g_out) {
   constexpr int E = Chunk<T>::N;
-  const int cpr = C / E;
+  const unsigned tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned stride = gridDim.x * blockDim.x;   // multiple of cpr
+  const int c0 = (int)(tid % (unsigned)cpr) * E;
+  const int C = cpr * E;
   const float inv_count = (float)(1.0 / count);
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nchunks;
-       i += (size_t)gridDim.x * blockDim.x) {
-    int c0 = (int)(i % cpr) * E;
-    size_t m = i / cpr;
+  const float inv_hw = 1.f / (float)HW;
+  // dy = k*(g - mg - (y-mu)*istd*mgx) = k*g + (-k*istd*mgx)*y + (-k*mg + k*istd*mgx*mu)
+  float ka[E], ba[E], ca[E], kb[E], bb[E], cb[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    int c = c0 + j;
+    float k = A.gamma[c] * A.istd[c];
+    float mg = (float)A.sum_g[c] * inv_count, mgx = (float)A.sum_gx[c] * inv_count;
+    ka[j] = k; ba[j] = -k * A.istd[c] * mgx; ca[j] = -k * mg + k * A.istd[c] * mgx * A.mean[c];
+    if (HAS_B) {
+      float k2 = B.gamma[c] * B.istd[c];
+      float mg2 = (float)B.sum_g[c] * inv_count, mgx2 = (float)B.sum_gx[c] * inv_count;
+      kb[j] = k2; bb[j] = -k2 * B.istd[c] * mgx2; cb[j] = -k2 * mg2 + k2 * B.istd[c] * mgx2 * B.mean[c];
+    }
+  }
+  for (unsigned i = tid; i < nchunks; i += stride) {
     float g[E], mk[E], y[E], d[E];
     if (dbc) {
-      int n = (int)(m / HW);
+      unsigned n = (i / (unsigned)cpr) / (unsigned)HW;
 #pragma unroll
-      for (int j = 0; j < E; ++j) g[j] = dbc[(size_t)n * C + c0 + j] / (float)HW;
+      for (int j = 0; j < E; ++j) g[j] = dbc[(size_t)n * C + c0 + j] * inv_hw;
     } else {
-      Chunk<T>::unpack(ldg16(dout + i * E), g);
+      Chunk<T>::unpack(ldg16(dout + (size_t)i * E), g);
     }
     if (mask) {
-      Chunk<T>::unpack(ldg16(mask + i * E), mk);
+      Chunk<T>::unpack(ldg16(mask + (size_t)i * E), mk);
 #pragma unroll
       for (int j = 0; j < E; ++j) g[j] = mk[j] > 0.f ? g[j] : 0.f;
     }
-    if (g_out) stg16(g_out + i * E, Chunk<T>::pack(g));
+    if (g_out) stg16(g_out + (size_t)i * E, Chunk<T>::pack(g));
+    Chunk<T>::unpack(ldg16((const T*)A.y + (size_t)i * E), y);
 #pragma unroll
-    for (int side = 0; side < 2; ++side) {
-      const BnBwdSide& S = side ? B : A;
-      if (!S.dy) continue;
-      Chunk<T>::unpack(ldg16((const T*)S.y + i * E), y);
+    for (int j = 0; j < E; ++j) d[j] = fmaf(ka[j], g[j], fmaf(ba[j], y[j], ca[j]));
+    stg16((T*)A.dy + (size_t)i * E, Chunk<T>::pack(d));
+    if (HAS_B) {
+      Chunk<T>::unpack(ldg16((const T*)B.y + (size_t)i * E), y);
 #pragma unroll
-      for (int j = 0; j < E; ++j) {
-        int c = c0 + j;
-        float is = S.istd[c];
-        float xh = (y[j] - S.mean[c]) * is;
-        float mg = (float)S.sum_g[c] * inv_count;
-        float mgx = (float)S.sum_gx[c] * inv_count;
-        d[j] = S.gamma[c] * is * (g[j] - mg - xh * mgx);
-      }
-      stg16((T*)S.dy + i * E, Chunk<T>::pack(d));
+      for (int j = 0; j < E; ++j) d[j] = fmaf(kb[j], g[j], fmaf(bb[j], y[j], cb[j]));
+      stg16((T*)B.dy + (size_t)i * E, Chunk<T>::pack(d));
     }
   }
 }
@@ -207,21 +239,25 @@ __global__ void bn_param_grad_kernel(int C, const double* sum_g, const double* s
 
 // ---- stem: maxpool 3x3/2 pad 1 over relu(sc*y + sh); records the argmax tap ----
 template <typename T>
-__global__ void maxpool_fwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const T* __restrict__ y,
-                                   const float* __restrict__ sc, const float* __restrict__ sh,
-                                   T* __restrict__ out, uint8_t* __restrict__ idx) {
+__global__ void __launch_bounds__(256)
+maxpool_fwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const T* __restrict__ y,
+                   const float* __restrict__ sc, const float* __restrict__ sh, T* __restrict__ out,
+                   uint8_t* __restrict__ idx) {
   constexpr int E = Chunk<T>::N;
   const int cpr = C / E;
-  size_t total = (size_t)N * Ho * Wo * cpr;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total;
-       i += (size_t)gridDim.x * blockDim.x) {
-    int cc = (int)(i % cpr);
-    size_t p = i / cpr;
+  const unsigned total = (unsigned)N * Ho * Wo * cpr;
+  const unsigned tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const unsigned stride = gridDim.x * blockDim.x;
+  const int c0 = (int)(tid % (unsigned)cpr) * E;
+  float a[E], b[E];
+#pragma unroll
+  for (int j = 0; j < E; ++j) { a[j] = sc[c0 + j]; b[j] = sh[c0 + j]; }
+  for (unsigned i = tid; i < total; i += stride) {
+    unsigned p = i / cpr;
     int wo = (int)(p % Wo);
-    size_t t = p / Wo;
+    unsigned t = p / Wo;
     int ho = (int)(t % Ho);
     int n = (int)(t / Ho);
-    int c0 = cc * E;
     float best[E], v[E];
     uint8_t bi[E];
 #pragma unroll
@@ -235,14 +271,21 @@ __global__ void maxpool_fwd_kernel(int N, int H, int W, int C, int Ho, int Wo, c
         Chunk<T>::unpack(ldg16(y + (((size_t)n * H + h) * W + w) * C + c0), v);
 #pragma unroll
         for (int j = 0; j < E; ++j) {
-          float a = fmaxf(fmaf(v[j], sc[c0 + j], sh[c0 + j]), 0.f);
-          if (a > best[j]) { best[j] = a; bi[j] = (uint8_t)(kh * 3 + kw); }
+          float q = fmaxf(fmaf(v[j], a[j], b[j]), 0.f);
+          if (q > best[j]) { best[j] = q; bi[j] = (uint8_t)(kh * 3 + kw); }
         }
       }
     }
-    stg16(out + p * C + c0, Chunk<T>::pack(best));
-#pragma unroll
-    for (int j = 0; j < E; ++j) idx[p * C + c0 + j] = bi[j];
+    stg16(out + (size_t)p * C + c0, Chunk<T>::pack(best));
+    if constexpr (E == 8) {
+      uint2 packed;
+      packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((unsigned)bi[3] << 24);
+      packed.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((unsigned)bi[7] << 24);
+      *reinterpret_cast<uint2*>(idx + (size_t)p * C + c0) = packed;
+    } else {
+      *reinterpret_cast<unsigned*>(idx + (size_t)p * C + c0) =
+          bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((unsigned)bi[3] << 24);
+    }
   }
 }
 
@@ -253,7 +296,7 @@ maxpool_bwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const T* __restri
                    const uint8_t* __restrict__ idx, const T* __restrict__ y,
                    const float* __restrict__ sc, const float* __restrict__ sh,
                    const float* __restrict__ mean, const float* __restrict__ istd,
-                   T* __restrict__ g_out, double* sum_g, double* sum_gx) {
+                   T* __restrict__ g_out, double* sum_g, double* sum_gx, int rep) {
   constexpr int E = Chunk<T>::N;
   const int cpr = C / E;
   const int rows_per_iter = 256 / cpr;
@@ -261,9 +304,12 @@ maxpool_bwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const T* __restri
   const int cc = t % cpr, rr = t / cpr;
   const int c0 = cc * E;
   const int M = N * H * W;
-  float ag[E], ax[E];
+  float ag[E], ax[E], a[E], b[E], mu[E], is[E];
 #pragma unroll
-  for (int j = 0; j < E; ++j) ag[j] = ax[j] = 0.f;
+  for (int j = 0; j < E; ++j) {
+    ag[j] = ax[j] = 0.f;
+    a[j] = sc[c0 + j]; b[j] = sh[c0 + j]; mu[j] = mean[c0 + j]; is[j] = istd[c0 + j];
+  }
   for (int m = blockIdx.x * rows_per_iter + rr; m < M; m += gridDim.x * rows_per_iter) {
     int w = m % W;
     int tt = m / W;
@@ -284,19 +330,29 @@ maxpool_bwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const T* __restri
         if (wo >= Wo) continue;
         size_t po = (((size_t)n * Ho + ho) * Wo + wo) * C + c0;
         Chunk<T>::unpack(ldg16(dp + po), v);
+        uint8_t ib[E];
+        if constexpr (E == 8) {
+          uint2 u = *reinterpret_cast<const uint2*>(idx + po);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { ib[j] = (u.x >> (8 * j)) & 255; ib[4 + j] = (u.y >> (8 * j)) & 255; }
+        } else {
+          unsigned u = *reinterpret_cast<const unsigned*>(idx + po);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) ib[j] = (u >> (8 * j)) & 255;
+        }
         const uint8_t tap = (uint8_t)(dh * 3 + dw);
 #pragma unroll
         for (int j = 0; j < E; ++j)
-          if (idx[po + j] == tap) g[j] += v[j];
+          if (ib[j] == tap) g[j] += v[j];
       }
     }
     size_t o = (size_t)m * C + c0;
     Chunk<T>::unpack(ldg16(y + o), yv);
 #pragma unroll
     for (int j = 0; j < E; ++j) {
-      if (!(fmaf(yv[j], sc[c0 + j], sh[c0 + j]) > 0.f)) g[j] = 0.f;
+      if (!(fmaf(yv[j], a[j], b[j]) > 0.f)) g[j] = 0.f;
       ag[j] += g[j];
-      ax[j] += g[j] * ((yv[j] - mean[c0 + j]) * istd[c0 + j]);
+      ax[j] += g[j] * ((yv[j] - mu[j]) * is[j]);
     }
     stg16(g_out + o, Chunk<T>::pack(g));
   }
@@ -308,10 +364,11 @@ maxpool_bwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const T* __restri
     for (int r = 1; r < rows_per_iter; ++r)
 #pragma unroll
       for (int j = 0; j < E; ++j) { ag[j] += red[0][t + r * cpr][j]; ax[j] += red[1][t + r * cpr][j]; }
+    const size_t ro = (size_t)(blockIdx.x % rep) * C + c0;
 #pragma unroll
     for (int j = 0; j < E; ++j) {
-      atomicAdd(sum_g + c0 + j, (double)ag[j]);
-      atomicAdd(sum_gx + c0 + j, (double)ax[j]);
+      atomicAdd(sum_g + ro + j, (double)ag[j]);
+      atomicAdd(sum_gx + ro + j, (double)ax[j]);
     }
   }
 }
@@ -326,6 +383,9 @@ __global__ void avgpool_fwd_kernel(int N, int HW, int C, const T* __restrict__ x
     feat[(size_t)n * C + c] = from_f<T>(s / (float)HW);
   }
 }
+
+// grid whose total thread count is a multiple of cpr (256 % cpr == 0)
+static inline int ew_grid(size_t nchunks) { return ew_blocks(nchunks, 256, 4096); }
 
 }  // namespace vlp
 
@@ -349,19 +409,27 @@ VLP_EXPORT int vlp_bn_eval_coeffs(int C, const float* gamma, const float* beta, 
   return (int)hipGetLastError();
 }
 
+VLP_EXPORT int vlp_stat_reduce(int rep, int C, double* a, double* b, double* c, void* stream) {
+  if (rep <= 1) return 0;
+  hipLaunchKernelGGL(stat_reduce_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     rep, C, a, b, c);
+  return (int)hipGetLastError();
+}
+
 VLP_EXPORT int vlp_bn_add_relu(int dtype, long long M, int C, const void* y, const float* sc,
                                const float* sh, const void* idt, const float* scd, const float* shd,
                                void* out, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == VLP_BF16) {
-    size_t n = (size_t)M * C / 8;
-    hipLaunchKernelGGL(bn_add_relu_kernel<bf16>, dim3(ew_blocks(n)), dim3(256), 0, st, n, C,
+  int epc = dtype == VLP_BF16 ? 8 : 4;
+  unsigned n = (unsigned)((size_t)M * C / epc);
+  int cpr = C / epc;
+  if (256 % cpr) return (int)hipErrorInvalidValue;
+  if (dtype == VLP_BF16)
+    hipLaunchKernelGGL(bn_add_relu_kernel<bf16>, dim3(ew_grid(n)), dim3(256), 0, st, n, cpr,
                        (const bf16*)y, sc, sh, (const bf16*)idt, scd, shd, (bf16*)out);
-  } else {
-    size_t n = (size_t)M * C / 4;
-    hipLaunchKernelGGL(bn_add_relu_kernel<float>, dim3(ew_blocks(n)), dim3(256), 0, st, n, C,
+  else
+    hipLaunchKernelGGL(bn_add_relu_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, st, n, cpr,
                        (const float*)y, sc, sh, (const float*)idt, scd, shd, (float*)out);
-  }
   return (int)hipGetLastError();
 }
 
@@ -369,19 +437,20 @@ VLP_EXPORT int vlp_bn_bwd_reduce(int dtype, long long M, int C, const void* dout
                                  int HW, const void* mask, const void* ya, const float* mean_a,
                                  const float* istd_a, const void* yb, const float* mean_b,
                                  const float* istd_b, double* sum_g, double* sum_ga, double* sum_gb,
-                                 void* stream) {
+                                 int stat_rep, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   int epc = dtype == VLP_BF16 ? 8 : 4;
   int rows_per_iter = 256 / (C / epc);
   int blocks = ew_blocks((size_t)M, rows_per_iter * 16, 2048);
+  if (stat_rep < 1) stat_rep = 1;
   if (dtype == VLP_BF16)
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<bf16>, dim3(blocks), dim3(256), 0, st, (int)M, C,
                        (const bf16*)dout, dbc, HW, (const bf16*)mask, (const bf16*)ya, mean_a, istd_a,
-                       (const bf16*)yb, mean_b, istd_b, sum_g, sum_ga, sum_gb);
+                       (const bf16*)yb, mean_b, istd_b, sum_g, sum_ga, sum_gb, stat_rep);
   else
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, dim3(blocks), dim3(256), 0, st, (int)M, C,
                        (const float*)dout, dbc, HW, (const float*)mask, (const float*)ya, mean_a,
-                       istd_a, (const float*)yb, mean_b, istd_b, sum_g, sum_ga, sum_gb);
+                       istd_a, (const float*)yb, mean_b, istd_b, sum_g, sum_ga, sum_gb, stat_rep);
   return (int)hipGetLastError();
 }
 
@@ -396,15 +465,26 @@ VLP_EXPORT int vlp_bn_bwd_apply(int dtype, long long M, int C, const void* dout,
   hipStream_t st = (hipStream_t)stream;
   BnBwdSide A{ya, mean_a, istd_a, gamma_a, sum_g_a, sum_gx_a, dy_a};
   BnBwdSide B{yb, mean_b, istd_b, gamma_b, sum_g_b, sum_gx_b, dy_b};
+  int epc = dtype == VLP_BF16 ? 8 : 4;
+  int cpr = C / epc;
+  if (256 % cpr) return (int)hipErrorInvalidValue;
+  unsigned n = (unsigned)((size_t)M * C / epc);
+  dim3 g(ew_grid(n));
+  bool hb = dy_b != nullptr;
   if (dtype == VLP_BF16) {
-    size_t n = (size_t)M * C / 8;
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16>, dim3(ew_blocks(n)), dim3(256), 0, st, n, C,
-                       (double)M, (const bf16*)dout, dbc, HW, (const bf16*)mask, A, B, (bf16*)g_out);
+    if (hb)
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16, true>), g, dim3(256), 0, st, n, cpr, (double)M,
+                         (const bf16*)dout, dbc, HW, (const bf16*)mask, A, B, (bf16*)g_out);
+    else
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16, false>), g, dim3(256), 0, st, n, cpr, (double)M,
+                         (const bf16*)dout, dbc, HW, (const bf16*)mask, A, B, (bf16*)g_out);
   } else {
-    size_t n = (size_t)M * C / 4;
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, dim3(ew_blocks(n)), dim3(256), 0, st, n, C,
-                       (double)M, (const float*)dout, dbc, HW, (const float*)mask, A, B,
-                       (float*)g_out);
+    if (hb)
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<float, true>), g, dim3(256), 0, st, n, cpr, (double)M,
+                         (const float*)dout, dbc, HW, (const float*)mask, A, B, (float*)g_out);
+    else
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<float, false>), g, dim3(256), 0, st, n, cpr, (double)M,
+                         (const float*)dout, dbc, HW, (const float*)mask, A, B, (float*)g_out);
   }
   return (int)hipGetLastError();
 }
@@ -423,10 +503,10 @@ VLP_EXPORT int vlp_maxpool_fwd(int dtype, int N, int H, int W, int C, const void
   int epc = dtype == VLP_BF16 ? 8 : 4;
   size_t n = (size_t)N * Ho * Wo * (C / epc);
   if (dtype == VLP_BF16)
-    hipLaunchKernelGGL(maxpool_fwd_kernel<bf16>, dim3(ew_blocks(n)), dim3(256), 0, st, N, H, W, C, Ho,
+    hipLaunchKernelGGL(maxpool_fwd_kernel<bf16>, dim3(ew_grid(n)), dim3(256), 0, st, N, H, W, C, Ho,
                        Wo, (const bf16*)y, sc, sh, (bf16*)out, idx);
   else
-    hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(ew_blocks(n)), dim3(256), 0, st, N, H, W, C, Ho,
+    hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, st, N, H, W, C, Ho,
                        Wo, (const float*)y, sc, sh, (float*)out, idx);
   return (int)hipGetLastError();
 }
@@ -434,20 +514,21 @@ VLP_EXPORT int vlp_maxpool_fwd(int dtype, int N, int H, int W, int C, const void
 VLP_EXPORT int vlp_maxpool_bwd(int dtype, int N, int H, int W, int C, const void* dp,
                                const uint8_t* idx, const void* y, const float* sc, const float* sh,
                                const float* mean, const float* istd, void* g_out, double* sum_g,
-                               double* sum_gx, void* stream) {
+                               double* sum_gx, int stat_rep, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
   int epc = dtype == VLP_BF16 ? 8 : 4;
   int rows_per_iter = 256 / (C / epc);
-  int blocks = ew_blocks((size_t)N * H * W, rows_per_iter * 16, 2048);
+  int blocks = ew_blocks((size_t)N * H * W, rows_per_iter * 16, 4096);
+  if (stat_rep < 1) stat_rep = 1;
   if (dtype == VLP_BF16)
     hipLaunchKernelGGL(maxpool_bwd_kernel<bf16>, dim3(blocks), dim3(256), 0, st, N, H, W, C, Ho, Wo,
                        (const bf16*)dp, idx, (const bf16*)y, sc, sh, mean, istd, (bf16*)g_out, sum_g,
-                       sum_gx);
+                       sum_gx, stat_rep);
   else
     hipLaunchKernelGGL(maxpool_bwd_kernel<float>, dim3(blocks), dim3(256), 0, st, N, H, W, C, Ho, Wo,
                        (const float*)dp, idx, (const float*)y, sc, sh, mean, istd, (float*)g_out,
-                       sum_g, sum_gx);
+                       sum_g, sum_gx, stat_rep);
   return (int)hipGetLastError();
 }
 

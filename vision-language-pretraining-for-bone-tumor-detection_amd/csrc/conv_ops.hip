@@ -208,7 +208,7 @@ struct StemWgradB {
 template <typename T>
 struct EpiConvFwd {
   static constexpr bool kStats = true;
-  double* stat1; double* stat2;
+  double* stat1; double* stat2; int stat_rep;
   T* y; int Co;
   __device__ void operator()(int row, int col, v4f v, v4f& s1, v4f& s2) const {
     store4(y + (size_t)row * Co + col, v);
@@ -221,7 +221,7 @@ struct EpiConvFwd {
 template <typename T>
 struct EpiDgradBN {
   static constexpr bool kStats = true;
-  double* stat1; double* stat2;
+  double* stat1; double* stat2; int stat_rep;
   T* g_out; int C;
   const T* y; const float* sc; const float* sh; const float* mean; const float* invstd;
   __device__ void operator()(int row, int col, v4f v, v4f& s1, v4f& s2) const {
@@ -277,11 +277,11 @@ static int gemm_wgrad(int M, int N, int K, const LA& la, const LB& lb, const EP&
 
 template <typename T>
 static int conv_fwd_t(const void* x, const void* wp, void* y, ConvGeom g, const float* sc,
-                      const float* sh, double* s1, double* s2, hipStream_t st) {
+                      const float* sh, double* s1, double* s2, int rep, hipStream_t st) {
   g.M = g.N * g.Ho * g.Wo;
   g.K = g.KH * g.KW * g.C;
   KMat<T> lb{(const T*)wp, g.K, g.Co, g.K};
-  EpiConvFwd<T> ep{s1, s2, (T*)y, g.Co};
+  EpiConvFwd<T> ep{s1, s2, rep, (T*)y, g.Co};
   if (sc) {
     ConvFwdA<T, true> la{g, (const T*)x, sc, sh};
     return gemm_auto<T>(g.M, g.Co, g.K, 1, la, lb, ep, st);
@@ -293,13 +293,13 @@ static int conv_fwd_t(const void* x, const void* wp, void* y, ConvGeom g, const 
 template <typename T>
 static int conv_dgrad_t(const void* dy, const void* wt, void* dx, ConvGeom g, const void* addend,
                         const void* ybn, const float* sc, const float* sh, const float* mean,
-                        const float* invstd, double* s1, double* s2, hipStream_t st) {
+                        const float* invstd, double* s1, double* s2, int rep, hipStream_t st) {
   g.M = g.N * g.H * g.W;
   g.K = g.KH * g.KW * g.Co;
   ConvDgradA<T> la{g, (const T*)dy};
   KMat<T> lb{(const T*)wt, g.K, g.C, g.K};
   if (ybn) {
-    EpiDgradBN<T> ep{s1, s2, (T*)dx, g.C, (const T*)ybn, sc, sh, mean, invstd};
+    EpiDgradBN<T> ep{s1, s2, rep, (T*)dx, g.C, (const T*)ybn, sc, sh, mean, invstd};
     return gemm_auto<T>(g.M, g.C, g.K, 1, la, lb, ep, st);
   }
   EpiDgradAdd<T> ep{nullptr, nullptr, (T*)dx, (const T*)addend, g.C};
@@ -380,12 +380,12 @@ using namespace vlp;
 VLP_EXPORT int vlp_conv_fwd(int dtype, const void* x, const void* wp, void* y, int N, int H, int W,
                             int C, int Co, int KH, int KW, int S, int P, const float* in_scale,
                             const float* in_shift, double* stat_sum, double* stat_sumsq,
-                            void* stream) {
+                            int stat_rep, void* stream) {
   ConvGeom g = make_geom(N, H, W, C, Co, KH, KW, S, P);
   hipStream_t st = (hipStream_t)stream;
   if (dtype == VLP_BF16)
-    return conv_fwd_t<bf16>(x, wp, y, g, in_scale, in_shift, stat_sum, stat_sumsq, st);
-  return conv_fwd_t<float>(x, wp, y, g, in_scale, in_shift, stat_sum, stat_sumsq, st);
+    return conv_fwd_t<bf16>(x, wp, y, g, in_scale, in_shift, stat_sum, stat_sumsq, stat_rep, st);
+  return conv_fwd_t<float>(x, wp, y, g, in_scale, in_shift, stat_sum, stat_sumsq, stat_rep, st);
 }
 
 VLP_EXPORT int vlp_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, int N, int H,
@@ -393,14 +393,14 @@ VLP_EXPORT int vlp_conv_dgrad(int dtype, const void* dy, const void* wt, void* d
                               const void* addend, const void* y_bn, const float* bn_scale,
                               const float* bn_shift, const float* bn_mean,
                               const float* bn_invstd, double* stat1, double* stat2,
-                              void* stream) {
+                              int stat_rep, void* stream) {
   ConvGeom g = make_geom(N, H, W, C, Co, KH, KW, S, P);
   hipStream_t st = (hipStream_t)stream;
   if (dtype == VLP_BF16)
     return conv_dgrad_t<bf16>(dy, wt, dx, g, addend, y_bn, bn_scale, bn_shift, bn_mean, bn_invstd,
-                              stat1, stat2, st);
+                              stat1, stat2, stat_rep, st);
   return conv_dgrad_t<float>(dy, wt, dx, g, addend, y_bn, bn_scale, bn_shift, bn_mean, bn_invstd,
-                             stat1, stat2, st);
+                             stat1, stat2, stat_rep, st);
 }
 
 VLP_EXPORT int vlp_conv_wgrad(int dtype, const void* dy, const void* x, float* dw_ws, int N, int H,
@@ -446,18 +446,18 @@ VLP_EXPORT void vlp_stem_geom(int H, int W, int* Ho, int* Wo, int* Hp, int* Wp) 
 }
 
 VLP_EXPORT int vlp_stem_fwd(int dtype, const void* xp, const void* wp, void* y, int N, int H, int W,
-                            double* stat_sum, double* stat_sumsq, void* stream) {
+                            double* stat_sum, double* stat_sumsq, int stat_rep, void* stream) {
   StemGeom g = make_stem(N, H, W);
   hipStream_t st = (hipStream_t)stream;
   if (dtype == VLP_BF16) {
     StemA<bf16> la{g, (const bf16*)xp};
     KMat<bf16> lb{(const bf16*)wp, 256, 64, 256};
-    EpiConvFwd<bf16> ep{stat_sum, stat_sumsq, (bf16*)y, 64};
+    EpiConvFwd<bf16> ep{stat_sum, stat_sumsq, stat_rep, (bf16*)y, 64};
     return launch_gemm<bf16, 256, 64, 4>(g.M, 64, 256, 1, la, lb, ep, st);
   }
   StemA<float> la{g, (const float*)xp};
   KMat<float> lb{(const float*)wp, 256, 64, 256};
-  EpiConvFwd<float> ep{stat_sum, stat_sumsq, (float*)y, 64};
+  EpiConvFwd<float> ep{stat_sum, stat_sumsq, stat_rep, (float*)y, 64};
   return launch_gemm<float, 256, 64, 4>(g.M, 64, 256, 1, la, lb, ep, st);
 }
 

@@ -267,6 +267,11 @@ gemm_kernel(GemmShape sh, LA la, LB lb, EP ep) {
     }
   }
   if constexpr (EP::kStats) {
+    // column sums: 16-lane shuffle -> per-wave partials in LDS -> one fp64
+    // atomic per column per workgroup, spread over `stat_rep` replicas
+    // (replica = tile id % stat_rep) so ~1e5 workgroups do not serialise on
+    // the same C addresses; vlp_stat_reduce folds the replicas afterwards.
+    float* red = reinterpret_cast<float*>(smem);   // [WGM][BN][2]; LDS is free after the K loop
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
 #pragma unroll
@@ -277,15 +282,23 @@ gemm_kernel(GemmShape sh, LA la, LB lb, EP ep) {
           x += __shfl_xor(x, o, 64);
           y += __shfl_xor(y, o, 64);
         }
-        s1[b][j] = x; s2[b][j] = y;
-      }
-      const int col = col0 + wn * WTN + b * 16 + 4 * lg;
-      if (li == 0 && col < sh.N) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          atomicAdd(ep.stat1 + col + j, (double)s1[b][j]);
-          atomicAdd(ep.stat2 + col + j, (double)s2[b][j]);
+        if (li == 0) {
+          const int cl = wn * WTN + b * 16 + 4 * lg + j;
+          red[(wm * BN + cl) * 2 + 0] = x;
+          red[(wm * BN + cl) * 2 + 1] = y;
         }
+      }
+    }
+    __syncthreads();
+    const int rep = ep.stat_rep > 1 ? (wid % ep.stat_rep) : 0;
+    for (int cl = threadIdx.x; cl < BN; cl += 256) {
+      const int col = col0 + cl;
+      if (col < sh.N) {
+        float x = 0.f, y = 0.f;
+#pragma unroll
+        for (int w = 0; w < WGM; ++w) { x += red[(w * BN + cl) * 2]; y += red[(w * BN + cl) * 2 + 1]; }
+        atomicAdd(ep.stat1 + (size_t)rep * sh.N + col, (double)x);
+        atomicAdd(ep.stat2 + (size_t)rep * sh.N + col, (double)y);
       }
     }
   }

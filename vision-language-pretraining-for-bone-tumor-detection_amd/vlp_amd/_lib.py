@@ -56,6 +56,11 @@ def parse_header(path: str = HEADER_PATH) -> Dict[str, dict]:
     return protos
 
 
+# entry points timed by ops.py under a kernel-family key (with algorithmic FLOPs)
+_FAMILY_TIMED = {"vlp_conv_fwd", "vlp_conv_dgrad", "vlp_conv_wgrad", "vlp_stem_fwd", "vlp_stem_wgrad",
+                 "vlp_linear_fwd", "vlp_linear_dgrad", "vlp_linear_wgrad"}
+
+
 class HipError(RuntimeError):
     pass
 
@@ -88,8 +93,14 @@ class _Lib:
             self.__dict__[name] = fn
             return fn
 
+        from . import ktimer
+        timed_here = name not in _FAMILY_TIMED
+
         def call(*args):
+            tk = ktimer.begin(name[4:]) if timed_here and ktimer._ENABLED else None
             r = fn(*args)
+            if tk is not None:
+                ktimer.end(tk)
             if ret == "int" and r != 0:
                 raise HipError(f"{name} failed with hipError {r}")
             return r

@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import torch
 
+from . import ktimer
 from ._lib import BF16, F32, lib, ptr, stream_of
 
 
@@ -27,39 +28,62 @@ def conv_out_hw(H, W, KH, KW, S, P):
     return (H + 2 * P - KH) // S + 1, (W + 2 * P - KW) // S + 1
 
 
+# kernel-family keys mirror the tile dispatch in csrc (one key = one kernel name)
+def _tile_auto(n):
+    return "256x64" if n <= 64 else "128x128"
+
+
+def _tile_wgrad(m):
+    return "64x256" if m <= 64 else "128x128"
+
+
+def _tile_lin(m, n):
+    return "256x64" if n <= 64 else ("64x256" if m <= 1024 else "128x128")
+
+
 # ---------------- convolutions ----------------
 def conv_fwd(x, wp, Co, KH, KW, S, P, in_scale=None, in_shift=None, stat_sum=None, stat_sumsq=None,
-             out=None):
+             out=None, stat_rep=1):
     N, H, W, C = x.shape
     Ho, Wo = conv_out_hw(H, W, KH, KW, S, P)
     y = out if out is not None else torch.empty((N, Ho, Wo, Co), dtype=x.dtype, device=x.device)
     if stat_sum is None:
         stat_sum = torch.zeros(Co, dtype=torch.float64, device=x.device)
         stat_sumsq = torch.zeros(Co, dtype=torch.float64, device=x.device)
+    tk = ktimer.begin(f"conv_fwd[{'xf' if in_scale is not None else 'raw'}]{_tile_auto(Co)}",
+                      2.0 * N * Ho * Wo * Co * C * KH * KW)
     lib().vlp_conv_fwd(dcode(x), ptr(x), ptr(wp), ptr(y), N, H, W, C, Co, KH, KW, S, P,
-                       ptr(in_scale), ptr(in_shift), ptr(stat_sum), ptr(stat_sumsq), _s())
+                       ptr(in_scale), ptr(in_shift), ptr(stat_sum), ptr(stat_sumsq), int(stat_rep), _s())
+    ktimer.end(tk)
     return y
 
 
 def conv_dgrad(dy, wt, H, W, C, KH, KW, S, P, addend=None, y_bn=None, bn=None, stat1=None,
-               stat2=None, out=None):
+               stat2=None, out=None, stat_rep=1):
     """bn = (scale, shift, mean, invstd) of the BN+ReLU producing the conv input."""
     N, Ho, Wo, Co = dy.shape
     dx = out if out is not None else torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
     sc = sh = mu = ist = None
     if y_bn is not None:
         sc, sh, mu, ist = bn
+    tk = ktimer.begin(f"conv_dgrad[{'bn' if y_bn is not None else 'add'}]{_tile_auto(C)}",
+                      2.0 * N * Ho * Wo * Co * C * KH * KW)
     lib().vlp_conv_dgrad(dcode(dy), ptr(dy), ptr(wt), ptr(dx), N, H, W, C, Co, KH, KW, S, P,
                          ptr(addend), ptr(y_bn), ptr(sc), ptr(sh), ptr(mu), ptr(ist), ptr(stat1),
-                         ptr(stat2), _s())
+                         ptr(stat2), int(stat_rep), _s())
+    ktimer.end(tk)
     return dx
 
 
 def conv_wgrad(dy, x, KH, KW, S, P, dw_ws, in_scale=None, in_shift=None):
     N, H, W, C = x.shape
     Co = dy.shape[-1]
+    Ho, Wo = dy.shape[1], dy.shape[2]
+    tk = ktimer.begin(f"conv_wgrad[{'xf' if in_scale is not None else 'raw'}]{_tile_wgrad(Co)}",
+                      2.0 * N * Ho * Wo * Co * C * KH * KW)
     lib().vlp_conv_wgrad(dcode(dy), ptr(dy), ptr(x), ptr(dw_ws), N, H, W, C, Co, KH, KW, S, P,
                          ptr(in_scale), ptr(in_shift), _s())
+    ktimer.end(tk)
     return dw_ws
 
 
@@ -81,16 +105,24 @@ def stem_prep_u8(x_u8, xp, mean, std):
     lib().vlp_stem_prep_u8(dcode(xp), ptr(x_u8), ptr(xp), N, H, W, float(mean), float(std), _s())
 
 
-def stem_fwd(xp, wp, N, H, W, y, stat_sum, stat_sumsq):
+def stem_fwd(xp, wp, N, H, W, y, stat_sum, stat_sumsq, stat_rep=1):
+    tk = ktimer.begin("stem_fwd", 2.0 * y.numel() * 147)
     lib().vlp_stem_fwd(dcode(xp), ptr(xp), ptr(wp), ptr(y), N, H, W, ptr(stat_sum),
-                       ptr(stat_sumsq), _s())
+                       ptr(stat_sumsq), int(stat_rep), _s())
+    ktimer.end(tk)
 
 
 def stem_wgrad(dy, xp, N, H, W, dw_ws):
+    tk = ktimer.begin("stem_wgrad", 2.0 * dy.numel() * 147)
     lib().vlp_stem_wgrad(dcode(dy), ptr(dy), ptr(xp), ptr(dw_ws), N, H, W, _s())
+    ktimer.end(tk)
 
 
 # ---------------- BN / pooling ----------------
+def stat_reduce(rep, C, a, b=None, c=None):
+    lib().vlp_stat_reduce(int(rep), int(C), ptr(a), ptr(b), ptr(c), _s())
+
+
 def bn_finalize(count, s, ss, gamma, beta, eps, momentum, running_mean, running_var, scale, shift,
                 mean, invstd):
     lib().vlp_bn_finalize(gamma.numel(), float(count), ptr(s), ptr(ss), ptr(gamma), ptr(beta),
@@ -111,10 +143,10 @@ def bn_add_relu(y, sc, sh, idt, scd, shd, out):
 
 
 def bn_bwd_reduce(M, C, dout, dbc, HW, mask, ya, mean_a, istd_a, yb, mean_b, istd_b, sum_g, sum_ga,
-                  sum_gb, dtype_ref):
+                  sum_gb, dtype_ref, stat_rep=1):
     lib().vlp_bn_bwd_reduce(dcode(dtype_ref), M, C, ptr(dout), ptr(dbc), HW, ptr(mask), ptr(ya),
                             ptr(mean_a), ptr(istd_a), ptr(yb), ptr(mean_b), ptr(istd_b), ptr(sum_g),
-                            ptr(sum_ga), ptr(sum_gb), _s())
+                            ptr(sum_ga), ptr(sum_gb), int(stat_rep), _s())
 
 
 def bn_bwd_apply(M, C, dout, dbc, HW, mask, A, B, g_out, dtype_ref):
@@ -134,10 +166,10 @@ def maxpool_fwd(y, sc, sh, out, idx):
     lib().vlp_maxpool_fwd(dcode(y), N, H, W, C, ptr(y), ptr(sc), ptr(sh), ptr(out), ptr(idx), _s())
 
 
-def maxpool_bwd(dp, idx, y, sc, sh, mean, istd, g_out, sum_g, sum_gx):
+def maxpool_bwd(dp, idx, y, sc, sh, mean, istd, g_out, sum_g, sum_gx, stat_rep=1):
     N, H, W, C = y.shape
     lib().vlp_maxpool_bwd(dcode(y), N, H, W, C, ptr(dp), ptr(idx), ptr(y), ptr(sc), ptr(sh),
-                          ptr(mean), ptr(istd), ptr(g_out), ptr(sum_g), ptr(sum_gx), _s())
+                          ptr(mean), ptr(istd), ptr(g_out), ptr(sum_g), ptr(sum_gx), int(stat_rep), _s())
 
 
 def avgpool_fwd(x, feat):
@@ -148,19 +180,25 @@ def avgpool_fwd(x, feat):
 # ---------------- text tower ----------------
 def linear_fwd(x, w, bias, y, M, N, K, ldx=None, ldy=None, mode=0, aux=None, res=None, ldr=None,
                p=0.0, seed=0):
+    tk = ktimer.begin(f"linear_fwd{_tile_lin(M, N)}", 2.0 * M * N * K)
     lib().vlp_linear_fwd(dcode(x), M, N, K, ptr(x), ldx or K, ptr(w), ptr(bias), ptr(y), ldy or N,
                          mode, ptr(aux), ptr(res), ldr or N, float(p), int(seed), _s())
+    ktimer.end(tk)
 
 
 def linear_dgrad(dy, w, dx, M, Kin, Nout, lddy=None, lddx=None, mode=0, aux=None, ldaux=None,
                  addend=None, ldad=None):
+    tk = ktimer.begin(f"linear_dgrad{_tile_lin(M, Kin)}", 2.0 * M * Kin * Nout)
     lib().vlp_linear_dgrad(dcode(dy), M, Kin, Nout, ptr(dy), lddy or Nout, ptr(w), ptr(dx),
                            lddx or Kin, mode, ptr(aux), ldaux or Kin, ptr(addend), ldad or Kin, _s())
+    ktimer.end(tk)
 
 
 def linear_wgrad(dy, x, dw, M, Nout, Kin, lddy=None, ldx=None):
+    tk = ktimer.begin("linear_wgrad128x128", 2.0 * M * Nout * Kin)
     lib().vlp_linear_wgrad(dcode(dy), M, Nout, Kin, ptr(dy), lddy or Nout, ptr(x), ldx or Kin,
                            ptr(dw), _s())
+    ktimer.end(tk)
 
 
 def colsum(x, out, M, N, ld=None):

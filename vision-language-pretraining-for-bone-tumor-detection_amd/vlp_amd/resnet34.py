@@ -36,6 +36,7 @@ LAYERS = (3, 4, 6, 3)
 WIDTHS = (64, 128, 256, 512)
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
+STAT_REP = 64   # replicas of per-channel fp64 sums (see vlp_stat_reduce)
 
 
 class _Holder(nn.Module):
@@ -186,8 +187,9 @@ class ResNet34Tower(ArenaModule):
         nb = len(self._bns)
         Cmax = 512
         ws["coef"] = torch.zeros(nb, 4, Cmax, dtype=torch.float32, device=dev)   # scale, shift, mean, istd
-        ws["fstat"] = torch.zeros(nb, 2, Cmax, dtype=torch.float64, device=dev)  # sum, sumsq
-        ws["bstat"] = torch.zeros(nb, 2, Cmax, dtype=torch.float64, device=dev)  # sum_g, sum_gx
+        # [R][C] replicated fp64 sums; replica 0 holds the total after vlp_stat_reduce
+        ws["fstat"] = torch.zeros(nb, 2, STAT_REP * Cmax, dtype=torch.float64, device=dev)  # sum, sumsq
+        ws["bstat"] = torch.zeros(nb, 3, STAT_REP * Cmax, dtype=torch.float64, device=dev)  # sum_g, sum_gx, sum_gx(ds)
         self._bn_idx = {k: i for i, k in enumerate(self._bns)}
         self._ws[key] = ws
         return ws
@@ -197,13 +199,19 @@ class ResNet34Tower(ArenaModule):
         c = ws["coef"][i]
         return c[0, :C], c[1, :C], c[2, :C], c[3, :C]
 
-    def _fstat(self, ws, key):
+    def _fstat(self, ws, key, full=False):
         i, C = self._bn_idx[key], self._bns[key].C
-        return ws["fstat"][i, 0, :C], ws["fstat"][i, 1, :C]
+        n = STAT_REP * C if full else C
+        return ws["fstat"][i, 0, :n], ws["fstat"][i, 1, :n]
 
-    def _bstat(self, ws, key):
+    def _bstat(self, ws, key, full=False):
         i, C = self._bn_idx[key], self._bns[key].C
-        return ws["bstat"][i, 0, :C], ws["bstat"][i, 1, :C]
+        n = STAT_REP * C if full else C
+        return ws["bstat"][i, 0, :n], ws["bstat"][i, 1, :n]
+
+    def _bstat_ds(self, ws, key, full=False):
+        i, C = self._bn_idx[key], self._bns[key].C
+        return ws["bstat"][i, 2, :(STAT_REP * C if full else C)]
 
     def pack_weights(self):
         """fp32 master (timm layout) -> GEMM operand layouts in the compute dtype."""
@@ -223,7 +231,9 @@ class ResNet34Tower(ArenaModule):
         sc, sh, mu, ist = self._coef(ws, key)
         h = bn.holder
         if training:
-            s, ss = self._fstat(ws, key)
+            s, ss = self._fstat(ws, key, full=True)
+            ops.stat_reduce(STAT_REP, bn.C, s, ss)
+            s, ss = s[:bn.C], ss[:bn.C]
             ops.bn_finalize(count, s, ss, gamma, beta, BN_EPS, BN_MOMENTUM, h.running_mean,
                             h.running_var, sc, sh, mu, ist)
             h.num_batches_tracked.add_(1)
@@ -255,8 +265,8 @@ class ResNet34Tower(ArenaModule):
         saved = {"N": N, "H": H, "W": W, "xp": xp, "training": training}
         # stem
         y0 = torch.empty(N, Ho, Wo, 64, dtype=T, device=dev)
-        s, ss = self._fstat(ws, "bn1")
-        ops.stem_fwd(xp, ws["conv1.wp"], N, H, W, y0, s, ss)
+        s, ss = self._fstat(ws, "bn1", full=True)
+        ops.stem_fwd(xp, ws["conv1.wp"], N, H, W, y0, s, ss, STAT_REP)
         sc0, sh0 = self._bn_finalize(ws, "bn1", N * Ho * Wo, training)
         Hq, Wq = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
         p = torch.empty(N, Hq, Wq, 64, dtype=T, device=dev)
@@ -267,19 +277,20 @@ class ResNet34Tower(ArenaModule):
         blocks = []
         for pre, has_ds in self._blocks:
             c1, c2 = self._convs[pre + ".conv1"], self._convs[pre + ".conv2"]
-            s, ss = self._fstat(ws, pre + ".bn1")
-            y1 = ops.conv_fwd(xcur, ws[c1.key + ".wp"], c1.Co, 3, 3, c1.S, 1, stat_sum=s, stat_sumsq=ss)
+            s, ss = self._fstat(ws, pre + ".bn1", full=True)
+            y1 = ops.conv_fwd(xcur, ws[c1.key + ".wp"], c1.Co, 3, 3, c1.S, 1, stat_sum=s, stat_sumsq=ss,
+                              stat_rep=STAT_REP)
             Mb = y1.numel() // y1.shape[-1]
             sc1, sh1 = self._bn_finalize(ws, pre + ".bn1", Mb, training)
-            s, ss = self._fstat(ws, pre + ".bn2")
-            y2 = ops.conv_fwd(y1, ws[c2.key + ".wp"], c2.Co, 3, 3, 1, 1, sc1, sh1, s, ss)
+            s, ss = self._fstat(ws, pre + ".bn2", full=True)
+            y2 = ops.conv_fwd(y1, ws[c2.key + ".wp"], c2.Co, 3, 3, 1, 1, sc1, sh1, s, ss, stat_rep=STAT_REP)
             sc2, sh2 = self._bn_finalize(ws, pre + ".bn2", Mb, training)
             yd = scd = shd = None
             if has_ds:
                 cd = self._convs[pre + ".downsample.0"]
-                s, ss = self._fstat(ws, pre + ".downsample.1")
+                s, ss = self._fstat(ws, pre + ".downsample.1", full=True)
                 yd = ops.conv_fwd(xcur, ws[cd.key + ".wp"], cd.Co, 1, 1, cd.S, 0, stat_sum=s,
-                                  stat_sumsq=ss)
+                                  stat_sumsq=ss, stat_rep=STAT_REP)
                 scd, shd = self._bn_finalize(ws, pre + ".downsample.1", Mb, training)
             out = torch.empty_like(y2)
             ops.bn_add_relu(y2, sc2, sh2, yd if has_ds else xcur, scd, shd, out)
@@ -315,13 +326,17 @@ class ResNet34Tower(ArenaModule):
             c1, c2 = self._convs[pre + ".conv1"], self._convs[pre + ".conv2"]
             k1, k2 = pre + ".bn1", pre + ".bn2"
             _, _, mu2, is2 = self._coef(ws, k2)
-            sg2, sgx2 = self._bstat(ws, k2)
-            mud = isd = sgxd = None
+            sg2f, sgx2f = self._bstat(ws, k2, full=True)
+            mud = isd = sgxdf = None
             if has_ds:
                 kd = pre + ".downsample.1"
                 _, _, mud, isd = self._coef(ws, kd)
-                sgd, sgxd = self._bstat(ws, kd)
-            ops.bn_bwd_reduce(M, C, dout, dbc, HW, out, y2, mu2, is2, yd, mud, isd, sg2, sgx2, sgxd, out)
+                sgxdf = self._bstat_ds(ws, k2, full=True)
+            ops.bn_bwd_reduce(M, C, dout, dbc, HW, out, y2, mu2, is2, yd, mud, isd, sg2f, sgx2f, sgxdf, out,
+                              stat_rep=STAT_REP)
+            ops.stat_reduce(STAT_REP, C, sg2f, sgx2f, sgxdf)
+            sg2, sgx2 = sg2f[:C], sgx2f[:C]
+            sgxd = sgxdf[:C] if has_ds else None
             ops.bn_param_grad(sg2, sgx2, self.arena.gview(k2 + ".weight"), self.arena.gview(k2 + ".bias"))
             dy2 = torch.empty_like(y2)
             A = (y2, mu2, is2, self.arena.view(k2 + ".weight"), sg2, sgx2, dy2)
@@ -335,9 +350,11 @@ class ResNet34Tower(ArenaModule):
             ops.bn_bwd_apply(M, C, dout, dbc, HW, out, A, Bside, g_id, out)
             # conv2: dgrad through relu(bn1(y1)) with BN1 backward sums; wgrad on relu(bn1(y1))
             sc1, sh1, mu1, is1 = self._coef(ws, k1)
-            sg1, sgx1 = self._bstat(ws, k1)
+            sg1f, sgx1f = self._bstat(ws, k1, full=True)
             g1 = ops.conv_dgrad(dy2, ws[c2.key + ".wt"], Hh, Ww, C, 3, 3, 1, 1, y_bn=y1,
-                                bn=(sc1, sh1, mu1, is1), stat1=sg1, stat2=sgx1)
+                                bn=(sc1, sh1, mu1, is1), stat1=sg1f, stat2=sgx1f, stat_rep=STAT_REP)
+            ops.stat_reduce(STAT_REP, C, sg1f, sgx1f)
+            sg1, sgx1 = sg1f[:C], sgx1f[:C]
             self._wgrad(ws, c2, dy2, y1, sc1, sh1)
             ops.bn_param_grad(sg1, sgx1, self.arena.gview(k1 + ".weight"), self.arena.gview(k1 + ".bias"))
             dy1 = torch.empty_like(y1)
@@ -355,9 +372,11 @@ class ResNet34Tower(ArenaModule):
         # stem: maxpool -> relu -> bn1 -> conv1
         y0, idx = saved["y0"], saved["idx"]
         sc0, sh0, mu0, is0 = self._coef(ws, "bn1")
-        sg0, sgx0 = self._bstat(ws, "bn1")
+        sg0f, sgx0f = self._bstat(ws, "bn1", full=True)
         g0 = torch.empty_like(y0)
-        ops.maxpool_bwd(dout, idx, y0, sc0, sh0, mu0, is0, g0, sg0, sgx0)
+        ops.maxpool_bwd(dout, idx, y0, sc0, sh0, mu0, is0, g0, sg0f, sgx0f, stat_rep=STAT_REP)
+        ops.stat_reduce(STAT_REP, 64, sg0f, sgx0f)
+        sg0, sgx0 = sg0f[:64], sgx0f[:64]
         ops.bn_param_grad(sg0, sgx0, self.arena.gview("bn1.weight"), self.arena.gview("bn1.bias"))
         dy0 = torch.empty_like(y0)
         M0 = y0.numel() // 64
