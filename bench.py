@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--seq-len", type=int, default=40)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-batch", type=int, default=4)
+    ap.add_argument("--cpu-sample-batch", type=int, default=32)
     ap.add_argument("--cpu-sample-steps", type=int, default=3)
     ap.add_argument("--roofline-kernel", default="auto")
     ap.add_argument("--kernel-report", default="")
