@@ -86,7 +86,7 @@ int vlp_bn_finalize(int C, double count, const double* sum, const double* sumsq,
 int vlp_bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* running_mean,
                        const float* running_var, float eps, float* scale, float* shift,
                        void* stream);
-/* out = relu(sc*y + sh + idt'), idt' = idt (scd == NULL) or scd*idt + shd */
+/* out = relu(sc*y + sh + idt'), idt' = idt (scd == NULL) or scd*idt + shd; idt == NULL: relu(sc*y + sh) */
 int vlp_bn_add_relu(int dtype, long long M, int C, const void* y, const float* sc, const float* sh,
                     const void* idt, const float* scd, const float* shd, void* out, void* stream);
 /* g = dout * (mask > 0) (dout may be a broadcast [N][C]/HW gradient `dbc`);

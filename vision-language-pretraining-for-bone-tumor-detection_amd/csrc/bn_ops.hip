@@ -74,7 +74,7 @@ __global__ void stat_reduce_kernel(int rep, int C, double* a, double* b, double*
 }
 
 // ---- out = relu(sc*y + sh + identity), identity = idt or (scd*idt + shd) ----
-template <typename T>
+template <typename T, bool HAS_IDT>
 __global__ void __launch_bounds__(256)
 bn_add_relu_kernel(unsigned nchunks, int cpr, const T* __restrict__ y, const float* __restrict__ sc,
                    const float* __restrict__ sh, const T* __restrict__ idt,
@@ -94,9 +94,14 @@ bn_add_relu_kernel(unsigned nchunks, int cpr, const T* __restrict__ y, const flo
   for (unsigned i = tid; i < nchunks; i += stride) {
     float u[E], v[E];
     Chunk<T>::unpack(ldg16(y + (size_t)i * E), u);
-    Chunk<T>::unpack(ldg16(idt + (size_t)i * E), v);
+    if constexpr (HAS_IDT) {
+      Chunk<T>::unpack(ldg16(idt + (size_t)i * E), v);
 #pragma unroll
-    for (int j = 0; j < E; ++j) u[j] = fmaxf(fmaf(u[j], a[j], fmaf(v[j], c[j], b[j])), 0.f);
+      for (int j = 0; j < E; ++j) u[j] = fmaxf(fmaf(u[j], a[j], fmaf(v[j], c[j], b[j])), 0.f);
+    } else {
+#pragma unroll
+      for (int j = 0; j < E; ++j) u[j] = fmaxf(fmaf(u[j], a[j], b[j]), 0.f);
+    }
     stg16(out + (size_t)i * E, Chunk<T>::pack(u));
   }
 }
@@ -424,12 +429,22 @@ VLP_EXPORT int vlp_bn_add_relu(int dtype, long long M, int C, const void* y, con
   unsigned n = (unsigned)((size_t)M * C / epc);
   int cpr = C / epc;
   if (256 % cpr) return (int)hipErrorInvalidValue;
-  if (dtype == VLP_BF16)
-    hipLaunchKernelGGL(bn_add_relu_kernel<bf16>, dim3(ew_grid(n)), dim3(256), 0, st, n, cpr,
-                       (const bf16*)y, sc, sh, (const bf16*)idt, scd, shd, (bf16*)out);
-  else
-    hipLaunchKernelGGL(bn_add_relu_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, st, n, cpr,
-                       (const float*)y, sc, sh, (const float*)idt, scd, shd, (float*)out);
+  dim3 g(ew_grid(n));
+  if (dtype == VLP_BF16) {
+    if (idt)
+      hipLaunchKernelGGL((bn_add_relu_kernel<bf16, true>), g, dim3(256), 0, st, n, cpr, (const bf16*)y, sc,
+                         sh, (const bf16*)idt, scd, shd, (bf16*)out);
+    else
+      hipLaunchKernelGGL((bn_add_relu_kernel<bf16, false>), g, dim3(256), 0, st, n, cpr, (const bf16*)y,
+                         sc, sh, (const bf16*)idt, scd, shd, (bf16*)out);
+  } else {
+    if (idt)
+      hipLaunchKernelGGL((bn_add_relu_kernel<float, true>), g, dim3(256), 0, st, n, cpr, (const float*)y,
+                         sc, sh, (const float*)idt, scd, shd, (float*)out);
+    else
+      hipLaunchKernelGGL((bn_add_relu_kernel<float, false>), g, dim3(256), 0, st, n, cpr,
+                         (const float*)y, sc, sh, (const float*)idt, scd, shd, (float*)out);
+  }
   return (int)hipGetLastError();
 }
 

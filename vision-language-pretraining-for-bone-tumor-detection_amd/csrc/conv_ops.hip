@@ -86,6 +86,17 @@ struct ConvFwdA {
     if constexpr (XF) v = xform_chunk<T>(v, sc, sh, ci);
     return v;
   }
+  static constexpr bool kDirect = !XF;
+  __device__ const void* addr(const State& s, int k) const {
+    if (!s.ok || k >= g.K) return zero_page();
+    int tap = fdiv(k, g.fd_c);
+    int ci = k - tap * g.C;
+    int kh = fdiv(tap, g.fd_kw);
+    int kw = tap - kh * g.KW;
+    int hi = s.hi0 + kh, wi = s.wi0 + kw;
+    if ((unsigned)hi >= (unsigned)g.H || (unsigned)wi >= (unsigned)g.W) return zero_page();
+    return s.base + ((size_t)hi * g.W + wi) * g.C + ci;
+  }
 };
 
 // ---- data-gradient A operand: output-gradient "patches", K-contiguous ----
@@ -123,6 +134,23 @@ struct ConvDgradA {
     if (ho >= g.Ho || wo >= g.Wo) return zero4();
     return ldg16(s.base + ((size_t)ho * g.Wo + wo) * g.Co + co);
   }
+  static constexpr bool kDirect = true;
+  __device__ const void* addr(const State& s, int k) const {
+    if (!s.ok || k >= g.K) return zero_page();
+    int tap = fdiv(k, g.fd_co);
+    int co = k - tap * g.Co;
+    int kh = fdiv(tap, g.fd_kw);
+    int kw = tap - kh * g.KW;
+    int th = s.hp - kh, tw = s.wp - kw;
+    if (th < 0 || tw < 0) return zero_page();
+    int ho = th, wo = tw;
+    if (g.S != 1) {
+      if ((th % g.S) | (tw % g.S)) return zero_page();
+      ho = th / g.S; wo = tw / g.S;
+    }
+    if (ho >= g.Ho || wo >= g.Wo) return zero_page();
+    return s.base + ((size_t)ho * g.Wo + wo) * g.Co + co;
+  }
 };
 
 // ---- weight-gradient B operand: input patches, MN-contiguous over (kh,kw,ci) ----
@@ -152,6 +180,17 @@ struct ConvWgradB {
     uint4 v = ldg16(x + (((size_t)n * g.H + hi) * g.W + wi) * g.C + s.ci);
     if constexpr (XF) v = xform_chunk<T>(v, sc, sh, s.ci);
     return v;
+  }
+  static constexpr bool kDirect = !XF;
+  __device__ const void* addr(const State& s, int m) const {
+    if (!s.ok || m >= g.M) return zero_page();
+    int n = fdiv(m, g.fd_howo);
+    int r = m - n * g.Ho * g.Wo;
+    int ho = fdiv(r, g.fd_wo);
+    int wo = r - ho * g.Wo;
+    int hi = ho * g.S - g.P + s.kh, wi = wo * g.S - g.P + s.kw;
+    if ((unsigned)hi >= (unsigned)g.H || (unsigned)wi >= (unsigned)g.W) return zero_page();
+    return x + (((size_t)n * g.H + hi) * g.W + wi) * g.C + s.ci;
   }
 };
 
@@ -183,6 +222,12 @@ struct StemA {
     if (!s.ok || kh >= 7) return zero4();
     return ldg16(s.base + ((size_t)kh * g.Wp + kw) * 4);
   }
+  static constexpr bool kDirect = true;
+  __device__ const void* addr(const State& s, int k) const {
+    int kh = k >> 5, kw = (k & 31) >> 2;
+    if (!s.ok || kh >= 7) return zero_page();
+    return s.base + ((size_t)kh * g.Wp + kw) * 4;
+  }
 };
 template <typename T>
 struct StemWgradB {
@@ -200,6 +245,15 @@ struct StemWgradB {
     int ho = fdiv(r, g.fd_wo);
     int wo = r - ho * g.Wo;
     return ldg16(xp + (((size_t)n * g.Hp + 2 * ho) * g.Wp + 2 * wo) * 4 + s.off);
+  }
+  static constexpr bool kDirect = true;
+  __device__ const void* addr(const State& s, int m) const {
+    if (!s.ok || m >= g.M) return zero_page();
+    int n = fdiv(m, g.fd_howo);
+    int r = m - n * g.Ho * g.Wo;
+    int ho = fdiv(r, g.fd_wo);
+    int wo = r - ho * g.Wo;
+    return xp + (((size_t)n * g.Hp + 2 * ho) * g.Wp + 2 * wo) * 4 + s.off;
   }
 };
 

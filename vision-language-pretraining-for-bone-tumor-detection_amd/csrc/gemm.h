@@ -26,6 +26,7 @@
 // remapped so that consecutive tile ids share an XCD (L2 reuse of the A panel).
 // Split-K over grid.y for reductions over pixels (weight gradients).
 #pragma once
+#include <type_traits>
 #include "common.h"
 
 namespace vlp {
@@ -102,6 +103,79 @@ struct Stager {
       *reinterpret_cast<uint4*>(lds + off) = r[i];
     }
   }
+};
+
+// ---------------- direct-to-LDS staging (bf16) ----------------
+// Loaders that can name the global address of a chunk (kDirect = true,
+// `const void* addr(State, k)`; out-of-range chunks point at a zero page)
+// are staged with global_load_lds_dwordx4: each wave-instruction writes 1 KiB
+// of LDS lane-linearly, so lane L of instruction i fills PHYSICAL chunk
+// q = (wave*NI + i)*64 + L and fetches the LOGICAL chunk that the XOR swizzle
+// places there (the swizzles are involutions).  No staging registers, no
+// ds_write pass; the loads of tile t+1 fly while tile t is multiplied.
+static __device__ uint4 g_zero16;
+__device__ __forceinline__ const void* zero_page() { return &g_zero16; }
+
+template <class L, class = void> struct DirectTrait { static constexpr bool value = false; };
+template <class L> struct DirectTrait<L, std::void_t<decltype(L::kDirect)>> {
+  static constexpr bool value = L::kDirect;
+};
+
+template <typename T, int BM, class L>
+struct GStager {
+  using G = TileGeom<T, BM, L::kKContig>;
+  static constexpr int NI = G::NCH;
+  typename L::State st[NI];
+  int koff[NI];
+
+  __device__ __forceinline__ void init(const L& ld, int row0) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int q = (w * NI + i) * 64 + lane;
+      if constexpr (L::kKContig) {
+        const int r = q >> 3, p = q & 7;
+        const int c = p ^ ((r >> 1) & 7);
+        st[i] = ld.fixed(row0 + r);
+        koff[i] = c * G::EPC;
+      } else {
+        const int o = q * 16;
+        const int k = o / G::RB, inrow = o % G::RB;
+        const int sw = (G::RB >= 256) ? (k & 7) : ((k >> 1) & 3);
+        const int b = (inrow >> 5) ^ sw, half = (inrow >> 4) & 1;
+        st[i] = ld.fixed(row0 + (2 * b + half) * G::EPC);
+        koff[i] = k;
+      }
+    }
+  }
+  __device__ __forceinline__ void issue(const L& ld, int k0, char* lds) const {
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const void* p = ld.addr(st[i], k0 + koff[i]);
+      __builtin_amdgcn_global_load_lds(p, (__attribute__((address_space(3))) void*)(lds + (w * NI + i) * 1024),
+                                       16, 0, 0);
+    }
+  }
+};
+
+// Uniform staging interface: register staging (any loader, fp32 parity mode,
+// transforming loaders) or direct-to-LDS (bf16 + kDirect loaders).
+template <typename T, int BM, class L, bool DIRECT = (sizeof(T) == 2) && DirectTrait<L>::value>
+struct OpStager;
+template <typename T, int BM, class L>
+struct OpStager<T, BM, L, false> {
+  Stager<T, BM, L> s;
+  __device__ __forceinline__ void init(const L& ld, int row0) { s.init(ld, row0); }
+  __device__ __forceinline__ void prefetch(const L& ld, int k0, char*) { s.load(ld, k0); }
+  __device__ __forceinline__ void commit(char* lds) const { s.store(lds); }
+};
+template <typename T, int BM, class L>
+struct OpStager<T, BM, L, true> {
+  GStager<T, BM, L> s;
+  __device__ __forceinline__ void init(const L& ld, int row0) { s.init(ld, row0); }
+  __device__ __forceinline__ void prefetch(const L& ld, int k0, char* lds) { s.issue(ld, k0, lds); }
+  __device__ __forceinline__ void commit(char*) const {}
 };
 
 // ---------------- fragment reads ----------------
@@ -183,8 +257,8 @@ gemm_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   const int wave = threadIdx.x >> 6;
   const int wm = wave / WGN, wn = wave - wm * WGN;
 
-  Stager<T, BM, LA> sa;
-  Stager<T, BN, LB> sb;
+  OpStager<T, BM, LA> sa;
+  OpStager<T, BN, LB> sb;
   sa.init(la, row0);
   sb.init(lb, col0);
 
@@ -195,18 +269,19 @@ gemm_kernel(GemmShape sh, LA la, LB lb, EP ep) {
     for (int b = 0; b < NB; ++b) acc[a][b] = v4f{0.f, 0.f, 0.f, 0.f};
 
   if (nk > 0) {
-    sa.load(la, kb);
-    sb.load(lb, kb);
-    sa.store(smem);
-    sb.store(smem + GA::BYTES);
+    sa.prefetch(la, kb, smem);
+    sb.prefetch(lb, kb, smem + GA::BYTES);
+    sa.commit(smem);
+    sb.commit(smem + GA::BYTES);
   }
   __syncthreads();
 
   for (int t = 0; t < nk; ++t) {
     const bool more = (t + 1) < nk;
+    char* nxt = smem + ((t + 1) & 1) * STAGE;
     if (more) {
-      sa.load(la, kb + (t + 1) * BK);
-      sb.load(lb, kb + (t + 1) * BK);
+      sa.prefetch(la, kb + (t + 1) * BK, nxt);
+      sb.prefetch(lb, kb + (t + 1) * BK, nxt + GA::BYTES);
     }
     const char* ia = smem + (t & 1) * STAGE;
     const char* ib = ia + GA::BYTES;
@@ -239,44 +314,36 @@ gemm_kernel(GemmShape sh, LA la, LB lb, EP ep) {
       }
     }
     if (more) {
-      char* nxt = smem + ((t + 1) & 1) * STAGE;
-      sa.store(nxt);
-      sb.store(nxt + GA::BYTES);
+      sa.commit(nxt);
+      sb.commit(nxt + GA::BYTES);
     }
     __syncthreads();
   }
 
   // ---------------- epilogue ----------------
-  // lane l = 16g + i owns C[row = rbase + i][col = cbase + 4g .. 4g+3]
+  // lane l = 16g + i owns C[row = rbase + i][col = cbase + 4g .. 4g+3].
+  // Column blocks are finished one at a time so the statistic partials have a
+  // short live range (the whole-tile form cost ~140 VGPRs and 2 waves/SIMD).
   const int l = threadIdx.x & 63;
   const int li = l & 15, lg = l >> 4;
-  v4f s1[NB], s2[NB];
+  float* red = reinterpret_cast<float*>(smem);   // [WGM][BN][2]; LDS is free after the K loop
 #pragma unroll
-  for (int b = 0; b < NB; ++b) { s1[b] = v4f{0.f, 0.f, 0.f, 0.f}; s2[b] = s1[b]; }
+  for (int b = 0; b < NB; ++b) {
+    const int col = col0 + wn * WTN + b * 16 + 4 * lg;
+    v4f s1 = v4f{0.f, 0.f, 0.f, 0.f}, s2 = s1;
 #pragma unroll
-  for (int a = 0; a < MB; ++a) {
-    const int row = row0 + wm * WTM + a * 16 + li;
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const int col = col0 + wn * WTN + b * 16 + 4 * lg;
+    for (int a = 0; a < MB; ++a) {
+      const int row = row0 + wm * WTM + a * 16 + li;
       if (row < sh.M && col < sh.N) {
         v4f c1 = v4f{0.f, 0.f, 0.f, 0.f}, c2 = c1;
         ep(row, col, acc[a][b], c1, c2);
-        if constexpr (EP::kStats) { s1[b] += c1; s2[b] += c2; }
+        if constexpr (EP::kStats) { s1 += c1; s2 += c2; }
       }
     }
-  }
-  if constexpr (EP::kStats) {
-    // column sums: 16-lane shuffle -> per-wave partials in LDS -> one fp64
-    // atomic per column per workgroup, spread over `stat_rep` replicas
-    // (replica = tile id % stat_rep) so ~1e5 workgroups do not serialise on
-    // the same C addresses; vlp_stat_reduce folds the replicas afterwards.
-    float* red = reinterpret_cast<float*>(smem);   // [WGM][BN][2]; LDS is free after the K loop
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
+    if constexpr (EP::kStats) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float x = s1[b][j], y = s2[b][j];
+        float x = s1[j], y = s2[j];
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) {
           x += __shfl_xor(x, o, 64);
@@ -289,6 +356,12 @@ gemm_kernel(GemmShape sh, LA la, LB lb, EP ep) {
         }
       }
     }
+  }
+  if constexpr (EP::kStats) {
+    // per-wave partials -> one fp64 atomic per column per workgroup, spread
+    // over `stat_rep` replicas (replica = tile id % stat_rep) so ~1e5
+    // workgroups do not serialise on the same C addresses; vlp_stat_reduce
+    // folds the replicas afterwards.
     __syncthreads();
     const int rep = ep.stat_rep > 1 ? (wid % ep.stat_rep) : 0;
     for (int cl = threadIdx.x; cl < BN; cl += 256) {
@@ -344,22 +417,30 @@ inline int launch_gemm(int M, int N, int K, int ksplit, const LA& la, const LB& 
 template <typename T>
 struct KMat {
   static constexpr bool kKContig = true;
+  static constexpr bool kDirect = true;
   struct State { const T* p; bool ok; };
   const T* p; int ld, M, K;
   __device__ State fixed(int m) const { return State{p + (size_t)m * ld, m < M}; }
   __device__ uint4 load(const State& s, int k) const {
     return (s.ok && k < K) ? ldg16(s.p + k) : zero4();
   }
+  __device__ const void* addr(const State& s, int k) const {
+    return (s.ok && k < K) ? (const void*)(s.p + k) : zero_page();
+  }
 };
 // MN contiguous: A(m,k) = p[k*ld + m].  Requires M % EPC == 0.
 template <typename T>
 struct MNMat {
   static constexpr bool kKContig = false;
+  static constexpr bool kDirect = true;
   struct State { const T* p; bool ok; };
   const T* p; int ld, M, K;
   __device__ State fixed(int m) const { return State{p + m, m < M}; }
   __device__ uint4 load(const State& s, int k) const {
     return (s.ok && k < K) ? ldg16(s.p + (size_t)k * ld) : zero4();
+  }
+  __device__ const void* addr(const State& s, int k) const {
+    return (s.ok && k < K) ? (const void*)(s.p + (size_t)k * ld) : zero_page();
   }
 };
 

@@ -282,8 +282,11 @@ class ResNet34Tower(ArenaModule):
                               stat_rep=STAT_REP)
             Mb = y1.numel() // y1.shape[-1]
             sc1, sh1 = self._bn_finalize(ws, pre + ".bn1", Mb, training)
+            a1 = torch.empty_like(y1)    # relu(bn1(y1)), materialised once: conv2 fwd + wgrad stream it
+            ops.bn_add_relu(y1, sc1, sh1, None, None, None, a1)
             s, ss = self._fstat(ws, pre + ".bn2", full=True)
-            y2 = ops.conv_fwd(y1, ws[c2.key + ".wp"], c2.Co, 3, 3, 1, 1, sc1, sh1, s, ss, stat_rep=STAT_REP)
+            y2 = ops.conv_fwd(a1, ws[c2.key + ".wp"], c2.Co, 3, 3, 1, 1, stat_sum=s, stat_sumsq=ss,
+                              stat_rep=STAT_REP)
             sc2, sh2 = self._bn_finalize(ws, pre + ".bn2", Mb, training)
             yd = scd = shd = None
             if has_ds:
@@ -294,7 +297,7 @@ class ResNet34Tower(ArenaModule):
                 scd, shd = self._bn_finalize(ws, pre + ".downsample.1", Mb, training)
             out = torch.empty_like(y2)
             ops.bn_add_relu(y2, sc2, sh2, yd if has_ds else xcur, scd, shd, out)
-            blocks.append({"x": xcur, "y1": y1, "y2": y2, "yd": yd, "out": out})
+            blocks.append({"x": xcur, "y1": y1, "a1": a1, "y2": y2, "yd": yd, "out": out})
             xcur = out
         feat = torch.empty(N, 512, dtype=T, device=dev)
         ops.avgpool_fwd(xcur, feat)
@@ -355,7 +358,7 @@ class ResNet34Tower(ArenaModule):
                                 bn=(sc1, sh1, mu1, is1), stat1=sg1f, stat2=sgx1f, stat_rep=STAT_REP)
             ops.stat_reduce(STAT_REP, C, sg1f, sgx1f)
             sg1, sgx1 = sg1f[:C], sgx1f[:C]
-            self._wgrad(ws, c2, dy2, y1, sc1, sh1)
+            self._wgrad(ws, c2, dy2, B["a1"])
             ops.bn_param_grad(sg1, sgx1, self.arena.gview(k1 + ".weight"), self.arena.gview(k1 + ".bias"))
             dy1 = torch.empty_like(y1)
             ops.bn_bwd_apply(M, C, g1, None, 1, None,
