@@ -355,9 +355,10 @@ VLP_EXPORT int vlp_linear_dgrad(int dtype, int M, int Kin, int Nout, const void*
 VLP_EXPORT int vlp_linear_wgrad(int dtype, int M, int Nout, int Kin, const void* dy, int lddy,
                                 const void* x, int ldx, float* dw, void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  // each split reduces >= 1024 token rows (short splits were prologue/atomic bound)
   int tiles = ((Nout + 127) / 128) * ((Kin + 127) / 128);
-  int ksplit = (1024 + tiles - 1) / tiles;
-  int maxsplit = (M + 255) / 256;
+  int ksplit = (512 + tiles - 1) / tiles;
+  int maxsplit = (M + 1023) / 1024;
   if (ksplit > maxsplit) ksplit = maxsplit;
   EpiAtomic ep{nullptr, nullptr, dw, Kin, 1.0f};
   if (dtype == VLP_BF16) {

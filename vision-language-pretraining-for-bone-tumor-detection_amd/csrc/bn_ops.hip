@@ -59,18 +59,23 @@ __global__ void bn_eval_kernel(int C, const float* gamma, const float* beta, con
   shift[c] = beta[c] - rm[c] * gamma[c] * invstd;
 }
 
-// fold `rep` replicas [rep][C] into replica 0, for up to 3 arrays
-__global__ void stat_reduce_kernel(int rep, int C, double* a, double* b, double* c) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
+// fold `rep` replicas [rep][C] into replica 0, for up to 3 arrays.  One block
+// per (array, 64-channel group); the 4 waves split the replicas so each lane
+// has only rep/4 independent loads in flight (latency-bound otherwise).
+__global__ void __launch_bounds__(256)
+stat_reduce_kernel(int rep, int C, double* a, double* b, double* c) {
+  __shared__ double part[4][64];
   double* arr[3] = {a, b, c};
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    double* p = arr[k];
-    if (!p || i >= C) continue;
-    double s = 0;
-    for (int r = 0; r < rep; ++r) s += p[(size_t)r * C + i];
-    p[i] = s;
-  }
+  double* p = arr[blockIdx.y];
+  if (!p) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ch = blockIdx.x * 64 + lane;
+  double s = 0;
+  if (ch < C)
+    for (int r = w; r < rep; r += 4) s += p[(size_t)r * C + ch];
+  part[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && ch < C) p[ch] = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
 }
 
 // ---- out = relu(sc*y + sh + identity), identity = idt or (scd*idt + shd) ----
@@ -416,7 +421,7 @@ VLP_EXPORT int vlp_bn_eval_coeffs(int C, const float* gamma, const float* beta, 
 
 VLP_EXPORT int vlp_stat_reduce(int rep, int C, double* a, double* b, double* c, void* stream) {
   if (rep <= 1) return 0;
-  hipLaunchKernelGGL(stat_reduce_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(stat_reduce_kernel, dim3((C + 63) / 64, 3), dim3(256), 0, (hipStream_t)stream,
                      rep, C, a, b, c);
   return (int)hipGetLastError();
 }

@@ -153,6 +153,98 @@ struct ConvDgradA {
   }
 };
 
+// ---- stride-2 data gradient, one pixel-parity class (ph, pw) per launch ----
+// dx pixels h = 2i + ph receive only taps kh = (ph + P) mod 2 + 2a, so the class
+// GEMM has K = ntaps_h * ntaps_w * Co with no masked (zero) MFMA work.
+struct S2Class {
+  int ph, pw, kh0, kw0, nth, ntw, Hc, Wc;
+  FastDiv fd_hwc, fd_wc, fd_ntw;
+};
+static S2Class make_s2class(const ConvGeom& g, int ph, int pw) {
+  S2Class c;
+  c.ph = ph; c.pw = pw;
+  c.kh0 = (ph + g.P) & 1;
+  c.kw0 = (pw + g.P) & 1;
+  c.nth = g.KH > c.kh0 ? (g.KH - c.kh0 + 1) / 2 : 0;
+  c.ntw = g.KW > c.kw0 ? (g.KW - c.kw0 + 1) / 2 : 0;
+  c.Hc = (g.H - ph + 1) / 2;
+  c.Wc = (g.W - pw + 1) / 2;
+  c.fd_hwc = make_fastdiv(c.Hc * c.Wc > 0 ? c.Hc * c.Wc : 1);
+  c.fd_wc = make_fastdiv(c.Wc > 0 ? c.Wc : 1);
+  c.fd_ntw = make_fastdiv(c.ntw > 0 ? c.ntw : 1);
+  return c;
+}
+template <typename T>
+struct ConvDgradS2A {
+  static constexpr bool kKContig = true;
+  static constexpr bool kDirect = true;
+  struct State { const T* base; int hq, wq; bool ok; };   // hq = (h + P) / 2 etc.
+  ConvGeom g; S2Class c; const T* dy; int Mc, Kc;
+  __device__ State fixed(int m) const {
+    State s;
+    s.ok = m < Mc;
+    int mm = s.ok ? m : 0;
+    int n = fdiv(mm, c.fd_hwc);
+    int r = mm - n * c.Hc * c.Wc;
+    int i = fdiv(r, c.fd_wc);
+    int j = r - i * c.Wc;
+    s.base = dy + (size_t)n * g.Ho * g.Wo * g.Co;
+    s.hq = 2 * i + c.ph + g.P;   // h + P
+    s.wq = 2 * j + c.pw + g.P;
+    return s;
+  }
+  __device__ const void* addr(const State& s, int k) const {
+    if (!s.ok || k >= Kc) return zero_page();
+    int tap = fdiv(k, g.fd_co);
+    int co = k - tap * g.Co;
+    int a = fdiv(tap, c.fd_ntw);
+    int b = tap - a * c.ntw;
+    int ho = (s.hq - c.kh0 - 2 * a) >> 1, wo = (s.wq - c.kw0 - 2 * b) >> 1;
+    if ((unsigned)ho >= (unsigned)g.Ho || (unsigned)wo >= (unsigned)g.Wo) return zero_page();
+    return s.base + ((size_t)ho * g.Wo + wo) * g.Co + co;
+  }
+  __device__ uint4 load(const State& s, int k) const {
+    const void* p = addr(s, k);
+    return ldg16(p);
+  }
+};
+// class-local row -> global NHWC row, then the wrapped epilogue
+template <class EP>
+struct EpiS2Remap {
+  static constexpr bool kStats = EP::kStats;
+  double* stat1; double* stat2; int stat_rep;
+  EP inner; S2Class c; int H, W;
+  __device__ void operator()(int row, int col, v4f v, v4f& s1, v4f& s2) const {
+    int n = fdiv(row, c.fd_hwc);
+    int r = row - n * c.Hc * c.Wc;
+    int i = fdiv(r, c.fd_wc);
+    int j = r - i * c.Wc;
+    int grow = (n * H + 2 * i + c.ph) * W + 2 * j + c.pw;
+    inner(grow, col, v, s1, s2);
+  }
+};
+
+// class B operand: B(ci, k = (a, b, co)) = Wt[ci][kh0 + 2a][kw0 + 2b][co]
+template <typename T>
+struct WtS2B {
+  static constexpr bool kKContig = true;
+  static constexpr bool kDirect = true;
+  struct State { const T* p; bool ok; };
+  const T* wt; ConvGeom g; S2Class c; int Kc;
+  __device__ State fixed(int ci) const {
+    return State{wt + (size_t)(ci < g.C ? ci : 0) * g.KH * g.KW * g.Co, ci < g.C};
+  }
+  __device__ const void* addr(const State& s, int k) const {
+    if (!s.ok || k >= Kc) return zero_page();
+    int tap = fdiv(k, g.fd_co);
+    int co = k - tap * g.Co;
+    int a = fdiv(tap, c.fd_ntw);
+    int b = tap - a * c.ntw;
+    return s.p + ((size_t)(c.kh0 + 2 * a) * g.KW + c.kw0 + 2 * b) * g.Co + co;
+  }
+  __device__ uint4 load(const State& s, int k) const { return ldg16(addr(s, k)); }
+};
+
 // ---- weight-gradient B operand: input patches, MN-contiguous over (kh,kw,ci) ----
 template <typename T, bool XF>
 struct ConvWgradB {
@@ -316,15 +408,18 @@ static int gemm_auto(int M, int N, int K, int ksplit, const LA& la, const LB& lb
 // weight-gradient GEMMs: rows = Co, cols = KH*KW*C, reduction = pixels
 template <typename T, class LA, class LB, class EP>
 static int gemm_wgrad(int M, int N, int K, const LA& la, const LB& lb, const EP& ep, hipStream_t st) {
+  // ~1024 workgroups (two waves of the chip at 2 WG/CU), >= 4096 pixels each:
+  // fewer splits = fewer fp32 atomics on the [Co][K] result
+  constexpr int kTargetWG = 1024;
   int tiles = ((M + 127) / 128) * ((N + 127) / 128);
-  int ksplit = (2048 + tiles - 1) / tiles;
-  int maxsplit = (K + 4095) / 4096;     // at least 4096 pixels per split
+  int ksplit = (kTargetWG + tiles - 1) / tiles;
+  int maxsplit = (K + 4095) / 4096;
   if (ksplit > maxsplit) ksplit = maxsplit;
-  if (M <= 64) {
-    tiles = (N + 255) / 256;
-    ksplit = (2048 + tiles - 1) / tiles;
+  if (M <= 64) {   // Co = 64 (stem, layer1): 64 x 128 tiles (K = 576 wastes 11%, not 33%)
+    tiles = (N + 127) / 128;
+    ksplit = (kTargetWG + tiles - 1) / tiles;
     if (ksplit > maxsplit) ksplit = maxsplit;
-    return launch_gemm<T, 64, 256, 1>(M, N, K, ksplit, la, lb, ep, st);
+    return launch_gemm<T, 64, 128, 1>(M, N, K, ksplit, la, lb, ep, st);
   }
   return launch_gemm<T, 128, 128, 2>(M, N, K, ksplit, la, lb, ep, st);
 }
@@ -350,6 +445,29 @@ static int conv_dgrad_t(const void* dy, const void* wt, void* dx, ConvGeom g, co
                         const float* invstd, double* s1, double* s2, int rep, hipStream_t st) {
   g.M = g.N * g.H * g.W;
   g.K = g.KH * g.KW * g.Co;
+  if (g.S == 2) {
+    // four parity classes, each a dense GEMM over its valid taps only
+    for (int ph = 0; ph < 2; ++ph)
+      for (int pw = 0; pw < 2; ++pw) {
+        S2Class c = make_s2class(g, ph, pw);
+        const int Mc = g.N * c.Hc * c.Wc, Kc = c.nth * c.ntw * g.Co;
+        if (Mc <= 0) continue;
+        ConvDgradS2A<T> la{g, c, (const T*)dy, Mc, Kc};
+        WtS2B<T> lb{(const T*)wt, g, c, Kc};
+        int r;
+        if (ybn) {
+          EpiDgradBN<T> in{s1, s2, rep, (T*)dx, g.C, (const T*)ybn, sc, sh, mean, invstd};
+          EpiS2Remap<EpiDgradBN<T>> ep{s1, s2, rep, in, c, g.H, g.W};
+          r = gemm_auto<T>(Mc, g.C, Kc, 1, la, lb, ep, st);
+        } else {
+          EpiDgradAdd<T> in{nullptr, nullptr, (T*)dx, (const T*)addend, g.C};
+          EpiS2Remap<EpiDgradAdd<T>> ep{nullptr, nullptr, 1, in, c, g.H, g.W};
+          r = gemm_auto<T>(Mc, g.C, Kc, 1, la, lb, ep, st);
+        }
+        if (r) return r;
+      }
+    return 0;
+  }
   ConvDgradA<T> la{g, (const T*)dy};
   KMat<T> lb{(const T*)wt, g.K, g.C, g.K};
   if (ybn) {

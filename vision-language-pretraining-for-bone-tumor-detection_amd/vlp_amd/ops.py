@@ -34,7 +34,7 @@ def _tile_auto(n):
 
 
 def _tile_wgrad(m):
-    return "64x256" if m <= 64 else "128x128"
+    return "64x128" if m <= 64 else "128x128"
 
 
 def _tile_lin(m, n):
