@@ -72,9 +72,9 @@ struct EpiLinearBwd {
 template <typename T, class LA, class LB, class EP>
 static int gemm_lin(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
                     hipStream_t st) {
-  if (N <= 64) return launch_gemm<T, 256, 64, 4>(M, N, K, ksplit, la, lb, ep, st);
+  if (N <= 64) return gemm_narrow<T>(M, N, K, ksplit, la, lb, ep, st);
   if (M <= 1024) return launch_gemm<T, 64, 256, 1>(M, N, K, ksplit, la, lb, ep, st);
-  return launch_gemm<T, 128, 128, 2>(M, N, K, ksplit, la, lb, ep, st);
+  return gemm_wide<T>(M, N, K, ksplit, la, lb, ep, st);
 }
 
 // ---------------- LayerNorm over rows of D ----------------
@@ -364,7 +364,7 @@ VLP_EXPORT int vlp_linear_wgrad(int dtype, int M, int Nout, int Kin, const void*
   if (dtype == VLP_BF16) {
     MNMat<bf16> la{(const bf16*)dy, lddy, Nout, M};
     MNMat<bf16> lb{(const bf16*)x, ldx, Kin, M};
-    return launch_gemm<bf16, 128, 128, 2>(Nout, Kin, M, ksplit, la, lb, ep, st);
+    return gemm_wide<bf16>(Nout, Kin, M, ksplit, la, lb, ep, st);
   }
   MNMat<float> la{(const float*)dy, lddy, Nout, M};
   MNMat<float> lb{(const float*)x, ldx, Kin, M};

@@ -91,25 +91,25 @@ __device__ __forceinline__ v4f load4(const bf16* p) {
 }
 __device__ __forceinline__ v4f load4(const float* p) { return *reinterpret_cast<const v4f*>(p); }
 
-// Unsigned division by a runtime constant (n < 2^31, d >= 1): q = umulhi(n, mul) >> sh.
+// Unsigned division by a runtime constant (n < 2^31, d >= 1), branch-free
+// (Granlund-Montgomery round-up): t = umulhi(n, mul); q = (t + ((n - t) >> s1)) >> s2.
 struct FastDiv {
-  uint32_t d, mul, sh;
+  uint32_t d, mul, s1, s2;
 };
 inline FastDiv make_fastdiv(uint32_t d) {
   FastDiv f;
   f.d = d;
-  if (d == 1) { f.mul = 0; f.sh = 0; return f; }
   uint32_t l = 0;
   while ((1ull << l) < d) ++l;  // l = ceil(log2 d)
   uint64_t m = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
-  f.mul = (uint32_t)m;
-  f.sh = l - 1;
+  f.mul = (uint32_t)m;          // d == 1: mul = 1, s1 = s2 = 0 -> q = n
+  f.s1 = l < 1 ? l : 1;
+  f.s2 = l > 1 ? l - 1 : 0;
   return f;
 }
 __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
-  if (f.d == 1) return n;
   uint32_t t = __umulhi(n, f.mul);
-  return (t + ((n - t) >> 1)) >> f.sh;
+  return (t + ((n - t) >> f.s1)) >> f.s2;
 }
 
 __device__ __forceinline__ float warp_sum(float v) {

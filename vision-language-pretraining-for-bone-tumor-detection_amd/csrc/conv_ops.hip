@@ -55,10 +55,18 @@ __device__ __forceinline__ uint4 xform_chunk(uint4 v, const float* sc, const flo
   return Chunk<T>::pack(f);
 }
 
+// Loaders carry two protocols (gemm.h): fixed/load (register staging: fp32
+// parity mode, BN-on-load) and start/next (incremental direct-to-LDS, bf16).
+// The direct path requires the channel count to be a multiple of the K-step
+// (64), so a K-step never straddles a filter tap and (kh, kw, channel offset)
+// are wave-uniform scalars; every ResNet34 conv except the stem satisfies it
+// (the stem has its own loaders).
+
 // ---- forward A operand: input patches, K-contiguous ----
 template <typename T, bool XF>
 struct ConvFwdA {
   static constexpr bool kKContig = true;
+  static constexpr bool kDirect = !XF;
   struct State { const T* base; int hi0, wi0; bool ok; };
   ConvGeom g; const T* x; const float* sc; const float* sh;
   __device__ State fixed(int m) const {
@@ -86,23 +94,32 @@ struct ConvFwdA {
     if constexpr (XF) v = xform_chunk<T>(v, sc, sh, ci);
     return v;
   }
-  static constexpr bool kDirect = !XF;
-  __device__ const void* addr(const State& s, int k) const {
-    if (!s.ok || k >= g.K) return zero_page();
-    int tap = fdiv(k, g.fd_c);
-    int ci = k - tap * g.C;
-    int kh = fdiv(tap, g.fd_kw);
-    int kw = tap - kh * g.KW;
-    int hi = s.hi0 + kh, wi = s.wi0 + kw;
-    if ((unsigned)hi >= (unsigned)g.H || (unsigned)wi >= (unsigned)g.W) return zero_page();
-    return s.base + ((size_t)hi * g.W + wi) * g.C + ci;
+  struct DState { long long off; int hi0, wi0; bool ok; };
+  __device__ DState start(int m, int koff, int) const {
+    State f = fixed(m);
+    DState d;
+    d.ok = f.ok; d.hi0 = f.hi0; d.wi0 = f.wi0;
+    d.off = (long long)(f.base - x) + ((long long)f.hi0 * g.W + f.wi0) * g.C + koff;
+    return d;
+  }
+  struct Step { long long delta; int kh, kw; bool kv; };   // K-step-uniform tap
+  __device__ Step step(int k0) const {
+    const int tap = fdiv(k0, g.fd_c), ci0 = k0 - tap * g.C;
+    const int kh = fdiv(tap, g.fd_kw), kw = tap - kh * g.KW;
+    return Step{((long long)kh * g.W + kw) * g.C + ci0, kh, kw, k0 < g.K};
+  }
+  __device__ const void* next(DState& d, const Step& s) const {
+    const bool v = d.ok & s.kv & ((unsigned)(d.hi0 + s.kh) < (unsigned)g.H) &
+                   ((unsigned)(d.wi0 + s.kw) < (unsigned)g.W);
+    return v ? (const void*)(x + d.off + s.delta) : zero_page();
   }
 };
 
-// ---- data-gradient A operand: output-gradient "patches", K-contiguous ----
+// ---- data-gradient A operand (stride 1): output-gradient "patches", K-contiguous ----
 template <typename T>
 struct ConvDgradA {
   static constexpr bool kKContig = true;
+  static constexpr bool kDirect = true;
   struct State { const T* base; int hp, wp; bool ok; };
   ConvGeom g; const T* dy;
   __device__ State fixed(int m) const {
@@ -134,22 +151,24 @@ struct ConvDgradA {
     if (ho >= g.Ho || wo >= g.Wo) return zero4();
     return ldg16(s.base + ((size_t)ho * g.Wo + wo) * g.Co + co);
   }
-  static constexpr bool kDirect = true;
-  __device__ const void* addr(const State& s, int k) const {
-    if (!s.ok || k >= g.K) return zero_page();
-    int tap = fdiv(k, g.fd_co);
-    int co = k - tap * g.Co;
-    int kh = fdiv(tap, g.fd_kw);
-    int kw = tap - kh * g.KW;
-    int th = s.hp - kh, tw = s.wp - kw;
-    if (th < 0 || tw < 0) return zero_page();
-    int ho = th, wo = tw;
-    if (g.S != 1) {
-      if ((th % g.S) | (tw % g.S)) return zero_page();
-      ho = th / g.S; wo = tw / g.S;
-    }
-    if (ho >= g.Ho || wo >= g.Wo) return zero_page();
-    return s.base + ((size_t)ho * g.Wo + wo) * g.Co + co;
+  struct DState { long long off; int hp, wp; bool ok; };
+  __device__ DState start(int m, int koff, int) const {
+    State f = fixed(m);
+    DState d;
+    d.ok = f.ok; d.hp = f.hp; d.wp = f.wp;
+    d.off = (long long)(f.base - dy) + ((long long)f.hp * g.Wo + f.wp) * g.Co + koff;
+    return d;
+  }
+  struct Step { long long delta; int kh, kw; bool kv; };
+  __device__ Step step(int k0) const {   // stride-1 only (S=2: ConvDgradS2A)
+    const int tap = fdiv(k0, g.fd_co), co0 = k0 - tap * g.Co;
+    const int kh = fdiv(tap, g.fd_kw), kw = tap - kh * g.KW;
+    return Step{co0 - ((long long)kh * g.Wo + kw) * g.Co, kh, kw, k0 < g.K};
+  }
+  __device__ const void* next(DState& d, const Step& s) const {
+    const bool v = d.ok & s.kv & ((unsigned)(d.hp - s.kh) < (unsigned)g.Ho) &
+                   ((unsigned)(d.wp - s.kw) < (unsigned)g.Wo);
+    return v ? (const void*)(dy + d.off + s.delta) : zero_page();
   }
 };
 
@@ -178,7 +197,7 @@ template <typename T>
 struct ConvDgradS2A {
   static constexpr bool kKContig = true;
   static constexpr bool kDirect = true;
-  struct State { const T* base; int hq, wq; bool ok; };   // hq = (h + P) / 2 etc.
+  struct State { const T* base; int hb, wb; bool ok; };   // hb = (h + P - kh0) / 2
   ConvGeom g; S2Class c; const T* dy; int Mc, Kc;
   __device__ State fixed(int m) const {
     State s;
@@ -189,23 +208,38 @@ struct ConvDgradS2A {
     int i = fdiv(r, c.fd_wc);
     int j = r - i * c.Wc;
     s.base = dy + (size_t)n * g.Ho * g.Wo * g.Co;
-    s.hq = 2 * i + c.ph + g.P;   // h + P
-    s.wq = 2 * j + c.pw + g.P;
+    s.hb = (2 * i + c.ph + g.P - c.kh0) >> 1;
+    s.wb = (2 * j + c.pw + g.P - c.kw0) >> 1;
     return s;
   }
-  __device__ const void* addr(const State& s, int k) const {
-    if (!s.ok || k >= Kc) return zero_page();
+  __device__ uint4 load(const State& s, int k) const {
+    if (!s.ok || k >= Kc) return zero4();
     int tap = fdiv(k, g.fd_co);
     int co = k - tap * g.Co;
     int a = fdiv(tap, c.fd_ntw);
     int b = tap - a * c.ntw;
-    int ho = (s.hq - c.kh0 - 2 * a) >> 1, wo = (s.wq - c.kw0 - 2 * b) >> 1;
-    if ((unsigned)ho >= (unsigned)g.Ho || (unsigned)wo >= (unsigned)g.Wo) return zero_page();
-    return s.base + ((size_t)ho * g.Wo + wo) * g.Co + co;
+    int ho = s.hb - a, wo = s.wb - b;
+    if ((unsigned)ho >= (unsigned)g.Ho || (unsigned)wo >= (unsigned)g.Wo) return zero4();
+    return ldg16(s.base + ((size_t)ho * g.Wo + wo) * g.Co + co);
   }
-  __device__ uint4 load(const State& s, int k) const {
-    const void* p = addr(s, k);
-    return ldg16(p);
+  struct DState { long long off; int hb, wb; bool ok; };
+  __device__ DState start(int m, int koff, int) const {
+    State f = fixed(m);
+    DState d;
+    d.ok = f.ok; d.hb = f.hb; d.wb = f.wb;
+    d.off = (long long)(f.base - dy) + ((long long)f.hb * g.Wo + f.wb) * g.Co + koff;
+    return d;
+  }
+  struct Step { long long delta; int a, b; bool kv; };
+  __device__ Step step(int k0) const {
+    const int tap = fdiv(k0, g.fd_co), co0 = k0 - tap * g.Co;
+    const int a = fdiv(tap, c.fd_ntw), b = tap - a * c.ntw;
+    return Step{co0 - ((long long)a * g.Wo + b) * g.Co, a, b, k0 < Kc};
+  }
+  __device__ const void* next(DState& d, const Step& s) const {
+    const bool v = d.ok & s.kv & ((unsigned)(d.hb - s.a) < (unsigned)g.Ho) &
+                   ((unsigned)(d.wb - s.b) < (unsigned)g.Wo);
+    return v ? (const void*)(dy + d.off + s.delta) : zero_page();
   }
 };
 // class-local row -> global NHWC row, then the wrapped epilogue
@@ -223,7 +257,6 @@ struct EpiS2Remap {
     inner(grow, col, v, s1, s2);
   }
 };
-
 // class B operand: B(ci, k = (a, b, co)) = Wt[ci][kh0 + 2a][kw0 + 2b][co]
 template <typename T>
 struct WtS2B {
@@ -234,23 +267,45 @@ struct WtS2B {
   __device__ State fixed(int ci) const {
     return State{wt + (size_t)(ci < g.C ? ci : 0) * g.KH * g.KW * g.Co, ci < g.C};
   }
-  __device__ const void* addr(const State& s, int k) const {
-    if (!s.ok || k >= Kc) return zero_page();
+  __device__ uint4 load(const State& s, int k) const {
+    if (!s.ok || k >= Kc) return zero4();
     int tap = fdiv(k, g.fd_co);
     int co = k - tap * g.Co;
     int a = fdiv(tap, c.fd_ntw);
     int b = tap - a * c.ntw;
-    return s.p + ((size_t)(c.kh0 + 2 * a) * g.KW + c.kw0 + 2 * b) * g.Co + co;
+    return ldg16(s.p + ((size_t)(c.kh0 + 2 * a) * g.KW + c.kw0 + 2 * b) * g.Co + co);
   }
-  __device__ uint4 load(const State& s, int k) const { return ldg16(addr(s, k)); }
+  struct DState { const T* p; bool ok; };
+  __device__ DState start(int ci, int koff, int) const {
+    State f = fixed(ci);
+    return DState{f.p + koff, f.ok};
+  }
+  struct Step { long long delta; bool kv; };
+  __device__ Step step(int k0) const {
+    const int tap = fdiv(k0, g.fd_co), co0 = k0 - tap * g.Co;
+    const int a = fdiv(tap, c.fd_ntw), b = tap - a * c.ntw;
+    return Step{((long long)(c.kh0 + 2 * a) * g.KW + c.kw0 + 2 * b) * g.Co + co0, k0 < Kc};
+  }
+  __device__ const void* next(DState& d, const Step& s) const {
+    return (d.ok & s.kv) ? (const void*)(d.p + s.delta) : zero_page();
+  }
 };
 
 // ---- weight-gradient B operand: input patches, MN-contiguous over (kh,kw,ci) ----
+// The reduction runs over output pixels; the direct path walks each chunk's
+// pixel (n, ho, wo) incrementally, BK pixels per K-step (constant carries).
+struct PixStep {
+  int dwo, dho;          // BK = dho*Wo + dwo
+  long long d_wo, d_ho;  // element deltas per unit of wo / ho in the input image
+  long long carry_w, carry_h;  // deltas applied when wo / ho wrap
+  int small;             // Ho*Wo <= BK: recompute by division instead
+};
 template <typename T, bool XF>
 struct ConvWgradB {
   static constexpr bool kKContig = false;
+  static constexpr bool kDirect = !XF;
   struct State { int kh, kw, ci; bool ok; };
-  ConvGeom g; const T* x; const float* sc; const float* sh; int Kcols;
+  ConvGeom g; const T* x; const float* sc; const float* sh; int Kcols; PixStep ps;
   __device__ State fixed(int col) const {
     State s;
     s.ok = col < Kcols;
@@ -273,18 +328,56 @@ struct ConvWgradB {
     if constexpr (XF) v = xform_chunk<T>(v, sc, sh, s.ci);
     return v;
   }
-  static constexpr bool kDirect = !XF;
-  __device__ const void* addr(const State& s, int m) const {
-    if (!s.ok || m >= g.M) return zero_page();
-    int n = fdiv(m, g.fd_howo);
-    int r = m - n * g.Ho * g.Wo;
+  struct DState { long long off; int hi, wi, mm, kh, kw, ci; bool ok; };
+  __device__ void locate(DState& d) const {
+    int mm = d.mm < g.M ? d.mm : 0;
+    int n = fdiv(mm, g.fd_howo);
+    int r = mm - n * g.Ho * g.Wo;
     int ho = fdiv(r, g.fd_wo);
     int wo = r - ho * g.Wo;
-    int hi = ho * g.S - g.P + s.kh, wi = wo * g.S - g.P + s.kw;
-    if ((unsigned)hi >= (unsigned)g.H || (unsigned)wi >= (unsigned)g.W) return zero_page();
-    return x + (((size_t)n * g.H + hi) * g.W + wi) * g.C + s.ci;
+    d.hi = ho * g.S - g.P + d.kh;
+    d.wi = wo * g.S - g.P + d.kw;
+    d.off = (((long long)n * g.H + d.hi) * g.W + d.wi) * g.C;
+  }
+  __device__ DState start(int col, int koff, int kb) const {
+    State f = fixed(col);
+    DState d;
+    d.ok = f.ok; d.kh = f.kh; d.kw = f.kw; d.ci = f.ci; d.mm = kb + koff;
+    locate(d);
+    d.off += f.ci;
+    return d;
+  }
+  struct Step {};
+  __device__ Step step(int) const { return Step{}; }
+  __device__ const void* next(DState& d, const Step&) const {
+    const bool v = d.ok && d.mm < g.M && (unsigned)d.hi < (unsigned)g.H && (unsigned)d.wi < (unsigned)g.W;
+    const void* r = v ? (const void*)(x + d.off) : zero_page();
+    d.mm += Elem<T>::BK;
+    if (ps.small) {   // tiny images (Ho*Wo <= BK): recompute
+      locate(d);
+      d.off += d.ci;
+    } else {
+      const int wo = (d.wi - d.kw + g.P) / g.S + ps.dwo;
+      d.wi += ps.dwo * g.S; d.hi += ps.dho * g.S;
+      d.off += ps.dwo * ps.d_wo + ps.dho * ps.d_ho;
+      if (wo >= g.Wo) { d.wi -= g.Wo * g.S; d.hi += g.S; d.off += ps.carry_w; }
+      const int ho = (d.hi - d.kh + g.P) / g.S;
+      if (ho >= g.Ho) { d.hi -= g.Ho * g.S; d.off += ps.carry_h; }
+    }
+    return r;
   }
 };
+static PixStep make_pixstep(const ConvGeom& g, int BK) {
+  PixStep p;
+  p.small = g.Ho * g.Wo <= BK;
+  p.dho = BK / g.Wo;
+  p.dwo = BK % g.Wo;
+  p.d_wo = (long long)g.S * g.C;
+  p.d_ho = (long long)g.S * g.W * g.C;
+  p.carry_w = (long long)g.S * g.W * g.C - (long long)g.Wo * g.S * g.C;            // wo -= Wo, ho += 1
+  p.carry_h = (long long)g.H * g.W * g.C - (long long)g.Ho * g.S * g.W * g.C;      // ho -= Ho, n += 1
+  return p;
+}
 
 // ---- stem (7x7/2, 3 input channels) on a zero-padded NHWC4 image ----
 // Xp[n][Hp][Wp][4] with the 3-pixel top/left padding materialised; K layout
@@ -296,6 +389,7 @@ struct StemGeom {
 template <typename T>
 struct StemA {
   static constexpr bool kKContig = true;
+  static constexpr bool kDirect = true;
   struct State { const T* base; bool ok; };
   StemGeom g; const T* xp;
   __device__ State fixed(int m) const {
@@ -314,16 +408,21 @@ struct StemA {
     if (!s.ok || kh >= 7) return zero4();
     return ldg16(s.base + ((size_t)kh * g.Wp + kw) * 4);
   }
-  static constexpr bool kDirect = true;
-  __device__ const void* addr(const State& s, int k) const {
-    int kh = k >> 5, kw = (k & 31) >> 2;
-    if (!s.ok || kh >= 7) return zero_page();
-    return s.base + ((size_t)kh * g.Wp + kw) * 4;
+  struct DState { const T* p; int khc; bool ok; };
+  __device__ DState start(int m, int koff, int) const {
+    State f = fixed(m);
+    return DState{f.base + ((size_t)(koff >> 5) * g.Wp + ((koff & 31) >> 2)) * 4, koff >> 5, f.ok};
+  }
+  struct Step { int kh; long long delta; };
+  __device__ Step step(int k0) const { return Step{k0 >> 5, (long long)(k0 >> 5) * g.Wp * 4}; }
+  __device__ const void* next(DState& d, const Step& s) const {
+    return (d.ok & (s.kh + d.khc < 7)) ? (const void*)(d.p + s.delta) : zero_page();
   }
 };
 template <typename T>
 struct StemWgradB {
   static constexpr bool kKContig = false;
+  static constexpr bool kDirect = true;
   struct State { int off; bool ok; };
   StemGeom g; const T* xp;
   __device__ State fixed(int col) const {
@@ -338,14 +437,22 @@ struct StemWgradB {
     int wo = r - ho * g.Wo;
     return ldg16(xp + (((size_t)n * g.Hp + 2 * ho) * g.Wp + 2 * wo) * 4 + s.off);
   }
-  static constexpr bool kDirect = true;
-  __device__ const void* addr(const State& s, int m) const {
-    if (!s.ok || m >= g.M) return zero_page();
+  struct DState { int off, mm; bool ok; };
+  __device__ DState start(int col, int koff, int kb) const {
+    State f = fixed(col);
+    return DState{f.off, kb + koff, f.ok};
+  }
+  struct Step {};
+  __device__ Step step(int) const { return Step{}; }
+  __device__ const void* next(DState& d, const Step&) const {
+    const int m = d.mm;
+    d.mm += Elem<T>::BK;
+    if (!d.ok || m >= g.M) return zero_page();
     int n = fdiv(m, g.fd_howo);
     int r = m - n * g.Ho * g.Wo;
     int ho = fdiv(r, g.fd_wo);
     int wo = r - ho * g.Wo;
-    return xp + (((size_t)n * g.Hp + 2 * ho) * g.Wp + 2 * wo) * 4 + s.off;
+    return xp + (((size_t)n * g.Hp + 2 * ho) * g.Wp + 2 * wo) * 4 + d.off;
   }
 };
 
@@ -401,9 +508,8 @@ struct EpiDgradAdd {
 template <typename T, class LA, class LB, class EP>
 static int gemm_auto(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
                      hipStream_t st) {
-  if (N <= 64)
-    return launch_gemm<T, 256, 64, 4>(M, N, K, ksplit, la, lb, ep, st);
-  return launch_gemm<T, 128, 128, 2>(M, N, K, ksplit, la, lb, ep, st);
+  if (N <= 64) return gemm_narrow<T>(M, N, K, ksplit, la, lb, ep, st);
+  return gemm_wide<T>(M, N, K, ksplit, la, lb, ep, st);
 }
 // weight-gradient GEMMs: rows = Co, cols = KH*KW*C, reduction = pixels
 template <typename T, class LA, class LB, class EP>
@@ -419,9 +525,9 @@ static int gemm_wgrad(int M, int N, int K, const LA& la, const LB& lb, const EP&
     tiles = (N + 127) / 128;
     ksplit = (kTargetWG + tiles - 1) / tiles;
     if (ksplit > maxsplit) ksplit = maxsplit;
-    return launch_gemm<T, 64, 128, 1>(M, N, K, ksplit, la, lb, ep, st);
+    return gemm_short<T>(M, N, K, ksplit, la, lb, ep, st);
   }
-  return launch_gemm<T, 128, 128, 2>(M, N, K, ksplit, la, lb, ep, st);
+  return gemm_wide<T>(M, N, K, ksplit, la, lb, ep, st);
 }
 
 template <typename T>
@@ -486,10 +592,10 @@ static int conv_wgrad_t(const void* dy, const void* x, float* dw, ConvGeom g, co
   MNMat<T> la{(const T*)dy, g.Co, g.Co, g.M};
   EpiAtomic ep{nullptr, nullptr, dw, g.K, 1.0f};
   if (sc) {
-    ConvWgradB<T, true> lb{g, (const T*)x, sc, sh, g.K};
+    ConvWgradB<T, true> lb{g, (const T*)x, sc, sh, g.K, make_pixstep(g, Elem<T>::BK)};
     return gemm_wgrad<T>(g.Co, g.K, g.M, la, lb, ep, st);
   }
-  ConvWgradB<T, false> lb{g, (const T*)x, nullptr, nullptr, g.K};
+  ConvWgradB<T, false> lb{g, (const T*)x, nullptr, nullptr, g.K, make_pixstep(g, Elem<T>::BK)};
   return gemm_wgrad<T>(g.Co, g.K, g.M, la, lb, ep, st);
 }
 
@@ -625,7 +731,7 @@ VLP_EXPORT int vlp_stem_fwd(int dtype, const void* xp, const void* wp, void* y, 
     StemA<bf16> la{g, (const bf16*)xp};
     KMat<bf16> lb{(const bf16*)wp, 256, 64, 256};
     EpiConvFwd<bf16> ep{stat_sum, stat_sumsq, stat_rep, (bf16*)y, 64};
-    return launch_gemm<bf16, 256, 64, 4>(g.M, 64, 256, 1, la, lb, ep, st);
+    return gemm_narrow<bf16>(g.M, 64, 256, 1, la, lb, ep, st);
   }
   StemA<float> la{g, (const float*)xp};
   KMat<float> lb{(const float*)wp, 256, 64, 256};

@@ -106,13 +106,23 @@ struct Stager {
 };
 
 // ---------------- direct-to-LDS staging (bf16) ----------------
-// Loaders that can name the global address of a chunk (kDirect = true,
-// `const void* addr(State, k)`; out-of-range chunks point at a zero page)
-// are staged with global_load_lds_dwordx4: each wave-instruction writes 1 KiB
-// of LDS lane-linearly, so lane L of instruction i fills PHYSICAL chunk
+// Loaders that can name the global address of a chunk (kDirect = true) are
+// staged with global_load_lds_dwordx4: each wave-instruction writes 1 KiB of
+// LDS lane-linearly, so lane L of instruction i fills PHYSICAL chunk
 // q = (wave*NI + i)*64 + L and fetches the LOGICAL chunk that the XOR swizzle
 // places there (the swizzles are involutions).  No staging registers, no
 // ds_write pass; the loads of tile t+1 fly while tile t is multiplied.
+//
+// Direct loaders are INCREMENTAL (profiling showed ~8 VALU per MFMA when every
+// chunk address was rebuilt from scratch each K-step):
+//   DState start(int coord, int koff, int kb)  once per chunk: coord = the
+//        operand row (K-contig) or first row of the chunk (MN-contig), koff = the
+//        chunk's k offset inside a K-step, kb = the first K-step's base
+//   Step step(int k0)                           once per K-step per wave: the
+//        k0-only context (conv tap, channel offset, K bound) -- wave-uniform,
+//        so it lives in scalar registers and is shared by all NI chunks
+//   const void* next(DState&, const Step&)     per chunk per K-step: the
+//        chunk's address or the zero page (branch-free select); advances state
 static __device__ uint4 g_zero16;
 __device__ __forceinline__ const void* zero_page() { return &g_zero16; }
 
@@ -125,10 +135,9 @@ template <typename T, int BM, class L>
 struct GStager {
   using G = TileGeom<T, BM, L::kKContig>;
   static constexpr int NI = G::NCH;
-  typename L::State st[NI];
-  int koff[NI];
+  typename L::DState st[NI];
 
-  __device__ __forceinline__ void init(const L& ld, int row0) {
+  __device__ __forceinline__ void init(const L& ld, int row0, int kb) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
@@ -136,23 +145,22 @@ struct GStager {
       if constexpr (L::kKContig) {
         const int r = q >> 3, p = q & 7;
         const int c = p ^ ((r >> 1) & 7);
-        st[i] = ld.fixed(row0 + r);
-        koff[i] = c * G::EPC;
+        st[i] = ld.start(row0 + r, c * G::EPC, kb);
       } else {
         const int o = q * 16;
         const int k = o / G::RB, inrow = o % G::RB;
         const int sw = (G::RB >= 256) ? (k & 7) : ((k >> 1) & 3);
         const int b = (inrow >> 5) ^ sw, half = (inrow >> 4) & 1;
-        st[i] = ld.fixed(row0 + (2 * b + half) * G::EPC);
-        koff[i] = k;
+        st[i] = ld.start(row0 + (2 * b + half) * G::EPC, k, kb);
       }
     }
   }
-  __device__ __forceinline__ void issue(const L& ld, int k0, char* lds) const {
+  __device__ __forceinline__ void issue(const L& ld, int k0, char* lds) {
     const int w = threadIdx.x >> 6;
+    const auto stp = ld.step(k0);   // K-step-uniform context (scalar registers)
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const void* p = ld.addr(st[i], k0 + koff[i]);
+      const void* p = ld.next(st[i], stp);
       __builtin_amdgcn_global_load_lds(p, (__attribute__((address_space(3))) void*)(lds + (w * NI + i) * 1024),
                                        16, 0, 0);
     }
@@ -166,14 +174,14 @@ struct OpStager;
 template <typename T, int BM, class L>
 struct OpStager<T, BM, L, false> {
   Stager<T, BM, L> s;
-  __device__ __forceinline__ void init(const L& ld, int row0) { s.init(ld, row0); }
+  __device__ __forceinline__ void init(const L& ld, int row0, int) { s.init(ld, row0); }
   __device__ __forceinline__ void prefetch(const L& ld, int k0, char*) { s.load(ld, k0); }
   __device__ __forceinline__ void commit(char* lds) const { s.store(lds); }
 };
 template <typename T, int BM, class L>
 struct OpStager<T, BM, L, true> {
   GStager<T, BM, L> s;
-  __device__ __forceinline__ void init(const L& ld, int row0) { s.init(ld, row0); }
+  __device__ __forceinline__ void init(const L& ld, int row0, int kb) { s.init(ld, row0, kb); }
   __device__ __forceinline__ void prefetch(const L& ld, int k0, char* lds) { s.issue(ld, k0, lds); }
   __device__ __forceinline__ void commit(char*) const {}
 };
@@ -259,8 +267,8 @@ gemm_kernel(GemmShape sh, LA la, LB lb, EP ep) {
 
   OpStager<T, BM, LA> sa;
   OpStager<T, BN, LB> sb;
-  sa.init(la, row0);
-  sb.init(lb, col0);
+  sa.init(la, row0, kb);
+  sb.init(lb, col0, kb);
 
   v4f acc[MB][NB];
 #pragma unroll
@@ -377,8 +385,297 @@ gemm_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   }
 }
 
+// ---------------- multi-stage direct-to-LDS kernel (bf16) ----------------
+// S-slot LDS ring: tiles t+1 .. t+S-2 stay in flight while tile t is
+// multiplied.  Per K-step: wait (counted vmcnt: this wave's loads of tile t
+// have landed), raw s_barrier (every wave's have; every wave finished tile
+// t-1, whose slot is refilled next), issue tile t+S-1, compute tile t.  A
+// __syncthreads() would drain the ring (an LDS-DMA is a pending VM op), so
+// the wait and barrier are explicit.
+template <typename T, int BM, class L, int NT>
+struct GStagerN {
+  using G = TileGeom<T, BM, L::kKContig>;
+  static constexpr int NI = BM * 8 / NT;   // 16-B chunks (= 1 KiB wave-instructions) per thread
+  static_assert(NI >= 1 && (BM * 8) % NT == 0, "tile / thread geometry");
+  typename L::DState st[NI];
+  __device__ __forceinline__ void init(const L& ld, int row0, int kb) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int q = (w * NI + i) * 64 + lane;
+      if constexpr (L::kKContig) {
+        const int r = q >> 3, p = q & 7;
+        st[i] = ld.start(row0 + r, (p ^ ((r >> 1) & 7)) * G::EPC, kb);
+      } else {
+        const int o = q * 16;
+        const int k = o / G::RB, inrow = o % G::RB;
+        const int sw = (G::RB >= 256) ? (k & 7) : ((k >> 1) & 3);
+        const int b = (inrow >> 5) ^ sw, half = (inrow >> 4) & 1;
+        st[i] = ld.start(row0 + (2 * b + half) * G::EPC, k, kb);
+      }
+    }
+  }
+  __device__ __forceinline__ void issue(const L& ld, int k0, char* lds) {
+    const int w = threadIdx.x >> 6;
+    const auto stp = ld.step(k0);   // K-step-uniform context (scalar registers)
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const void* p = ld.next(st[i], stp);
+      __builtin_amdgcn_global_load_lds(p, (__attribute__((address_space(3))) void*)(lds + (w * NI + i) * 1024),
+                                       16, 0, 0);
+    }
+  }
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
+
+template <int BM, int BN, int WGM, int WGN, int S, class LA, class LB, class EP>
+__global__ void __launch_bounds__(WGM * WGN * 64)
+gemm_ms_kernel(GemmShape sh, LA la, LB lb, EP ep) {
+  using T = bf16;
+  constexpr int NT = WGM * WGN * 64;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int MB = WTM / 16, NB = WTN / 16;
+  constexpr int BK = 64;
+  using GA = TileGeom<T, BM, LA::kKContig>;
+  using GB = TileGeom<T, BN, LB::kKContig>;
+  constexpr int ABYTES = BM * 128;
+  constexpr int STAGE = (BM + BN) * 128;
+  using SA = GStagerN<T, BM, LA, NT>;
+  using SB = GStagerN<T, BN, LB, NT>;
+  constexpr int NI = SA::NI + SB::NI;   // VM ops per thread per tile
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int nwg = sh.tiles_m * sh.tiles_n;
+  const int bid = blockIdx.x;
+  int wid = bid;
+  if (nwg >= 16) {
+    const int xcd = bid & 7, idx = bid >> 3, q = nwg >> 3, rr = nwg & 7;
+    wid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
+  }
+  const int tm = wid / sh.tiles_n, tn = wid - tm * sh.tiles_n;
+  const int row0 = tm * BM, col0 = tn * BN;
+  const int kb = blockIdx.y * sh.kchunk;
+  int ke = kb + sh.kchunk;
+  if (ke > sh.K) ke = sh.K;
+  const int nk = (ke - kb + BK - 1) / BK;
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave / WGN, wn = wave - wm * WGN;
+
+  SA sa;
+  SB sb;
+  sa.init(la, row0, kb);
+  sb.init(lb, col0, kb);
+  v4f acc[MB][NB];
+#pragma unroll
+  for (int a = 0; a < MB; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[a][b] = v4f{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s) {
+    if (s < nk) {
+      sa.issue(la, kb + s * BK, smem + s * STAGE);
+      sb.issue(lb, kb + s * BK, smem + s * STAGE + ABYTES);
+    }
+  }
+  int slot = 0;                 // slot of tile t
+  int fill = S - 1;             // slot receiving tile t + S - 1
+  for (int t = 0; t < nk; ++t) {
+    // tiles issued after t so far: min(t + S - 2, nk - 1) - t
+    const int ahead = (t + S - 2 < nk - 1 ? S - 2 : nk - 1 - t);
+    if constexpr (S >= 4) {
+      if (ahead >= 2) wait_vmcnt<2 * NI>();
+      else if (ahead == 1) wait_vmcnt<NI>();
+      else wait_vmcnt<0>();
+    } else if constexpr (S == 3) {
+      if (ahead >= 1) wait_vmcnt<NI>();
+      else wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    raw_barrier();
+    if (t + S - 1 < nk) {
+      char* f = smem + fill * STAGE;
+      sa.issue(la, kb + (t + S - 1) * BK, f);
+      sb.issue(lb, kb + (t + S - 1) * BK, f + ABYTES);
+    }
+    const char* ia = smem + slot * STAGE;
+    const char* ib = ia + ABYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      v8bf fa[MB], fb[NB];
+#pragma unroll
+      for (int a = 0; a < MB; ++a) fa[a] = frag_bf16<LA::kKContig, GA::RB>(ia, wm * WTM + a * 16, s);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) fb[b] = frag_bf16<LB::kKContig, GB::RB>(ib, wn * WTN + b * 16, s);
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], acc[a][b], 0, 0, 0);
+    }
+    slot = (slot + 1 == S) ? 0 : slot + 1;
+    fill = (fill + 1 == S) ? 0 : fill + 1;
+  }
+  __syncthreads();   // all waves done with the ring before the epilogue reuses LDS
+
+  const int l = threadIdx.x & 63;
+  const int li = l & 15, lg = l >> 4;
+  float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int col = col0 + wn * WTN + b * 16 + 4 * lg;
+    v4f s1 = v4f{0.f, 0.f, 0.f, 0.f}, s2 = s1;
+#pragma unroll
+    for (int a = 0; a < MB; ++a) {
+      const int row = row0 + wm * WTM + a * 16 + li;
+      if (row < sh.M && col < sh.N) {
+        v4f c1 = v4f{0.f, 0.f, 0.f, 0.f}, c2 = c1;
+        ep(row, col, acc[a][b], c1, c2);
+        if constexpr (EP::kStats) { s1 += c1; s2 += c2; }
+      }
+    }
+    if constexpr (EP::kStats) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float x = s1[j], y = s2[j];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          x += __shfl_xor(x, o, 64);
+          y += __shfl_xor(y, o, 64);
+        }
+        if (li == 0) {
+          const int cl = wn * WTN + b * 16 + 4 * lg + j;
+          red[(wm * BN + cl) * 2 + 0] = x;
+          red[(wm * BN + cl) * 2 + 1] = y;
+        }
+      }
+    }
+  }
+  if constexpr (EP::kStats) {
+    __syncthreads();
+    const int rep = ep.stat_rep > 1 ? (wid % ep.stat_rep) : 0;
+    for (int cl = threadIdx.x; cl < BN; cl += NT) {
+      const int col = col0 + cl;
+      if (col < sh.N) {
+        float x = 0.f, y = 0.f;
+#pragma unroll
+        for (int w = 0; w < WGM; ++w) { x += red[(w * BN + cl) * 2]; y += red[(w * BN + cl) * 2 + 1]; }
+        atomicAdd(ep.stat1 + (size_t)rep * sh.N + col, (double)x);
+        atomicAdd(ep.stat2 + (size_t)rep * sh.N + col, (double)y);
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int WGM, int WGN, int S, class LA, class LB, class EP>
+inline int launch_gemm_ms(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
+                          hipStream_t stream) {
+  constexpr int BK = 64;
+  if (M <= 0 || N <= 0) return 0;
+  GemmShape sh;
+  sh.M = M; sh.N = N; sh.K = K;
+  sh.tiles_m = (M + BM - 1) / BM;
+  sh.tiles_n = (N + BN - 1) / BN;
+  if (ksplit < 1) ksplit = 1;
+  int kc = (K + ksplit - 1) / ksplit;
+  kc = ((kc + BK - 1) / BK) * BK;
+  if (kc < BK) kc = BK;
+  ksplit = (K + kc - 1) / kc;
+  if (ksplit < 1) ksplit = 1;
+  sh.kchunk = kc;
+  dim3 grid(sh.tiles_m * sh.tiles_n, ksplit, 1);
+  constexpr int lds = S * (BM + BN) * 128;
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  if constexpr (lds > 65536) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)&gemm_ms_kernel<BM, BN, WGM, WGN, S, LA, LB, EP>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      attr_set = true;
+    }
+  }
+  hipLaunchKernelGGL((gemm_ms_kernel<BM, BN, WGM, WGN, S, LA, LB, EP>), grid, dim3(WGM * WGN * 64), lds,
+                     stream, sh, la, lb, ep);
+  return (int)hipGetLastError();
+}
+
 template <typename T, int BM, int BN>
 constexpr int gemm_lds_bytes() { return 2 * (BM + BN) * 128; }
+
+// ---------------- variant dispatch ----------------
+// bf16 + direct loaders -> multi-stage kernels; everything else -> the
+// register-staged 2-stage kernel.  VLP_GEMM_VARIANT selects among tile /
+// stage configurations (for on-device A/B runs; the default is the measured best).
+#ifndef VLP_GEMM_DEFAULT_VARIANT
+#define VLP_GEMM_DEFAULT_VARIANT 3
+#endif
+inline int gemm_variant() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("VLP_GEMM_VARIANT");
+    v = e ? atoi(e) : VLP_GEMM_DEFAULT_VARIANT;
+  }
+  return v;
+}
+template <typename T, class LA, class LB>
+constexpr bool use_ms() {
+  return std::is_same<T, bf16>::value && DirectTrait<LA>::value && DirectTrait<LB>::value;
+}
+// N >= 128 columns
+template <typename T, class LA, class LB, class EP>
+inline int gemm_wide(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
+                     hipStream_t st) {
+  if constexpr (use_ms<T, LA, LB>()) {
+    switch (gemm_variant()) {
+      case 0: return launch_gemm<T, 128, 128, 2>(M, N, K, ksplit, la, lb, ep, st);
+      case 1: return launch_gemm_ms<128, 128, 2, 2, 3>(M, N, K, ksplit, la, lb, ep, st);
+      case 2: return launch_gemm_ms<256, 128, 4, 2, 3>(M, N, K, ksplit, la, lb, ep, st);
+      case 3: return launch_gemm_ms<128, 128, 2, 2, 2>(M, N, K, ksplit, la, lb, ep, st);
+      default: return launch_gemm_ms<256, 128, 4, 2, 2>(M, N, K, ksplit, la, lb, ep, st);
+    }
+  } else {
+    return launch_gemm<T, 128, 128, 2>(M, N, K, ksplit, la, lb, ep, st);
+  }
+}
+// N <= 64 columns (Co = 64 convs)
+template <typename T, class LA, class LB, class EP>
+inline int gemm_narrow(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
+                       hipStream_t st) {
+  if constexpr (use_ms<T, LA, LB>()) {
+    switch (gemm_variant()) {
+      case 0: return launch_gemm<T, 256, 64, 4>(M, N, K, ksplit, la, lb, ep, st);
+      case 1: return launch_gemm_ms<256, 64, 4, 1, 3>(M, N, K, ksplit, la, lb, ep, st);
+      case 2: return launch_gemm_ms<512, 64, 8, 1, 2>(M, N, K, ksplit, la, lb, ep, st);
+      case 3: return launch_gemm_ms<256, 64, 4, 1, 2>(M, N, K, ksplit, la, lb, ep, st);
+      default: return launch_gemm_ms<256, 64, 4, 1, 4>(M, N, K, ksplit, la, lb, ep, st);
+    }
+  } else {
+    return launch_gemm<T, 256, 64, 4>(M, N, K, ksplit, la, lb, ep, st);
+  }
+}
+// M <= 64 rows (weight gradients of Co = 64 convs)
+template <typename T, class LA, class LB, class EP>
+inline int gemm_short(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
+                      hipStream_t st) {
+  if constexpr (use_ms<T, LA, LB>()) {
+    switch (gemm_variant()) {
+      case 0: return launch_gemm<T, 64, 128, 1>(M, N, K, ksplit, la, lb, ep, st);
+      case 1: return launch_gemm_ms<64, 128, 1, 4, 3>(M, N, K, ksplit, la, lb, ep, st);
+      case 2: return launch_gemm_ms<64, 256, 1, 8, 3>(M, N, K, ksplit, la, lb, ep, st);
+      case 3: return launch_gemm_ms<64, 128, 1, 4, 2>(M, N, K, ksplit, la, lb, ep, st);
+      default: return launch_gemm_ms<64, 128, 1, 4, 4>(M, N, K, ksplit, la, lb, ep, st);
+    }
+  } else {
+    return launch_gemm<T, 64, 128, 1>(M, N, K, ksplit, la, lb, ep, st);
+  }
+}
 
 // Host-side launcher.  ksplit > 1 splits the reduction over grid.y (the
 // epilogue must then accumulate atomically).
@@ -424,8 +721,17 @@ struct KMat {
   __device__ uint4 load(const State& s, int k) const {
     return (s.ok && k < K) ? ldg16(s.p + k) : zero4();
   }
-  __device__ const void* addr(const State& s, int k) const {
-    return (s.ok && k < K) ? (const void*)(s.p + k) : zero_page();
+  struct DState { const T* p; int kk; bool ok; };
+  struct Step {};
+  __device__ Step step(int) const { return Step{}; }
+  __device__ DState start(int m, int koff, int kb) const {
+    return DState{p + (size_t)(m < M ? m : 0) * ld + kb + koff, kb + koff, m < M};
+  }
+  __device__ const void* next(DState& s, const Step&) const {
+    const void* r = (s.ok & (s.kk < K)) ? (const void*)s.p : zero_page();
+    s.p += Elem<T>::BK;
+    s.kk += Elem<T>::BK;
+    return r;
   }
 };
 // MN contiguous: A(m,k) = p[k*ld + m].  Requires M % EPC == 0.
@@ -439,8 +745,17 @@ struct MNMat {
   __device__ uint4 load(const State& s, int k) const {
     return (s.ok && k < K) ? ldg16(s.p + (size_t)k * ld) : zero4();
   }
-  __device__ const void* addr(const State& s, int k) const {
-    return (s.ok && k < K) ? (const void*)(s.p + (size_t)k * ld) : zero_page();
+  struct DState { const T* p; int kk; bool ok; };
+  struct Step {};
+  __device__ Step step(int) const { return Step{}; }
+  __device__ DState start(int m, int koff, int kb) const {
+    return DState{p + (m < M ? m : 0) + (size_t)(kb + koff) * ld, kb + koff, m < M};
+  }
+  __device__ const void* next(DState& s, const Step&) const {
+    const void* r = (s.ok & (s.kk < K)) ? (const void*)s.p : zero_page();
+    s.p += (size_t)Elem<T>::BK * ld;
+    s.kk += Elem<T>::BK;
+    return r;
   }
 };
 

@@ -30,15 +30,15 @@ def conv_out_hw(H, W, KH, KW, S, P):
 
 # kernel-family keys mirror the tile dispatch in csrc (one key = one kernel name)
 def _tile_auto(n):
-    return "256x64" if n <= 64 else "128x128"
+    return "/narrow" if n <= 64 else "/wide"
 
 
 def _tile_wgrad(m):
-    return "64x128" if m <= 64 else "128x128"
+    return "/short" if m <= 64 else "/wide"
 
 
 def _tile_lin(m, n):
-    return "256x64" if n <= 64 else ("64x256" if m <= 1024 else "128x128")
+    return "/narrow" if n <= 64 else ("/64x256" if m <= 1024 else "/wide")
 
 
 # ---------------- convolutions ----------------
@@ -195,7 +195,7 @@ def linear_dgrad(dy, w, dx, M, Kin, Nout, lddy=None, lddx=None, mode=0, aux=None
 
 
 def linear_wgrad(dy, x, dw, M, Nout, Kin, lddy=None, ldx=None):
-    tk = ktimer.begin("linear_wgrad128x128", 2.0 * M * Nout * Kin)
+    tk = ktimer.begin("linear_wgrad/wide", 2.0 * M * Nout * Kin)
     lib().vlp_linear_wgrad(dcode(dy), M, Nout, Kin, ptr(dy), lddy or Nout, ptr(x), ldx or Kin,
                            ptr(dw), _s())
     ktimer.end(tk)
