@@ -118,17 +118,12 @@ def main():
                                  False, False, 512, 312, 128, compute_dtype=args.dtype, device=dev)
     model.train()
     opt = model.configure_optimizers()["optimizer"]
-    from vlp_amd.dist import GradReducer
-    reducer = GradReducer()
-    arenas = [model._head.arena, model.image_encoder.model.arena, model.text_encoder.model.arena]
     batch = make_batch(args.batch, args.image_size, args.seq_len, dev, seed=rank)
 
     def step():
         opt.zero_grad()
         loss = model.training_step(batch)
-        loss.backward()
-        reducer.reduce(arenas)
-        reducer.wait()
+        loss.backward()   # includes the gradient all-reduce (N > 1)
         opt.step()
         return loss
 

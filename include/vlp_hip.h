@@ -61,8 +61,11 @@ int vlp_conv_wgrad(int dtype, const void* dy, const void* x, float* dw_ws, int N
                    int C, int Co, int KH, int KW, int S, int P, const float* in_scale,
                    const float* in_shift, void* stream);
 
-/* stem conv 7x7/2 pad 3, 3 -> 64 channels, on a zero-padded NHWC4 image xp of
- * size [N][Hp][Wp][4] (vlp_stem_geom); the caller zeroes xp once. */
+/* stem conv 7x7/2 pad 3, 3 -> 64 channels (timm resnet34 conv1, called from
+ * ImageEncoder.forward, VisionLanguageModule.py:34-35), on a zero-padded NHWC4
+ * image xp of size [N][Hp][Wp][4] (vlp_stem_geom); the caller zeroes xp once.
+ * vlp_stem_prep_u8 also folds the collation's normalise + 3-channel replicate
+ * (PretrainDataModule.py:167-171) into the upload of 1-channel uint8 images. */
 void vlp_stem_geom(int H, int W, int* Ho, int* Wo, int* Hp, int* Wp);
 int vlp_stem_prep(int dtype, const float* x_nchw, void* xp, int N, int H, int W, void* stream);
 int vlp_stem_prep_u8(int dtype, const uint8_t* x_u8, void* xp, int N, int H, int W, float mean,
@@ -73,6 +76,8 @@ int vlp_stem_wgrad(int dtype, const void* dy, const void* xp, float* dw_ws, int 
                    void* stream);
 
 /* ---------------- image tower: BatchNorm / residual / pooling ----------------
+ * Replace timm resnet34's BatchNorm2d (train-mode batch statistics), ReLU,
+ * residual add, maxpool 3x3/2 and global average pool (VisionLanguageModule.py:30-35).
  * Per-channel statistic outputs (fp64) are REPLICATED: a producer called with
  * stat_rep = R adds into R copies laid out [R][C] (copy = workgroup % R) so
  * that ~1e5 workgroups do not serialise on C addresses; vlp_stat_reduce folds
@@ -149,7 +154,9 @@ int vlp_scatter_rows(int dtype, int R, int D, const void* in, int ldi, void* out
                      void* stream);
 
 /* ---------------- contrastive head ----------------
- * Replace forward (:441-461) and _compute_loss (:532-554). */
+ * Replace VisionLanguageModule.forward (VisionLanguageModule.py:441-461: projections,
+ * F.normalize, logit_scale.exp().clamp(max=100) * img @ txt.T) and
+ * VisionLanguageModule._compute_loss (VisionLanguageModule.py:532-554: symmetric CE). */
 int vlp_l2norm_fwd(int R, int E, const float* x, float* y, float* norm, void* stream);
 /* dx = gscale[0] * d normalize(x) (gscale may be NULL = 1); optional compute-dtype copy */
 int vlp_l2norm_bwd(int dtype, int R, int E, const float* y, const float* norm, const float* dy,
@@ -176,7 +183,8 @@ int vlp_matmul(int dtype, int M, int N, int K, const void* A, int lda, int a_kc,
 int vlp_cast(int dtype, long long n, const float* x, void* y, void* stream);
 
 /* ---------------- optimizer / packing ----------------
- * Replace torch.optim.AdamW (configs/optimizer/adamw.yaml). */
+ * Replace torch.optim.AdamW as built by configure_optimizers
+ * (VisionLanguageModule.py:130-184, configs/optimizer/adamw.yaml:1-3). */
 int vlp_adamw(long long n, float* p, const float* g, float* m, float* v, float lr, float beta1,
               float beta2, float eps, float wd, float step_size, float bc2_sqrt, void* stream);
 int vlp_pack_conv(int dtype, int Co, int C, int KH, int KW, const float* w, void* wp, void* wt,

@@ -140,8 +140,14 @@ class ClipStepFn(torch.autograd.Function):
                                       g_img, gs)
         dcls = _project_backward(head, wT, h_last, Tn * D, D, "text_projection", E, te, tnorm,
                                  g_txt, gs)
-        img_t.run_backward(sv_img, dfeat_img)
+        # data parallel: SUM all-reduce of the flat gradient arenas, the head and
+        # text tower's launched while the (much longer) image backward runs
+        reducer = vdist.GradReducer()
         txt_t.run_backward(sv_txt, dcls)
+        reducer.reduce([head.arena, txt_t.arena])
+        img_t.run_backward(sv_img, dfeat_img)
+        reducer.reduce([img_t.arena])
+        reducer.wait()
         grads = (head.grads_for_autograd() + img_t.grads_for_autograd() + txt_t.grads_for_autograd())
         return (None, None, None, None, None, None, *grads)
 
