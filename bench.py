@@ -105,6 +105,19 @@ def cpu_baseline(args):
                       f"median of {len(times)} steps after 1 warm-up ({med:.2f} s/step)"}
 
 
+def _traffic(family):
+    """HBM bytes per launch of the roofline kernel from the committed PMC passes
+    (profiles/roofline_traffic.json, written by tools/pmc_traffic.py from
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this same command)."""
+    path = os.path.join(ROOT, "profiles", "roofline_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return round(d["traffic_bytes_per_launch"]) if d.get("family") == family else None
+
+
 def main():
     args = parse()
     rank, world, local = setup_dist(args)
@@ -188,7 +201,8 @@ def main():
             "roofline": {"bound": "mfma", "kernel": tk, "achieved": round(achieved, 2), "peak": peak,
                          "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                          "avg_launch_us": round(ms_k * 1e3 / max(nl, 1), 2), "launches": nl,
-                         "traffic": None},
+                         "flop_per_launch": round(flop_k / max(nl, 1)), "traffic_unit": "HBM bytes/launch",
+                         "traffic": _traffic(tk)},
             "loss": round(loss.item(), 5),
         }
         if world == 1 and not args.no_cpu_baseline:
