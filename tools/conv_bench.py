@@ -1,0 +1,70 @@
+"""Micro-benchmark of single implicit-GEMM conv launches at the bs=256, 512x512
+ResNet34 shapes (for A/B work on the GEMM engine and for focused rocprofv3
+PMC runs).
+
+  python tools/conv_bench.py [--ops fwd,dgrad,wgrad] [--layers l1,l2,l3,l4] [--iters 20]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "vision-language-pretraining-for-bone-tumor-detection_amd")]
+
+import torch  # noqa: E402
+from vlp_amd import ops  # noqa: E402
+
+# (name, N, H, W, C, Co, KH, KW, S, P) for the dominant 3x3 stride-1 convs
+LAYERS = {
+    "l1": (256, 128, 128, 64, 64, 3, 3, 1, 1),
+    "l2": (256, 64, 64, 128, 128, 3, 3, 1, 1),
+    "l3": (256, 32, 32, 256, 256, 3, 3, 1, 1),
+    "l4": (256, 16, 16, 512, 512, 3, 3, 1, 1),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ops", default="fwd,dgrad,wgrad")
+    ap.add_argument("--layers", default="l1,l2,l3,l4")
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    res = {}
+    for ln in args.layers.split(","):
+        N, H, W, C, Co, KH, KW, S, P = LAYERS[ln]
+        Ho, Wo = (H + 2 * P - KH) // S + 1, (W + 2 * P - KW) // S + 1
+        x = (torch.randn(N, H, W, C, device=dev) * 0.5).to(torch.bfloat16)
+        dy = (torch.randn(N, Ho, Wo, Co, device=dev) * 0.5).to(torch.bfloat16)
+        wp = (torch.randn(Co, KH, KW, C, device=dev) * 0.05).to(torch.bfloat16)
+        wt = wp.permute(3, 1, 2, 0).contiguous()
+        s1 = torch.zeros(64 * Co, dtype=torch.float64, device=dev)
+        s2 = torch.zeros_like(s1)
+        dws = torch.zeros(Co, KH * KW * C, device=dev)
+        flop = 2.0 * N * Ho * Wo * Co * C * KH * KW
+        for op in args.ops.split(","):
+            if op == "fwd":
+                fn = lambda: ops.conv_fwd(x, wp, Co, KH, KW, S, P, stat_sum=s1, stat_sumsq=s2, stat_rep=64)  # noqa: E731
+            elif op == "dgrad":
+                fn = lambda: ops.conv_dgrad(dy, wt, H, W, C, KH, KW, S, P)  # noqa: E731
+            else:
+                fn = lambda: ops.conv_wgrad(dy, x, KH, KW, S, P, dws)  # noqa: E731
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.iters):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / args.iters
+            res[f"{op}_{ln}"] = {"us": round(us, 1), "tflops": round(flop / us / 1e6, 1)}
+            print(f"{op:6s} {ln}: {us:9.1f} us  {flop / us / 1e6:7.1f} TF/s", flush=True)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -296,8 +296,8 @@ struct WtS2B {
 // pixel (n, ho, wo) incrementally, BK pixels per K-step (constant carries).
 struct PixStep {
   int dwo, dho;          // BK = dho*Wo + dwo
-  long long d_wo, d_ho;  // element deltas per unit of wo / ho in the input image
-  long long carry_w, carry_h;  // deltas applied when wo / ho wrap
+  int dpoff;             // element delta of (dho, dwo) in the input image
+  int carry_w, carry_h;  // deltas applied when wo / ho wrap
   int small;             // Ho*Wo <= BK: recompute by division instead
 };
 template <typename T, bool XF>
@@ -328,43 +328,50 @@ struct ConvWgradB {
     if constexpr (XF) v = xform_chunk<T>(v, sc, sh, s.ci);
     return v;
   }
-  struct DState { long long off; int hi, wi, mm, kh, kw, ci; bool ok; };
-  __device__ void locate(DState& d) const {
-    int mm = d.mm < g.M ? d.mm : 0;
-    int n = fdiv(mm, g.fd_howo);
-    int r = mm - n * g.Ho * g.Wo;
-    int ho = fdiv(r, g.fd_wo);
-    int wo = r - ho * g.Wo;
-    d.hi = ho * g.S - g.P + d.kh;
-    d.wi = wo * g.S - g.P + d.kw;
-    d.off = (((long long)n * g.H + d.hi) * g.W + d.wi) * g.C;
+  // direct staging (GStagerN, MN-contig): one output-pixel walk per thread
+  // (RState, 32-bit element offsets; x < 2^31 elements is checked on the
+  // host) combined with a fixed (tap, channel) offset per chunk column.
+  struct RState { int poff, ho, wo, mm; };     // poff = ((n*H + ho*S)*W + wo*S)*C
+  struct CState { int colofs, khp, kwp; bool ok; };
+  __device__ void locate(RState& r) const {
+    const int mm = r.mm < g.M ? r.mm : 0;
+    const int n = fdiv(mm, g.fd_howo);
+    const int rr = mm - n * g.Ho * g.Wo;
+    r.ho = fdiv(rr, g.fd_wo);
+    r.wo = rr - r.ho * g.Wo;
+    r.poff = ((n * g.H + r.ho * g.S) * g.W + r.wo * g.S) * g.C;
   }
-  __device__ DState start(int col, int koff, int kb) const {
-    State f = fixed(col);
-    DState d;
-    d.ok = f.ok; d.kh = f.kh; d.kw = f.kw; d.ci = f.ci; d.mm = kb + koff;
-    locate(d);
-    d.off += f.ci;
-    return d;
-  }
-  struct Step {};
-  __device__ Step step(int) const { return Step{}; }
-  __device__ const void* next(DState& d, const Step&) const {
-    const bool v = d.ok && d.mm < g.M && (unsigned)d.hi < (unsigned)g.H && (unsigned)d.wi < (unsigned)g.W;
-    const void* r = v ? (const void*)(x + d.off) : zero_page();
-    d.mm += Elem<T>::BK;
-    if (ps.small) {   // tiny images (Ho*Wo <= BK): recompute
-      locate(d);
-      d.off += d.ci;
-    } else {
-      const int wo = (d.wi - d.kw + g.P) / g.S + ps.dwo;
-      d.wi += ps.dwo * g.S; d.hi += ps.dho * g.S;
-      d.off += ps.dwo * ps.d_wo + ps.dho * ps.d_ho;
-      if (wo >= g.Wo) { d.wi -= g.Wo * g.S; d.hi += g.S; d.off += ps.carry_w; }
-      const int ho = (d.hi - d.kh + g.P) / g.S;
-      if (ho >= g.Ho) { d.hi -= g.Ho * g.S; d.off += ps.carry_h; }
-    }
+  __device__ RState rstart(int k, int kb) const {
+    RState r;
+    r.mm = kb + k;
+    locate(r);
     return r;
+  }
+  __device__ CState cstart(int col) const {
+    const State f = fixed(col);
+    return CState{((f.kh - g.P) * g.W + (f.kw - g.P)) * g.C + f.ci, f.kh - g.P, f.kw - g.P, f.ok};
+  }
+  __device__ const void* addr(const RState& r, const CState& c) const {
+    const int hi = r.ho * g.S + c.khp, wi = r.wo * g.S + c.kwp;
+    const bool v = c.ok & (r.mm < g.M) & ((unsigned)hi < (unsigned)g.H) & ((unsigned)wi < (unsigned)g.W);
+    return v ? (const void*)(x + (r.poff + c.colofs)) : zero_page();
+  }
+  __device__ void radvance(RState& r) const {
+    r.mm += Elem<T>::BK;
+    if (ps.small) {   // tiny images (Ho*Wo <= BK): recompute
+      locate(r);
+      return;
+    }
+    r.wo += ps.dwo;
+    r.ho += ps.dho;
+    r.poff += ps.dpoff;
+    const bool cw = r.wo >= g.Wo;
+    r.wo = cw ? r.wo - g.Wo : r.wo;
+    r.ho = cw ? r.ho + 1 : r.ho;
+    r.poff = cw ? r.poff + ps.carry_w : r.poff;
+    const bool ch = r.ho >= g.Ho;
+    r.ho = ch ? r.ho - g.Ho : r.ho;
+    r.poff = ch ? r.poff + ps.carry_h : r.poff;
   }
 };
 static PixStep make_pixstep(const ConvGeom& g, int BK) {
@@ -372,10 +379,9 @@ static PixStep make_pixstep(const ConvGeom& g, int BK) {
   p.small = g.Ho * g.Wo <= BK;
   p.dho = BK / g.Wo;
   p.dwo = BK % g.Wo;
-  p.d_wo = (long long)g.S * g.C;
-  p.d_ho = (long long)g.S * g.W * g.C;
-  p.carry_w = (long long)g.S * g.W * g.C - (long long)g.Wo * g.S * g.C;            // wo -= Wo, ho += 1
-  p.carry_h = (long long)g.H * g.W * g.C - (long long)g.Ho * g.S * g.W * g.C;      // ho -= Ho, n += 1
+  p.dpoff = p.dwo * g.S * g.C + p.dho * g.S * g.W * g.C;
+  p.carry_w = g.S * g.W * g.C - g.Wo * g.S * g.C;            // wo -= Wo, ho += 1
+  p.carry_h = g.H * g.W * g.C - g.Ho * g.S * g.W * g.C;      // ho -= Ho, n += 1
   return p;
 }
 
@@ -437,22 +443,32 @@ struct StemWgradB {
     int wo = r - ho * g.Wo;
     return ldg16(xp + (((size_t)n * g.Hp + 2 * ho) * g.Wp + 2 * wo) * 4 + s.off);
   }
-  struct DState { int off, mm; bool ok; };
-  __device__ DState start(int col, int koff, int kb) const {
-    State f = fixed(col);
-    return DState{f.off, kb + koff, f.ok};
+  struct RState { int poff, mm; };   // pixel (n, 2ho, 2wo) of the padded image, x 4 channels
+  struct CState { int off; bool ok; };
+  __device__ RState rstart(int k, int kb) const {
+    RState r;
+    r.mm = kb + k;
+    locate(r);
+    return r;
   }
-  struct Step {};
-  __device__ Step step(int) const { return Step{}; }
-  __device__ const void* next(DState& d, const Step&) const {
-    const int m = d.mm;
-    d.mm += Elem<T>::BK;
-    if (!d.ok || m >= g.M) return zero_page();
-    int n = fdiv(m, g.fd_howo);
-    int r = m - n * g.Ho * g.Wo;
-    int ho = fdiv(r, g.fd_wo);
-    int wo = r - ho * g.Wo;
-    return xp + (((size_t)n * g.Hp + 2 * ho) * g.Wp + 2 * wo) * 4 + d.off;
+  __device__ void locate(RState& r) const {
+    const int m = r.mm < g.M ? r.mm : 0;
+    const int n = fdiv(m, g.fd_howo);
+    const int rr = m - n * g.Ho * g.Wo;
+    const int ho = fdiv(rr, g.fd_wo);
+    const int wo = rr - ho * g.Wo;
+    r.poff = ((n * g.Hp + 2 * ho) * g.Wp + 2 * wo) * 4;
+  }
+  __device__ CState cstart(int col) const {
+    const State f = fixed(col);
+    return CState{f.off, f.ok};
+  }
+  __device__ const void* addr(const RState& r, const CState& c) const {
+    return (c.ok & (r.mm < g.M)) ? (const void*)(xp + (r.poff + c.off)) : zero_page();
+  }
+  __device__ void radvance(RState& r) const {
+    r.mm += Elem<T>::BK;
+    locate(r);
   }
 };
 
@@ -511,22 +527,20 @@ static int gemm_auto(int M, int N, int K, int ksplit, const LA& la, const LB& lb
   if (N <= 64) return gemm_narrow<T>(M, N, K, ksplit, la, lb, ep, st);
   return gemm_wide<T>(M, N, K, ksplit, la, lb, ep, st);
 }
-// weight-gradient GEMMs: rows = Co, cols = KH*KW*C, reduction = pixels
+// weight-gradient GEMMs: rows = Co, cols = KH*KW*C, reduction = pixels.
+//  Co = 64 (stem, layer1): 64 x 128 tiles, split-K chosen by the launcher to
+//    fill whole rounds of resident workgroups (ksplit = -2048: >= 2048 pixels)
+//  Co >= 128: ~1024 workgroups, >= 4096 pixels each, splits in multiples of 8
+//    so each XCD owns whole splits (GemmShape::xsplit); measured faster than
+//    the slot-balanced split for these shapes (r1: 21.1 vs 26.1 ms per step)
 template <typename T, class LA, class LB, class EP>
 static int gemm_wgrad(int M, int N, int K, const LA& la, const LB& lb, const EP& ep, hipStream_t st) {
-  // ~1024 workgroups (two waves of the chip at 2 WG/CU), >= 4096 pixels each:
-  // fewer splits = fewer fp32 atomics on the [Co][K] result
-  constexpr int kTargetWG = 1024;
-  int tiles = ((M + 127) / 128) * ((N + 127) / 128);
-  int ksplit = (kTargetWG + tiles - 1) / tiles;
-  int maxsplit = (K + 4095) / 4096;
+  if (M <= 64) return gemm_short<T>(M, N, K, -2048, la, lb, ep, st);
+  const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
+  int ksplit = (1024 + tiles - 1) / tiles;
+  const int maxsplit = (K + 4095) / 4096;
   if (ksplit > maxsplit) ksplit = maxsplit;
-  if (M <= 64) {   // Co = 64 (stem, layer1): 64 x 128 tiles (K = 576 wastes 11%, not 33%)
-    tiles = (N + 127) / 128;
-    ksplit = (kTargetWG + tiles - 1) / tiles;
-    if (ksplit > maxsplit) ksplit = maxsplit;
-    return gemm_short<T>(M, N, K, ksplit, la, lb, ep, st);
-  }
+  if (ksplit >= 8) ksplit = (ksplit + 7) / 8 * 8;
   return gemm_wide<T>(M, N, K, ksplit, la, lb, ep, st);
 }
 
@@ -686,6 +700,7 @@ VLP_EXPORT int vlp_conv_wgrad(int dtype, const void* dy, const void* x, float* d
                               const float* in_scale, const float* in_shift, void* stream) {
   ConvGeom g = make_geom(N, H, W, C, Co, KH, KW, S, P);
   hipStream_t st = (hipStream_t)stream;
+  if ((long long)N * H * W * C >= (1ll << 31)) return (int)hipErrorInvalidValue;   // 32-bit pixel walk
   if (dtype == VLP_BF16) return conv_wgrad_t<bf16>(dy, x, dw_ws, g, in_scale, in_shift, st);
   return conv_wgrad_t<float>(dy, x, dw_ws, g, in_scale, in_shift, st);
 }
@@ -744,6 +759,7 @@ VLP_EXPORT int vlp_stem_wgrad(int dtype, const void* dy, const void* xp, float* 
                               int W, void* stream) {
   StemGeom g = make_stem(N, H, W);
   hipStream_t st = (hipStream_t)stream;
+  if ((long long)N * g.Hp * g.Wp * 4 >= (1ll << 31)) return (int)hipErrorInvalidValue;
   EpiAtomic ep{nullptr, nullptr, dw_ws, 256, 1.0f};
   if (dtype == VLP_BF16) {
     MNMat<bf16> la{(const bf16*)dy, 64, 64, g.M};

@@ -37,6 +37,7 @@ struct GemmShape {
   int M, N, K;
   int kchunk;   // K range per split (multiple of BK); == K rounded up when no split
   int tiles_m, tiles_n;
+  int xsplit;   // 1: split-K grid is 1-D and every split's tiles share one XCD
 };
 
 // ---------------- LDS image addressing (bytes) ----------------
@@ -142,17 +143,9 @@ struct GStager {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int q = (w * NI + i) * 64 + lane;
-      if constexpr (L::kKContig) {
-        const int r = q >> 3, p = q & 7;
-        const int c = p ^ ((r >> 1) & 7);
-        st[i] = ld.start(row0 + r, c * G::EPC, kb);
-      } else {
-        const int o = q * 16;
-        const int k = o / G::RB, inrow = o % G::RB;
-        const int sw = (G::RB >= 256) ? (k & 7) : ((k >> 1) & 3);
-        const int b = (inrow >> 5) ^ sw, half = (inrow >> 4) & 1;
-        st[i] = ld.start(row0 + (2 * b + half) * G::EPC, k, kb);
-      }
+      const int r = q >> 3, p = q & 7;
+      const int c = p ^ ((r >> 1) & 7);
+      st[i] = ld.start(row0 + r, c * G::EPC, kb);
     }
   }
   __device__ __forceinline__ void issue(const L& ld, int k0, char* lds) {
@@ -169,7 +162,10 @@ struct GStager {
 
 // Uniform staging interface: register staging (any loader, fp32 parity mode,
 // transforming loaders) or direct-to-LDS (bf16 + kDirect loaders).
-template <typename T, int BM, class L, bool DIRECT = (sizeof(T) == 2) && DirectTrait<L>::value>
+// (the 2-stage kernel stages MN-contig operands through registers; direct
+// MN staging lives in the multi-stage kernel)
+template <typename T, int BM, class L,
+          bool DIRECT = (sizeof(T) == 2) && DirectTrait<L>::value && L::kKContig>
 struct OpStager;
 template <typename T, int BM, class L>
 struct OpStager<T, BM, L, false> {
@@ -190,7 +186,10 @@ struct OpStager<T, BM, L, true> {
 // bf16 fragment for MFMA 16x16x32, k-step s (0/1) within a BK=64 stage.
 // Lane l = 16g + i holds operand row (rb + i) at k in {32s+4g..+3} U {32s+16+4g..+3}
 // (a k-permutation shared by both operands, chosen so the reads are conflict-free).
-template <bool KC, int RB>
+// MNCOL: MN-contig image in the column-major chunk layout of the direct
+// MN stager (GStagerN<..., false>): chunk column cb = mn/8 is 1 KiB of 64
+// k-rows x 16 B, rows XOR 8 on odd columns (conflict-free tr reads).
+template <bool KC, int RB, bool MNCOL = false>
 __device__ __forceinline__ v8bf frag_bf16(const char* lds, int rb, int s) {
   const int l = threadIdx.x & 63;
   const int i = l & 15, g = l >> 4;
@@ -200,6 +199,14 @@ __device__ __forceinline__ v8bf frag_bf16(const char* lds, int rb, int s) {
     const int c1 = 4 * s + (g >> 1), c2 = 4 * s + 2 + (g >> 1);
     lo = *reinterpret_cast<const v4bf*>(lds + kc_off(r, c1) + 8 * (g & 1));
     hi = *reinterpret_cast<const v4bf*>(lds + kc_off(r, c2) + 8 * (g & 1));
+  } else if constexpr (MNCOL) {
+    const int q = i >> 2, p = i & 3;
+    const int k1 = 32 * s + 4 * g + q;
+    const int mn = rb + 4 * p, cb = mn >> 3;
+    const int base = cb * 1024 + ((mn & 4) << 1);
+    const int sw = (cb & 1) << 3;
+    lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(lds + base + ((k1 ^ sw) << 4)));
+    hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(lds + base + (((k1 + 16) ^ sw) << 4)));
   } else {
     const int q = i >> 2, p = i & 3;
     const int k1 = 32 * s + 4 * g + q;
@@ -392,9 +399,11 @@ gemm_kernel(GemmShape sh, LA la, LB lb, EP ep) {
 // t-1, whose slot is refilled next), issue tile t+S-1, compute tile t.  A
 // __syncthreads() would drain the ring (an LDS-DMA is a pending VM op), so
 // the wait and barrier are explicit.
+template <typename T, int BM, class L, int NT, bool KC = L::kKContig>
+struct GStagerN;
+// K-contig operand: [BM rows][128 B] image, 16-B chunks XOR-swizzled by row.
 template <typename T, int BM, class L, int NT>
-struct GStagerN {
-  using G = TileGeom<T, BM, L::kKContig>;
+struct GStagerN<T, BM, L, NT, true> {
   static constexpr int NI = BM * 8 / NT;   // 16-B chunks (= 1 KiB wave-instructions) per thread
   static_assert(NI >= 1 && (BM * 8) % NT == 0, "tile / thread geometry");
   typename L::DState st[NI];
@@ -403,16 +412,8 @@ struct GStagerN {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int q = (w * NI + i) * 64 + lane;
-      if constexpr (L::kKContig) {
-        const int r = q >> 3, p = q & 7;
-        st[i] = ld.start(row0 + r, (p ^ ((r >> 1) & 7)) * G::EPC, kb);
-      } else {
-        const int o = q * 16;
-        const int k = o / G::RB, inrow = o % G::RB;
-        const int sw = (G::RB >= 256) ? (k & 7) : ((k >> 1) & 3);
-        const int b = (inrow >> 5) ^ sw, half = (inrow >> 4) & 1;
-        st[i] = ld.start(row0 + (2 * b + half) * G::EPC, k, kb);
-      }
+      const int r = q >> 3, p = q & 7;
+      st[i] = ld.start(row0 + r, (p ^ ((r >> 1) & 7)) * Elem<T>::EPC, kb);
     }
   }
   __device__ __forceinline__ void issue(const L& ld, int k0, char* lds) {
@@ -424,6 +425,41 @@ struct GStagerN {
       __builtin_amdgcn_global_load_lds(p, (__attribute__((address_space(3))) void*)(lds + (w * NI + i) * 1024),
                                        16, 0, 0);
     }
+  }
+};
+// MN-contig operand: column-major chunk image -- chunk column cb (8 MN values)
+// is 1 KiB = 64 k-rows x 16 B, k-row XOR 8 on odd columns.  Wave w,
+// instruction i fills column cb = i*NW + w, lane L its physical row L, so all
+// of a thread's chunks share ONE k-row (logical k = L ^ 8*(w&1)): the loader's
+// per-k state (e.g. the output pixel of a weight-gradient reduction) is walked
+// once per thread per K-step and combined with fixed per-column offsets:
+//   RState rstart(int k, int kb); void radvance(RState&)      per k-row
+//   CState cstart(int mn)                                      per column
+//   const void* addr(const RState&, const CState&)             address / zero page
+template <typename T, int BM, class L, int NT>
+struct GStagerN<T, BM, L, NT, false> {
+  static constexpr int NW = NT / 64;
+  static constexpr int NCOL = BM / 8;
+  static constexpr int NI = NCOL / NW;
+  static_assert(NI >= 1 && NCOL % NW == 0 && NW % 2 == 0, "tile / thread geometry");
+  static_assert(sizeof(T) == 2, "MN direct staging is bf16 (BK = 64 rows)");
+  typename L::RState rs;
+  typename L::CState cs[NI];
+  __device__ __forceinline__ void init(const L& ld, int row0, int kb) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) cs[i] = ld.cstart(row0 + (i * NW + w) * 8);
+    rs = ld.rstart(lane ^ ((w & 1) << 3), kb);
+  }
+  __device__ __forceinline__ void issue(const L& ld, int, char* lds) {
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const void* p = ld.addr(rs, cs[i]);
+      __builtin_amdgcn_global_load_lds(p, (__attribute__((address_space(3))) void*)(lds + (i * NW + w) * 1024),
+                                       16, 0, 0);
+    }
+    ld.radvance(rs);
   }
 };
 
@@ -453,14 +489,21 @@ gemm_ms_kernel(GemmShape sh, LA la, LB lb, EP ep) {
 
   const int nwg = sh.tiles_m * sh.tiles_n;
   const int bid = blockIdx.x;
-  int wid = bid;
-  if (nwg >= 16) {
+  int wid = bid, split = blockIdx.y;
+  if (sh.xsplit) {
+    // split-K reductions re-read their K slice once per tile: keep all tiles of
+    // a split on one XCD (dispatch is round-robin over XCDs) so the slice is
+    // fetched into ONE L2 instead of eight
+    const int xcd = bid & 7, j = bid >> 3, jt = j / nwg;
+    split = xcd + 8 * jt;
+    wid = j - jt * nwg;
+  } else if (nwg >= 16) {
     const int xcd = bid & 7, idx = bid >> 3, q = nwg >> 3, rr = nwg & 7;
     wid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
   }
   const int tm = wid / sh.tiles_n, tn = wid - tm * sh.tiles_n;
   const int row0 = tm * BM, col0 = tn * BN;
-  const int kb = blockIdx.y * sh.kchunk;
+  const int kb = split * sh.kchunk;
   int ke = kb + sh.kchunk;
   if (ke > sh.K) ke = sh.K;
   const int nk = (ke - kb + BK - 1) / BK;
@@ -511,9 +554,9 @@ gemm_ms_kernel(GemmShape sh, LA la, LB lb, EP ep) {
     for (int s = 0; s < 2; ++s) {
       v8bf fa[MB], fb[NB];
 #pragma unroll
-      for (int a = 0; a < MB; ++a) fa[a] = frag_bf16<LA::kKContig, GA::RB>(ia, wm * WTM + a * 16, s);
+      for (int a = 0; a < MB; ++a) fa[a] = frag_bf16<LA::kKContig, GA::RB, true>(ia, wm * WTM + a * 16, s);
 #pragma unroll
-      for (int b = 0; b < NB; ++b) fb[b] = frag_bf16<LB::kKContig, GB::RB>(ib, wn * WTN + b * 16, s);
+      for (int b = 0; b < NB; ++b) fb[b] = frag_bf16<LB::kKContig, GB::RB, true>(ib, wn * WTN + b * 16, s);
 #pragma unroll
       for (int a = 0; a < MB; ++a)
 #pragma unroll
@@ -574,15 +617,59 @@ gemm_ms_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   }
 }
 
+// Split-K count for a reduction of K over `tiles` output tiles, given the
+// number of workgroups the chip holds at once (`slots`).  Workgroups of one
+// launch all cost about the same, so the launch takes ceil(WG / slots)
+// rounds: pick the split (1..4 rounds' worth) with the best slot fill, each
+// split still >= min_k deep (epilogue atomics amortised).
+inline int balanced_ksplit(int tiles, int K, int slots, int min_k) {
+  if (tiles >= slots) return 1;
+  int best = 1;
+  double best_eff = 0.0;
+  for (int r = 1; r <= 4; ++r) {
+    int ks = r * slots / tiles;
+    if (ks < 1) continue;
+    if (ks > 1 && K / ks < min_k) break;
+    const long long wg = (long long)ks * tiles;
+    const double eff = (double)wg / (double)(((wg + slots - 1) / slots) * slots);
+    if (eff > best_eff + 0.01) { best_eff = eff; best = ks; }
+  }
+  return best;
+}
+inline int device_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+
 template <int BM, int BN, int WGM, int WGN, int S, class LA, class LB, class EP>
 inline int launch_gemm_ms(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
                           hipStream_t stream) {
   constexpr int BK = 64;
   if (M <= 0 || N <= 0) return 0;
   GemmShape sh;
+  sh.xsplit = 0;
   sh.M = M; sh.N = N; sh.K = K;
   sh.tiles_m = (M + BM - 1) / BM;
   sh.tiles_n = (N + BN - 1) / BN;
+  if (ksplit <= 0) {   // auto: fill whole rounds of resident workgroups
+    static int occ = 0;
+    if (!occ) {
+      constexpr int lds_b = S * (BM + BN) * 128;
+      if (lds_b > 65536)
+        (void)hipFuncSetAttribute((const void*)&gemm_ms_kernel<BM, BN, WGM, WGN, S, LA, LB, EP>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_b);
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+              &occ, (const void*)&gemm_ms_kernel<BM, BN, WGM, WGN, S, LA, LB, EP>, WGM * WGN * 64,
+              lds_b) != hipSuccess || occ <= 0)
+        occ = 1;
+    }
+    ksplit = balanced_ksplit(sh.tiles_m * sh.tiles_n, K, occ * device_cus(), -ksplit > 0 ? -ksplit : 2048);
+  }
   if (ksplit < 1) ksplit = 1;
   int kc = (K + ksplit - 1) / ksplit;
   kc = ((kc + BK - 1) / BK) * BK;
@@ -590,7 +677,9 @@ inline int launch_gemm_ms(int M, int N, int K, int ksplit, const LA& la, const L
   ksplit = (K + kc - 1) / kc;
   if (ksplit < 1) ksplit = 1;
   sh.kchunk = kc;
-  dim3 grid(sh.tiles_m * sh.tiles_n, ksplit, 1);
+  sh.xsplit = (ksplit >= 8 && ksplit % 8 == 0) ? 1 : 0;
+  dim3 grid = sh.xsplit ? dim3(sh.tiles_m * sh.tiles_n * ksplit, 1, 1)
+                        : dim3(sh.tiles_m * sh.tiles_n, ksplit, 1);
   constexpr int lds = S * (BM + BN) * 128;
   static_assert(lds <= 160 * 1024, "LDS budget");
   if constexpr (lds > 65536) {
@@ -685,9 +774,16 @@ inline int launch_gemm(int M, int N, int K, int ksplit, const LA& la, const LB& 
   constexpr int BK = Elem<T>::BK;
   if (M <= 0 || N <= 0) return 0;
   GemmShape sh;
+  sh.xsplit = 0;
   sh.M = M; sh.N = N; sh.K = K;
   sh.tiles_m = (M + BM - 1) / BM;
   sh.tiles_n = (N + BN - 1) / BN;
+  if (ksplit <= 0) {   // auto: ~1024 workgroups, >= 4096-deep splits
+    const int tiles = sh.tiles_m * sh.tiles_n;
+    ksplit = (1024 + tiles - 1) / tiles;
+    const int maxsplit = (K + 4095) / 4096;
+    if (ksplit > maxsplit) ksplit = maxsplit;
+  }
   if (ksplit < 1) ksplit = 1;
   int kc = (K + ksplit - 1) / ksplit;
   kc = ((kc + BK - 1) / BK) * BK;
@@ -745,17 +841,16 @@ struct MNMat {
   __device__ uint4 load(const State& s, int k) const {
     return (s.ok && k < K) ? ldg16(s.p + (size_t)k * ld) : zero4();
   }
-  struct DState { const T* p; int kk; bool ok; };
-  struct Step {};
-  __device__ Step step(int) const { return Step{}; }
-  __device__ DState start(int m, int koff, int kb) const {
-    return DState{p + (m < M ? m : 0) + (size_t)(kb + koff) * ld, kb + koff, m < M};
+  struct RState { const T* p; int kk; };   // row k of this thread
+  struct CState { int m; bool ok; };
+  __device__ RState rstart(int k, int kb) const { return RState{p + (size_t)(kb + k) * ld, kb + k}; }
+  __device__ CState cstart(int m) const { return CState{m < M ? m : 0, m < M}; }
+  __device__ const void* addr(const RState& r, const CState& c) const {
+    return (c.ok & (r.kk < K)) ? (const void*)(r.p + c.m) : zero_page();
   }
-  __device__ const void* next(DState& s, const Step&) const {
-    const void* r = (s.ok & (s.kk < K)) ? (const void*)s.p : zero_page();
-    s.p += (size_t)Elem<T>::BK * ld;
-    s.kk += Elem<T>::BK;
-    return r;
+  __device__ void radvance(RState& r) const {
+    r.p += (size_t)Elem<T>::BK * ld;
+    r.kk += Elem<T>::BK;
   }
 };
 
