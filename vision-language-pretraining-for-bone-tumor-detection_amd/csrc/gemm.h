@@ -184,37 +184,36 @@ struct OpStager<T, BM, L, true> {
 
 // ---------------- fragment reads ----------------
 // bf16 fragment for MFMA 16x16x32, k-step s (0/1) within a BK=64 stage.
-// Lane l = 16g + i holds operand row (rb + i) at k in {32s+4g..+3} U {32s+16+4g..+3}
-// (a k-permutation shared by both operands, chosen so the reads are conflict-free).
-// MNCOL: MN-contig image in the column-major chunk layout of the direct
-// MN stager (GStagerN<..., false>): chunk column cb = mn/8 is 1 KiB of 64
-// k-rows x 16 B, rows XOR 8 on odd columns (conflict-free tr reads).
+// Lane l = 16g + i holds operand row (rb + i) at k = 32s + 8g + (0..7): a
+// k-permutation shared by both operands, chosen so a K-contig fragment is ONE
+// 16-B chunk (ds_read_b128, conflict-free under the kc_off swizzle) and an
+// MN-contig fragment is two ds_read_b64_tr_b16 (k-rows 32s+8g+q, +4).
+// MNCOL: MN-contig image in the column-major chunk layout of the direct MN
+// stager (GStagerN<..., false>): chunk column cb = mn/8 is 1 KiB of 64 k-rows
+// x 16 B, rows XOR 4 on odd columns (conflict-free tr reads).
 template <bool KC, int RB, bool MNCOL = false>
 __device__ __forceinline__ v8bf frag_bf16(const char* lds, int rb, int s) {
   const int l = threadIdx.x & 63;
   const int i = l & 15, g = l >> 4;
-  v4bf lo, hi;
   if constexpr (KC) {
-    const int r = rb + i;
-    const int c1 = 4 * s + (g >> 1), c2 = 4 * s + 2 + (g >> 1);
-    lo = *reinterpret_cast<const v4bf*>(lds + kc_off(r, c1) + 8 * (g & 1));
-    hi = *reinterpret_cast<const v4bf*>(lds + kc_off(r, c2) + 8 * (g & 1));
-  } else if constexpr (MNCOL) {
-    const int q = i >> 2, p = i & 3;
-    const int k1 = 32 * s + 4 * g + q;
-    const int mn = rb + 4 * p, cb = mn >> 3;
-    const int base = cb * 1024 + ((mn & 4) << 1);
-    const int sw = (cb & 1) << 3;
-    lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(lds + base + ((k1 ^ sw) << 4)));
-    hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(lds + base + (((k1 + 16) ^ sw) << 4)));
+    return *reinterpret_cast<const v8bf*>(lds + kc_off(rb + i, 4 * s + g));
   } else {
+    v4bf lo, hi;
     const int q = i >> 2, p = i & 3;
-    const int k1 = 32 * s + 4 * g + q;
-    const int by = (rb + 4 * p) * 2;
-    lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(lds + mn_off<RB>(k1, by)));
-    hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(lds + mn_off<RB>(k1 + 16, by)));
+    const int k1 = 32 * s + 8 * g + q;
+    if constexpr (MNCOL) {
+      const int mn = rb + 4 * p, cb = mn >> 3;
+      const int base = cb * 1024 + ((mn & 4) << 1);
+      const int sw = (cb & 1) << 2;
+      lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(lds + base + ((k1 ^ sw) << 4)));
+      hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(lds + base + (((k1 + 4) ^ sw) << 4)));
+    } else {
+      const int by = (rb + 4 * p) * 2;
+      lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(lds + mn_off<RB>(k1, by)));
+      hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(lds + mn_off<RB>(k1 + 4, by)));
+    }
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   }
-  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
 // fp32 fragment for 4 x MFMA 16x16x4f32 over a 16-k sub-step s (0/1) of BK=32.
@@ -428,9 +427,9 @@ struct GStagerN<T, BM, L, NT, true> {
   }
 };
 // MN-contig operand: column-major chunk image -- chunk column cb (8 MN values)
-// is 1 KiB = 64 k-rows x 16 B, k-row XOR 8 on odd columns.  Wave w,
+// is 1 KiB = 64 k-rows x 16 B, k-row XOR 4 on odd columns.  Wave w,
 // instruction i fills column cb = i*NW + w, lane L its physical row L, so all
-// of a thread's chunks share ONE k-row (logical k = L ^ 8*(w&1)): the loader's
+// of a thread's chunks share ONE k-row (logical k = L ^ 4*(w&1)): the loader's
 // per-k state (e.g. the output pixel of a weight-gradient reduction) is walked
 // once per thread per K-step and combined with fixed per-column offsets:
 //   RState rstart(int k, int kb); void radvance(RState&)      per k-row
@@ -449,7 +448,7 @@ struct GStagerN<T, BM, L, NT, false> {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
     for (int i = 0; i < NI; ++i) cs[i] = ld.cstart(row0 + (i * NW + w) * 8);
-    rs = ld.rstart(lane ^ ((w & 1) << 3), kb);
+    rs = ld.rstart(lane ^ ((w & 1) << 2), kb);
   }
   __device__ __forceinline__ void issue(const L& ld, int, char* lds) {
     const int w = threadIdx.x >> 6;
