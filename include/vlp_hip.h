@@ -56,10 +56,12 @@ int vlp_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, int N, i
                    const float* bn_invstd, double* stat1, double* stat2, int stat_rep,
                    void* stream);
 /* dw_ws[Co][KH][KW][C] += sum over pixels dy x_patch (fp32 atomics; zero first).
- * Optional BN+ReLU-on-load of x as in vlp_conv_fwd. */
+ * Optional BN+ReLU-on-load of x as in vlp_conv_fwd.  dyT (optional, bf16): the
+ * same gradient transposed to [Co][N*Ho*Wo] (vlp_bn_bwd_apply writes it); when
+ * given it is the GEMM's A operand instead of dy. */
 int vlp_conv_wgrad(int dtype, const void* dy, const void* x, float* dw_ws, int N, int H, int W,
                    int C, int Co, int KH, int KW, int S, int P, const float* in_scale,
-                   const float* in_shift, void* stream);
+                   const float* in_shift, const void* dyT, void* stream);
 
 /* stem conv 7x7/2 pad 3, 3 -> 64 channels (timm resnet34 conv1, called from
  * ImageEncoder.forward, VisionLanguageModule.py:34-35), on a zero-padded NHWC4
@@ -73,7 +75,7 @@ int vlp_stem_prep_u8(int dtype, const uint8_t* x_u8, void* xp, int N, int H, int
 int vlp_stem_fwd(int dtype, const void* xp, const void* wp, void* y, int N, int H, int W,
                  double* stat_sum, double* stat_sumsq, int stat_rep, void* stream);
 int vlp_stem_wgrad(int dtype, const void* dy, const void* xp, float* dw_ws, int N, int H, int W,
-                   void* stream);
+                   const void* dyT, void* stream);
 
 /* ---------------- image tower: BatchNorm / residual / pooling ----------------
  * Replace timm resnet34's BatchNorm2d (train-mode batch statistics), ReLU,
@@ -100,13 +102,15 @@ int vlp_bn_bwd_reduce(int dtype, long long M, int C, const void* dout, const flo
                       const void* mask, const void* ya, const float* mean_a, const float* istd_a,
                       const void* yb, const float* mean_b, const float* istd_b, double* sum_g,
                       double* sum_ga, double* sum_gb, int stat_rep, void* stream);
-/* dy_s = gamma_s*istd_s*(g - mean(g) - xhat_s*mean(g*xhat_s)) for sides a, b; g_out = g */
+/* dy_s = gamma_s*istd_s*(g - mean(g) - xhat_s*mean(g*xhat_s)) for sides a, b; g_out = g.
+ * dyT_a / dyT_b (optional, bf16, C % 64 == 0, M % 8 == 0): also write dy_s
+ * transposed to [C][M] (the weight-gradient GEMM's pixel-contiguous operand). */
 int vlp_bn_bwd_apply(int dtype, long long M, int C, const void* dout, const float* dbc, int HW,
                      const void* mask, const void* ya, const float* mean_a, const float* istd_a,
                      const float* gamma_a, const double* sum_g_a, const double* sum_gx_a,
                      void* dy_a, const void* yb, const float* mean_b, const float* istd_b,
                      const float* gamma_b, const double* sum_g_b, const double* sum_gx_b,
-                     void* dy_b, void* g_out, void* stream);
+                     void* dy_b, void* g_out, void* dyT_a, void* dyT_b, void* stream);
 int vlp_bn_param_grad(int C, const double* sum_g, const double* sum_gx, float* dgamma,
                       float* dbeta, void* stream);
 int vlp_maxpool_fwd(int dtype, int N, int H, int W, int C, const void* y, const float* sc,

@@ -112,6 +112,17 @@ def test_conv_dgrad_wgrad(ops, dt, case):
     torch.cuda.synchronize()
     assert rel(nchw(dx.float().cpu()), x.grad + add) < tol(dt)
     assert rel(g.cpu(), w.grad) < tol(dt) / 2
+    Mp = dy.shape[0] * dy.shape[2] * dy.shape[3]
+    if dt == torch.bfloat16 and Mp % 8 == 0:
+        # pixel-contiguous A operand (dy^T [Co][pixels], as vlp_bn_bwd_apply writes it)
+        dyT = nhwc(dy).to(dt).reshape(Mp, Co).t().contiguous().cuda()
+        ws2 = torch.zeros(Co, KH, KW, C, device="cuda")
+        ops.conv_wgrad(nhwc(dy).to(dt).cuda(), nhwc(x.detach()).to(dt).cuda(), KH, KW, S, P, ws2, dyT=dyT)
+        g2 = torch.empty(Co, C, KH, KW, device="cuda")
+        ops.unpack_conv_grad(ws2, g2)
+        torch.cuda.synchronize()
+        assert rel(g2.cpu(), w.grad) < tol(dt) / 2
+        assert rel(g2.cpu(), g.cpu()) < 1e-5
 
 
 @pytest.mark.parametrize("dt", DT)
@@ -167,3 +178,54 @@ def test_stem_fwd_wgrad(ops, dt):
     torch.cuda.synchronize()
     assert rel(nchw(yd.float().cpu()), y.detach()) < tol(dt)
     assert rel(g.cpu(), w.grad) < tol(dt) / 2
+    if dt == torch.bfloat16:
+        Mp = N * Ho * Wo
+        dyT = nhwc(dy).to(dt).reshape(Mp, 64).t().contiguous().cuda()
+        ws2 = torch.zeros(64, 256, device="cuda")
+        ops.stem_wgrad(nhwc(dy).to(dt).cuda(), xp, N, H, W, ws2, dyT=dyT)
+        g2 = torch.empty(64, 3, 7, 7, device="cuda")
+        ops.unpack_stem_grad(ws2, g2)
+        torch.cuda.synchronize()
+        assert rel(g2.cpu(), g.cpu()) < 1e-5
+
+
+@pytest.mark.parametrize("has_b", [False, True])
+@pytest.mark.parametrize("bcast", [False, True])
+@pytest.mark.parametrize("C", [64, 128])
+def test_bn_bwd_apply_transposed(ops, has_b, bcast, C):
+    """The tiled BN-backward apply that also writes dy^T equals the plain one."""
+    torch.manual_seed(11)
+    N, HW = 3, 40              # M = 120: a partial 64-pixel tile
+    M = N * HW
+    dt = torch.bfloat16
+    dev = "cuda"
+    dout = torch.randn(M, C, device=dev).to(dt)
+    dbc = torch.randn(N, C, device=dev) if bcast else None
+    mask = torch.randn(M, C, device=dev).to(dt)
+    def side(seed):
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        y = torch.randn(M, C, generator=g).to(dt).to(dev)
+        mean = torch.randn(C, generator=g).to(dev) * 0.1
+        istd = (torch.rand(C, generator=g) + 0.5).to(dev)
+        gamma = torch.randn(C, generator=g).to(dev)
+        sg = (torch.randn(C, generator=g) * M).double().to(dev)
+        sgx = (torch.randn(C, generator=g) * M).double().to(dev)
+        return [y, mean, istd, gamma, sg, sgx]
+    A = side(1)
+    B = side(2) if has_b else None
+    outs = []
+    for transposed in (False, True):
+        dya = torch.empty(M, C, device=dev, dtype=dt)
+        dyb = torch.empty(M, C, device=dev, dtype=dt) if has_b else None
+        gout = torch.empty(M, C, device=dev, dtype=dt)
+        ta = torch.full((C, M), 7.0, device=dev, dtype=dt) if transposed else None
+        tb = torch.full((C, M), 7.0, device=dev, dtype=dt) if (transposed and has_b) else None
+        ops.bn_bwd_apply(M, C, None if bcast else dout, dbc, HW, mask, A + [dya],
+                         (B + [dyb]) if has_b else None, gout, dout, dyT_a=ta, dyT_b=tb)
+        outs.append((dya, dyb, gout, ta, tb))
+    torch.cuda.synchronize()
+    (a0, b0, g0, _, _), (a1, b1, g1, ta, tb) = outs
+    assert torch.equal(a0, a1) and torch.equal(g0, g1)
+    assert torch.equal(ta, a1.t())
+    if has_b:
+        assert torch.equal(b0, b1) and torch.equal(tb, b1.t())

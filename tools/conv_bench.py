@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--ops", default="fwd,dgrad,wgrad")
     ap.add_argument("--layers", default="l1,l2,l3,l4")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--gemm", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
@@ -63,6 +64,35 @@ def main():
             us = e0.elapsed_time(e1) * 1e3 / args.iters
             res[f"{op}_{ln}"] = {"us": round(us, 1), "tflops": round(flop / us / 1e6, 1)}
             print(f"{op:6s} {ln}: {us:9.1f} us  {flop / us / 1e6:7.1f} TF/s", flush=True)
+    if args.gemm:
+        # plain GEMMs with the three operand layouts at a conv-like size:
+        # fwd (K-contig x K-contig), dgrad (K-contig x MN-contig), wgrad (MN x MN)
+        M, N, K = 65536, 512, 4608
+        flop = 2.0 * M * N * K
+        a = (torch.randn(M, K, device=dev) * 0.1).to(torch.bfloat16)
+        w = (torch.randn(N, K, device=dev) * 0.1).to(torch.bfloat16)
+        y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        dyb = (torch.randn(M, N, device=dev) * 0.1).to(torch.bfloat16)
+        dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
+        dw = torch.zeros(N, K, device=dev)
+        cases = {
+            "gemm_kk": (lambda: ops.linear_fwd(a, w, None, y, M, N, K), 2.0 * M * N * K),
+            "gemm_kmn": (lambda: ops.linear_dgrad(dyb, w, dx, M, K, N), 2.0 * M * N * K),
+            "gemm_mnmn": (lambda: ops.linear_wgrad(dyb, a, dw, M, N, K), 2.0 * M * N * K),
+        }
+        for name, (fn, flop) in cases.items():
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.iters):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / args.iters
+            res[name] = {"us": round(us, 1), "tflops": round(flop / us / 1e6, 1)}
+            print(f"{name:9s}: {us:9.1f} us  {flop / us / 1e6:7.1f} TF/s", flush=True)
     print(json.dumps(res))
 
 

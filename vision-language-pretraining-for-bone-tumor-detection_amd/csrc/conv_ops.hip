@@ -600,9 +600,17 @@ static int conv_dgrad_t(const void* dy, const void* wt, void* dx, ConvGeom g, co
 
 template <typename T>
 static int conv_wgrad_t(const void* dy, const void* x, float* dw, ConvGeom g, const float* sc,
-                        const float* sh, hipStream_t st) {
+                        const float* sh, hipStream_t st, const void* dyT = nullptr) {
   g.M = g.N * g.Ho * g.Wo;        // pixels (reduction)
   g.K = g.KH * g.KW * g.C;        // columns
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (dyT && !sc) {   // A = dy^T [Co][pixels]: K-contiguous, no transposing LDS reads
+      KMat<bf16> la{(const bf16*)dyT, g.M, g.Co, g.M};
+      EpiAtomic ep{nullptr, nullptr, dw, g.K, 1.0f};
+      ConvWgradB<bf16, false> lb{g, (const bf16*)x, nullptr, nullptr, g.K, make_pixstep(g, Elem<bf16>::BK)};
+      return gemm_wgrad<bf16>(g.Co, g.K, g.M, la, lb, ep, st);
+    }
+  }
   MNMat<T> la{(const T*)dy, g.Co, g.Co, g.M};
   EpiAtomic ep{nullptr, nullptr, dw, g.K, 1.0f};
   if (sc) {
@@ -697,11 +705,12 @@ VLP_EXPORT int vlp_conv_dgrad(int dtype, const void* dy, const void* wt, void* d
 
 VLP_EXPORT int vlp_conv_wgrad(int dtype, const void* dy, const void* x, float* dw_ws, int N, int H,
                               int W, int C, int Co, int KH, int KW, int S, int P,
-                              const float* in_scale, const float* in_shift, void* stream) {
+                              const float* in_scale, const float* in_shift, const void* dyT,
+                              void* stream) {
   ConvGeom g = make_geom(N, H, W, C, Co, KH, KW, S, P);
   hipStream_t st = (hipStream_t)stream;
   if ((long long)N * H * W * C >= (1ll << 31)) return (int)hipErrorInvalidValue;   // 32-bit pixel walk
-  if (dtype == VLP_BF16) return conv_wgrad_t<bf16>(dy, x, dw_ws, g, in_scale, in_shift, st);
+  if (dtype == VLP_BF16) return conv_wgrad_t<bf16>(dy, x, dw_ws, g, in_scale, in_shift, st, dyT);
   return conv_wgrad_t<float>(dy, x, dw_ws, g, in_scale, in_shift, st);
 }
 
@@ -756,14 +765,18 @@ VLP_EXPORT int vlp_stem_fwd(int dtype, const void* xp, const void* wp, void* y, 
 
 // dW_ws[64][256] (kh:8, kw:8, c:4 layout), fp32, accumulated atomically.
 VLP_EXPORT int vlp_stem_wgrad(int dtype, const void* dy, const void* xp, float* dw_ws, int N, int H,
-                              int W, void* stream) {
+                              int W, const void* dyT, void* stream) {
   StemGeom g = make_stem(N, H, W);
   hipStream_t st = (hipStream_t)stream;
   if ((long long)N * g.Hp * g.Wp * 4 >= (1ll << 31)) return (int)hipErrorInvalidValue;
   EpiAtomic ep{nullptr, nullptr, dw_ws, 256, 1.0f};
   if (dtype == VLP_BF16) {
-    MNMat<bf16> la{(const bf16*)dy, 64, 64, g.M};
     StemWgradB<bf16> lb{g, (const bf16*)xp};
+    if (dyT) {   // dy^T [64][pixels]: K-contiguous A operand
+      KMat<bf16> la{(const bf16*)dyT, g.M, 64, g.M};
+      return gemm_wgrad<bf16>(64, 224, g.M, la, lb, ep, st);
+    }
+    MNMat<bf16> la{(const bf16*)dy, 64, 64, g.M};
     return gemm_wgrad<bf16>(64, 224, g.M, la, lb, ep, st);
   }
   MNMat<float> la{(const float*)dy, 64, 64, g.M};

@@ -38,6 +38,7 @@ struct GemmShape {
   int kchunk;   // K range per split (multiple of BK); == K rounded up when no split
   int tiles_m, tiles_n;
   int xsplit;   // 1: split-K grid is 1-D and every split's tiles share one XCD
+  int dbg;      // diagnostics (VLP_GEMM_DBG, ms kernel): 1 skip epilogue, 2/4 freeze A/B MN rows
 };
 
 // ---------------- LDS image addressing (bytes) ----------------
@@ -415,7 +416,7 @@ struct GStagerN<T, BM, L, NT, true> {
       st[i] = ld.start(row0 + r, (p ^ ((r >> 1) & 7)) * Elem<T>::EPC, kb);
     }
   }
-  __device__ __forceinline__ void issue(const L& ld, int k0, char* lds) {
+  __device__ __forceinline__ void issue(const L& ld, int k0, char* lds, bool = false) {
     const int w = threadIdx.x >> 6;
     const auto stp = ld.step(k0);   // K-step-uniform context (scalar registers)
 #pragma unroll
@@ -450,7 +451,7 @@ struct GStagerN<T, BM, L, NT, false> {
     for (int i = 0; i < NI; ++i) cs[i] = ld.cstart(row0 + (i * NW + w) * 8);
     rs = ld.rstart(lane ^ ((w & 1) << 2), kb);
   }
-  __device__ __forceinline__ void issue(const L& ld, int, char* lds) {
+  __device__ __forceinline__ void issue(const L& ld, int, char* lds, bool freeze = false) {
     const int w = threadIdx.x >> 6;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
@@ -458,7 +459,7 @@ struct GStagerN<T, BM, L, NT, false> {
       __builtin_amdgcn_global_load_lds(p, (__attribute__((address_space(3))) void*)(lds + (i * NW + w) * 1024),
                                        16, 0, 0);
     }
-    ld.radvance(rs);
+    if (!freeze) ld.radvance(rs);
   }
 };
 
@@ -542,30 +543,46 @@ gemm_ms_kernel(GemmShape sh, LA la, LB lb, EP ep) {
       wait_vmcnt<0>();
     }
     raw_barrier();
-    if (t + S - 1 < nk) {
-      char* f = smem + fill * STAGE;
-      sa.issue(la, kb + (t + S - 1) * BK, f);
-      sb.issue(lb, kb + (t + S - 1) * BK, f + ABYTES);
-    }
+    // All fragments of tile t are read BEFORE tile t+S-1 is issued: hipcc
+    // cannot tell a ds_read_b64_tr_b16 from a read of the DMA target and
+    // would otherwise drain the just-issued loads (s_waitcnt vmcnt(0)) in
+    // front of the first transposed read, serialising load and compute.
     const char* ia = smem + slot * STAGE;
     const char* ib = ia + ABYTES;
+    v8bf fa[2][MB], fb[2][NB];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      v8bf fa[MB], fb[NB];
 #pragma unroll
-      for (int a = 0; a < MB; ++a) fa[a] = frag_bf16<LA::kKContig, GA::RB, true>(ia, wm * WTM + a * 16, s);
+      for (int a = 0; a < MB; ++a) fa[s][a] = frag_bf16<LA::kKContig, GA::RB, true>(ia, wm * WTM + a * 16, s);
 #pragma unroll
-      for (int b = 0; b < NB; ++b) fb[b] = frag_bf16<LB::kKContig, GB::RB, true>(ib, wn * WTN + b * 16, s);
+      for (int b = 0; b < NB; ++b) fb[s][b] = frag_bf16<LB::kKContig, GB::RB, true>(ib, wn * WTN + b * 16, s);
+    }
+    if (t + S - 1 < nk) {
+      char* f = smem + fill * STAGE;
+      sa.issue(la, kb + (t + S - 1) * BK, f, sh.dbg & 2);
+      sb.issue(lb, kb + (t + S - 1) * BK, f + ABYTES, sh.dbg & 4);
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
 #pragma unroll
       for (int a = 0; a < MB; ++a)
 #pragma unroll
         for (int b = 0; b < NB; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], acc[a][b], 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[s][b], fa[s][a], acc[a][b], 0, 0, 0);
     }
     slot = (slot + 1 == S) ? 0 : slot + 1;
     fill = (fill + 1 == S) ? 0 : fill + 1;
   }
   __syncthreads();   // all waves done with the ring before the epilogue reuses LDS
+  if (sh.dbg & 1) {   // diagnostics: no epilogue (acc kept live)
+    float z = 0.f;
+#pragma unroll
+    for (int a = 0; a < MB; ++a)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) z += acc[a][b][0] + acc[a][b][3];
+    if (z == 1234.5f) ep(row0, col0, acc[0][0], acc[0][0], acc[0][0]);
+    return;
+  }
 
   const int l = threadIdx.x & 63;
   const int li = l & 15, lg = l >> 4;
@@ -652,6 +669,7 @@ inline int launch_gemm_ms(int M, int N, int K, int ksplit, const LA& la, const L
   if (M <= 0 || N <= 0) return 0;
   GemmShape sh;
   sh.xsplit = 0;
+  sh.dbg = 0;
   sh.M = M; sh.N = N; sh.K = K;
   sh.tiles_m = (M + BM - 1) / BM;
   sh.tiles_n = (N + BN - 1) / BN;
@@ -677,6 +695,8 @@ inline int launch_gemm_ms(int M, int N, int K, int ksplit, const LA& la, const L
   if (ksplit < 1) ksplit = 1;
   sh.kchunk = kc;
   sh.xsplit = (ksplit >= 8 && ksplit % 8 == 0) ? 1 : 0;
+  static const int dbg = getenv("VLP_GEMM_DBG") ? atoi(getenv("VLP_GEMM_DBG")) : 0;
+  sh.dbg = dbg;
   dim3 grid = sh.xsplit ? dim3(sh.tiles_m * sh.tiles_n * ksplit, 1, 1)
                         : dim3(sh.tiles_m * sh.tiles_n, ksplit, 1);
   constexpr int lds = S * (BM + BN) * 128;
@@ -723,8 +743,8 @@ inline int gemm_wide(int M, int N, int K, int ksplit, const LA& la, const LB& lb
   if constexpr (use_ms<T, LA, LB>()) {
     switch (gemm_variant()) {
       case 0: return launch_gemm<T, 128, 128, 2>(M, N, K, ksplit, la, lb, ep, st);
-      case 1: return launch_gemm_ms<128, 128, 2, 2, 3>(M, N, K, ksplit, la, lb, ep, st);
-      case 2: return launch_gemm_ms<256, 128, 4, 2, 3>(M, N, K, ksplit, la, lb, ep, st);
+      case 1: return launch_gemm_ms<256, 128, 2, 2, 2>(M, N, K, ksplit, la, lb, ep, st);
+      case 2: return launch_gemm_ms<128, 256, 2, 2, 2>(M, N, K, ksplit, la, lb, ep, st);
       case 3: return launch_gemm_ms<128, 128, 2, 2, 2>(M, N, K, ksplit, la, lb, ep, st);
       default: return launch_gemm_ms<256, 128, 4, 2, 2>(M, N, K, ksplit, la, lb, ep, st);
     }
@@ -774,6 +794,7 @@ inline int launch_gemm(int M, int N, int K, int ksplit, const LA& la, const LB& 
   if (M <= 0 || N <= 0) return 0;
   GemmShape sh;
   sh.xsplit = 0;
+  sh.dbg = 0;
   sh.M = M; sh.N = N; sh.K = K;
   sh.tiles_m = (M + BM - 1) / BM;
   sh.tiles_n = (N + BN - 1) / BN;

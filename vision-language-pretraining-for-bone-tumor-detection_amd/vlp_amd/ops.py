@@ -75,14 +75,14 @@ def conv_dgrad(dy, wt, H, W, C, KH, KW, S, P, addend=None, y_bn=None, bn=None, s
     return dx
 
 
-def conv_wgrad(dy, x, KH, KW, S, P, dw_ws, in_scale=None, in_shift=None):
+def conv_wgrad(dy, x, KH, KW, S, P, dw_ws, in_scale=None, in_shift=None, dyT=None):
     N, H, W, C = x.shape
     Co = dy.shape[-1]
     Ho, Wo = dy.shape[1], dy.shape[2]
     tk = ktimer.begin(f"conv_wgrad[{'xf' if in_scale is not None else 'raw'}]{_tile_wgrad(Co)}",
                       2.0 * N * Ho * Wo * Co * C * KH * KW)
     lib().vlp_conv_wgrad(dcode(dy), ptr(dy), ptr(x), ptr(dw_ws), N, H, W, C, Co, KH, KW, S, P,
-                         ptr(in_scale), ptr(in_shift), _s())
+                         ptr(in_scale), ptr(in_shift), ptr(dyT), _s())
     ktimer.end(tk)
     return dw_ws
 
@@ -112,9 +112,9 @@ def stem_fwd(xp, wp, N, H, W, y, stat_sum, stat_sumsq, stat_rep=1):
     ktimer.end(tk)
 
 
-def stem_wgrad(dy, xp, N, H, W, dw_ws):
+def stem_wgrad(dy, xp, N, H, W, dw_ws, dyT=None):
     tk = ktimer.begin("stem_wgrad", 2.0 * dy.numel() * 147)
-    lib().vlp_stem_wgrad(dcode(dy), ptr(dy), ptr(xp), ptr(dw_ws), N, H, W, _s())
+    lib().vlp_stem_wgrad(dcode(dy), ptr(dy), ptr(xp), ptr(dw_ws), N, H, W, ptr(dyT), _s())
     ktimer.end(tk)
 
 
@@ -149,12 +149,14 @@ def bn_bwd_reduce(M, C, dout, dbc, HW, mask, ya, mean_a, istd_a, yb, mean_b, ist
                             ptr(sum_ga), ptr(sum_gb), int(stat_rep), _s())
 
 
-def bn_bwd_apply(M, C, dout, dbc, HW, mask, A, B, g_out, dtype_ref):
-    """A/B = (y, mean, istd, gamma, sum_g, sum_gx, dy_out) or None."""
+def bn_bwd_apply(M, C, dout, dbc, HW, mask, A, B, g_out, dtype_ref, dyT_a=None, dyT_b=None):
+    """A/B = (y, mean, istd, gamma, sum_g, sum_gx, dy_out) or None.  dyT_a/dyT_b:
+    optional [C][M] transposed copies of the dy outputs (bf16)."""
     a = A if A is not None else (None,) * 7
     b = B if B is not None else (None,) * 7
     lib().vlp_bn_bwd_apply(dcode(dtype_ref), M, C, ptr(dout), ptr(dbc), HW, ptr(mask),
-                           *[ptr(t) for t in a], *[ptr(t) for t in b], ptr(g_out), _s())
+                           *[ptr(t) for t in a], *[ptr(t) for t in b], ptr(g_out), ptr(dyT_a),
+                           ptr(dyT_b), _s())
 
 
 def bn_param_grad(sum_g, sum_gx, dgamma, dbeta):

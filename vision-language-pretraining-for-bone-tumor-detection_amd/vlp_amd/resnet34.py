@@ -350,7 +350,9 @@ class ResNet34Tower(ArenaModule):
                 ops.bn_param_grad(sg2, sgxd, self.arena.gview(kd + ".weight"), self.arena.gview(kd + ".bias"))
             else:
                 g_id = torch.empty_like(out)
-            ops.bn_bwd_apply(M, C, dout, dbc, HW, out, A, Bside, g_id, out)
+            tA = self._tbuf(ws, "tA", C, M)
+            tB = self._tbuf(ws, "tB", C, M) if (has_ds and tA is not None) else None
+            ops.bn_bwd_apply(M, C, dout, dbc, HW, out, A, Bside, g_id, out, dyT_a=tA, dyT_b=tB)
             # conv2: dgrad through relu(bn1(y1)) with BN1 backward sums; wgrad on relu(bn1(y1))
             sc1, sh1, mu1, is1 = self._coef(ws, k1)
             sg1f, sgx1f = self._bstat(ws, k1, full=True)
@@ -358,19 +360,20 @@ class ResNet34Tower(ArenaModule):
                                 bn=(sc1, sh1, mu1, is1), stat1=sg1f, stat2=sgx1f, stat_rep=STAT_REP)
             ops.stat_reduce(STAT_REP, C, sg1f, sgx1f)
             sg1, sgx1 = sg1f[:C], sgx1f[:C]
-            self._wgrad(ws, c2, dy2, B["a1"])
+            self._wgrad(ws, c2, dy2, B["a1"], dyT=tA)
             ops.bn_param_grad(sg1, sgx1, self.arena.gview(k1 + ".weight"), self.arena.gview(k1 + ".bias"))
             dy1 = torch.empty_like(y1)
             ops.bn_bwd_apply(M, C, g1, None, 1, None,
-                             (y1, mu1, is1, self.arena.view(k1 + ".weight"), sg1, sgx1, dy1), None, None, y1)
+                             (y1, mu1, is1, self.arena.view(k1 + ".weight"), sg1, sgx1, dy1), None, None, y1,
+                             dyT_a=tA)
             Hi, Wi = x.shape[1], x.shape[2]
             addend = g_id
             if has_ds:
                 cd = self._convs[pre + ".downsample.0"]
                 addend = ops.conv_dgrad(dyd, ws[cd.key + ".wt"], Hi, Wi, Cin, 1, 1, cd.S, 0)
-                self._wgrad(ws, cd, dyd, x)
+                self._wgrad(ws, cd, dyd, x, dyT=tB)
             dx = ops.conv_dgrad(dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, addend=addend)
-            self._wgrad(ws, c1, dy1, x)
+            self._wgrad(ws, c1, dy1, x, dyT=tA)
             dout = dx
         # stem: maxpool -> relu -> bn1 -> conv1
         y0, idx = saved["y0"], saved["idx"]
@@ -383,17 +386,31 @@ class ResNet34Tower(ArenaModule):
         ops.bn_param_grad(sg0, sgx0, self.arena.gview("bn1.weight"), self.arena.gview("bn1.bias"))
         dy0 = torch.empty_like(y0)
         M0 = y0.numel() // 64
+        t0 = self._tbuf(ws, "tA", 64, M0)
         ops.bn_bwd_apply(M0, 64, g0, None, 1, None,
-                         (y0, mu0, is0, self.arena.view("bn1.weight"), sg0, sgx0, dy0), None, None, y0)
+                         (y0, mu0, is0, self.arena.view("bn1.weight"), sg0, sgx0, dy0), None, None, y0,
+                         dyT_a=t0)
         o, n = self._wg_off["conv1"]
         wsb = ws["wgrad"][o:o + n]
-        ops.stem_wgrad(dy0, saved["xp"], saved["N"], saved["H"], saved["W"], wsb)
+        ops.stem_wgrad(dy0, saved["xp"], saved["N"], saved["H"], saved["W"], wsb, dyT=t0)
         ops.unpack_stem_grad(wsb, self.arena.gview("conv1.weight"))
 
-    def _wgrad(self, ws, c, dy, x, sc=None, sh=None):
+    def _tbuf(self, ws, name, C, M):
+        """[C][M] bf16 scratch for a transposed output gradient (the weight-gradient
+        GEMM's pixel-contiguous A operand), or None where the transposing BN
+        backward does not apply (fp32 parity mode, odd shapes)."""
+        if self.tdtype != torch.bfloat16 or C % 64 or M % 8:
+            return None
+        buf = ws.get(name)
+        if buf is None or buf.numel() < C * M:
+            buf = torch.empty(C * M, dtype=torch.bfloat16, device=self.arena.data.device)
+            ws[name] = buf
+        return buf[:C * M].view(C, M)
+
+    def _wgrad(self, ws, c, dy, x, sc=None, sh=None, dyT=None):
         o, n = self._wg_off[c.key]
         buf = ws["wgrad"][o:o + n]
-        ops.conv_wgrad(dy, x, c.KH, c.KW, c.S, c.P, buf, sc, sh)
+        ops.conv_wgrad(dy, x, c.KH, c.KW, c.S, c.P, buf, sc, sh, dyT=dyT)
         ops.unpack_conv_grad(buf, self.arena.gview(c.key + ".weight"))
 
     # ---------------- autograd entry ----------------
