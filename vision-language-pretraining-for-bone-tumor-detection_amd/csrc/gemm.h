@@ -53,6 +53,21 @@ __device__ __forceinline__ int mn_off(int k, int byte_in_row) {
   return k * RB + ((((byte_in_row >> 5) ^ sw) << 5) | (byte_in_row & 31));
 }
 
+// Blocked MN-contig image (direct staging): 1-KiB blocks of 8 k-rows x 8
+// 16-B chunks, block (k>>3, c>>3) at ((k>>3)*CPB + (c>>3)) KiB (CPB = chunk
+// blocks per k-row = MN/64); inside a block, chunk c&7 of row k&7 sits at
+// 16*((c&7) ^ h(k)), h = bit1(k)<<1 | bit3(k)<<2: the two 32-lane halves of a
+// ds_read_b64_tr_b16 fragment read (rows 32s+8g+q, chunk pair c0, c0+1)
+// land on 32 distinct 8-B bank slots.  Each 1-KiB block is ONE wave-wide
+// LDS-DMA of 8 rows x 128 B: 8 full cache lines per load instruction.
+__device__ __forceinline__ int mn8_h(int k) { return (((k >> 1) & 1) << 1) | (((k >> 3) & 1) << 2); }
+template <int CPB>
+__device__ __forceinline__ int mn8_off(int k, int mn) {
+  const int c = mn >> 3;
+  return ((k >> 3) * CPB + (c >> 3)) * 1024 + (k & 7) * 128 + (((c & 7) ^ mn8_h(k)) << 4) +
+         ((mn & 4) << 1);
+}
+
 template <typename T, int BM, bool KC>
 struct TileGeom {
   static constexpr int EPC = Elem<T>::EPC;
@@ -189,9 +204,8 @@ struct OpStager<T, BM, L, true> {
 // k-permutation shared by both operands, chosen so a K-contig fragment is ONE
 // 16-B chunk (ds_read_b128, conflict-free under the kc_off swizzle) and an
 // MN-contig fragment is two ds_read_b64_tr_b16 (k-rows 32s+8g+q, +4).
-// MNCOL: MN-contig image in the column-major chunk layout of the direct MN
-// stager (GStagerN<..., false>): chunk column cb = mn/8 is 1 KiB of 64 k-rows
-// x 16 B, rows XOR 4 on odd columns (conflict-free tr reads).
+// MNCOL: MN-contig image in the blocked layout of the direct MN stager
+// (GStagerN<..., false>, mn8_off): 1-KiB blocks of 8 k-rows x 8 chunks.
 template <bool KC, int RB, bool MNCOL = false>
 __device__ __forceinline__ v8bf frag_bf16(const char* lds, int rb, int s) {
   const int l = threadIdx.x & 63;
@@ -203,11 +217,9 @@ __device__ __forceinline__ v8bf frag_bf16(const char* lds, int rb, int s) {
     const int q = i >> 2, p = i & 3;
     const int k1 = 32 * s + 8 * g + q;
     if constexpr (MNCOL) {
-      const int mn = rb + 4 * p, cb = mn >> 3;
-      const int base = cb * 1024 + ((mn & 4) << 1);
-      const int sw = (cb & 1) << 2;
-      lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(lds + base + ((k1 ^ sw) << 4)));
-      hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(lds + base + (((k1 + 4) ^ sw) << 4)));
+      const int mn = rb + 4 * p;
+      lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(lds + mn8_off<RB / 128>(k1, mn)));
+      hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(lds + mn8_off<RB / 128>(k1 + 4, mn)));
     } else {
       const int by = (rb + 4 * p) * 2;
       lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(lds + mn_off<RB>(k1, by)));
@@ -427,39 +439,50 @@ struct GStagerN<T, BM, L, NT, true> {
     }
   }
 };
-// MN-contig operand: column-major chunk image -- chunk column cb (8 MN values)
-// is 1 KiB = 64 k-rows x 16 B, k-row XOR 4 on odd columns.  Wave w,
-// instruction i fills column cb = i*NW + w, lane L its physical row L, so all
-// of a thread's chunks share ONE k-row (logical k = L ^ 4*(w&1)): the loader's
-// per-k state (e.g. the output pixel of a weight-gradient reduction) is walked
-// once per thread per K-step and combined with fixed per-column offsets:
+// MN-contig operand, blocked image (mn8_off): wave w's instruction i fills
+// 1-KiB block b = w*NI + i = (k-row block b / CPB, chunk block b % CPB), lane
+// L row k = 8*(b / CPB) + L/8 -- 8 full 128-B lines per instruction.  The
+// loader's per-k state (e.g. the output pixel of a weight-gradient
+// reduction) is walked once per distinct row of the thread (NI / CPB rows)
+// and combined with a fixed offset per chunk column:
 //   RState rstart(int k, int kb); void radvance(RState&)      per k-row
 //   CState cstart(int mn)                                      per column
 //   const void* addr(const RState&, const CState&)             address / zero page
 template <typename T, int BM, class L, int NT>
 struct GStagerN<T, BM, L, NT, false> {
   static constexpr int NW = NT / 64;
-  static constexpr int NCOL = BM / 8;
-  static constexpr int NI = NCOL / NW;
-  static_assert(NI >= 1 && NCOL % NW == 0 && NW % 2 == 0, "tile / thread geometry");
+  static constexpr int CPB = BM / 64;              // chunk blocks per k-row block
+  static constexpr int NI = 8 * CPB / NW;          // 1-KiB blocks per thread
+  static constexpr int NR = NI >= CPB ? NI / CPB : 1;   // distinct k-rows per thread
+  static_assert(NI >= 1 && (8 * CPB) % NW == 0 && (NI % CPB == 0 || CPB % NI == 0), "tile / thread geometry");
   static_assert(sizeof(T) == 2, "MN direct staging is bf16 (BK = 64 rows)");
-  typename L::RState rs;
+  typename L::RState rs[NR];
   typename L::CState cs[NI];
   __device__ __forceinline__ void init(const L& ld, int row0, int kb) {
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
-    for (int i = 0; i < NI; ++i) cs[i] = ld.cstart(row0 + (i * NW + w) * 8);
-    rs = ld.rstart(lane ^ ((w & 1) << 2), kb);
+    for (int i = 0; i < NI; ++i) {
+      const int b = w * NI + i;
+      const int k = 8 * (b / CPB) + (lane >> 3);
+      const int c = 8 * (b % CPB) + ((lane & 7) ^ mn8_h(k));
+      cs[i] = ld.cstart(row0 + c * 8);
+      if (i % CPB == 0 || NI < CPB) {
+        if (i / CPB < NR) rs[i / CPB] = ld.rstart(k, kb);
+      }
+    }
   }
   __device__ __forceinline__ void issue(const L& ld, int, char* lds, bool freeze = false) {
     const int w = threadIdx.x >> 6;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const void* p = ld.addr(rs, cs[i]);
-      __builtin_amdgcn_global_load_lds(p, (__attribute__((address_space(3))) void*)(lds + (i * NW + w) * 1024),
+      const void* p = ld.addr(rs[NI >= CPB ? i / CPB : 0], cs[i]);
+      __builtin_amdgcn_global_load_lds(p, (__attribute__((address_space(3))) void*)(lds + (w * NI + i) * 1024),
                                        16, 0, 0);
     }
-    if (!freeze) ld.radvance(rs);
+    if (!freeze) {
+#pragma unroll
+      for (int r = 0; r < NR; ++r) ld.radvance(rs[r]);
+    }
   }
 };
 

@@ -26,6 +26,8 @@ from __future__ import annotations
 
 from typing import List, Optional
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -36,6 +38,7 @@ LAYERS = (3, 4, 6, 3)
 WIDTHS = (64, 128, 256, 512)
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
+_USE_DYT = os.environ.get("VLP_WGRAD_DYT", "1") != "0"
 STAT_REP = 64   # replicas of per-channel fp64 sums (see vlp_stat_reduce)
 
 
@@ -399,7 +402,7 @@ class ResNet34Tower(ArenaModule):
         """[C][M] bf16 scratch for a transposed output gradient (the weight-gradient
         GEMM's pixel-contiguous A operand), or None where the transposing BN
         backward does not apply (fp32 parity mode, odd shapes)."""
-        if self.tdtype != torch.bfloat16 or C % 64 or M % 8:
+        if self.tdtype != torch.bfloat16 or C % 64 or M % 8 or not _USE_DYT:
             return None
         buf = ws.get(name)
         if buf is None or buf.numel() < C * M:
