@@ -1,6 +1,4 @@
 cd $GRAFT_REPO_ROOT
-for e in "VLP_WGRAD_DYT=1" "VLP_WGRAD_DYT=0"; do
-  env $e timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --kernel-report gpurun_out/kr_ab.json > gpurun_out/ab.log 2>&1 || { echo FAIL $e; tail -5 gpurun_out/ab.log; exit 1; }
-  echo "$e $(tail -1 gpurun_out/ab.log | cut -c1-200)"
-  python tools/kreport.py gpurun_out/kr_ab.json 8
+for d in 0 1 6 7; do
+  echo "dbg=$d $(VLP_GEMM_DBG=$d timeout -k 10 120 python tools/conv_bench.py --ops fwd,dgrad --layers l1,l3 2>&1 | grep -E '^(fwd|dgrad)' | tr '\n' ' ')"
 done

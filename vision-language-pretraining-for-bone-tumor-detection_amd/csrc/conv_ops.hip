@@ -536,9 +536,13 @@ static int gemm_auto(int M, int N, int K, int ksplit, const LA& la, const LB& lb
 template <typename T, class LA, class LB, class EP>
 static int gemm_wgrad(int M, int N, int K, const LA& la, const LB& lb, const EP& ep, hipStream_t st) {
   if (M <= 64) return gemm_short<T>(M, N, K, -2048, la, lb, ep, st);
+  static const int balanced = getenv("VLP_WGRAD_BALANCED") ? atoi(getenv("VLP_WGRAD_BALANCED")) : 0;
+  if (balanced) return gemm_wide<T>(M, N, K, -balanced, la, lb, ep, st);
+  static const int target = getenv("VLP_WGRAD_TARGET") ? atoi(getenv("VLP_WGRAD_TARGET")) : 1024;
+  static const int mink = getenv("VLP_WGRAD_MINK") ? atoi(getenv("VLP_WGRAD_MINK")) : 4096;
   const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
-  int ksplit = (1024 + tiles - 1) / tiles;
-  const int maxsplit = (K + 4095) / 4096;
+  int ksplit = (target + tiles - 1) / tiles;
+  const int maxsplit = (K + mink - 1) / mink;
   if (ksplit > maxsplit) ksplit = maxsplit;
   if (ksplit >= 8) ksplit = (ksplit + 7) / 8 * 8;
   return gemm_wide<T>(M, N, K, ksplit, la, lb, ep, st);

@@ -68,6 +68,21 @@ __device__ __forceinline__ int mn8_off(int k, int mn) {
          ((mn & 4) << 1);
 }
 
+// Sum over each 16-lane DPP row (the 16 rows of an MFMA output block);
+// lane 15 of the row receives the total.  Four row_shr DPP adds: VALU only,
+// where __shfl_xor would issue ds_bpermute LDS traffic.
+__device__ __forceinline__ float row16_sum(float x) {
+  int v = __builtin_bit_cast(int, x);
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true));
+  v = __builtin_bit_cast(int, x);
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true));
+  v = __builtin_bit_cast(int, x);
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true));
+  v = __builtin_bit_cast(int, x);
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true));
+  return x;
+}
+
 template <typename T, int BM, bool KC>
 struct TileGeom {
   static constexpr int EPC = Elem<T>::EPC;
@@ -370,13 +385,8 @@ gemm_kernel(GemmShape sh, LA la, LB lb, EP ep) {
     if constexpr (EP::kStats) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float x = s1[j], y = s2[j];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          x += __shfl_xor(x, o, 64);
-          y += __shfl_xor(y, o, 64);
-        }
-        if (li == 0) {
+        const float x = row16_sum(s1[j]), y = row16_sum(s2[j]);
+        if (li == 15) {
           const int cl = wn * WTN + b * 16 + 4 * lg + j;
           red[(wm * BN + cl) * 2 + 0] = x;
           red[(wm * BN + cl) * 2 + 1] = y;
@@ -626,13 +636,8 @@ gemm_ms_kernel(GemmShape sh, LA la, LB lb, EP ep) {
     if constexpr (EP::kStats) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        float x = s1[j], y = s2[j];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          x += __shfl_xor(x, o, 64);
-          y += __shfl_xor(y, o, 64);
-        }
-        if (li == 0) {
+        const float x = row16_sum(s1[j]), y = row16_sum(s2[j]);
+        if (li == 15) {
           const int cl = wn * WTN + b * 16 + 4 * lg + j;
           red[(wm * BN + cl) * 2 + 0] = x;
           red[(wm * BN + cl) * 2 + 1] = y;
@@ -766,8 +771,6 @@ inline int gemm_wide(int M, int N, int K, int ksplit, const LA& la, const LB& lb
   if constexpr (use_ms<T, LA, LB>()) {
     switch (gemm_variant()) {
       case 0: return launch_gemm<T, 128, 128, 2>(M, N, K, ksplit, la, lb, ep, st);
-      case 1: return launch_gemm_ms<256, 128, 2, 2, 2>(M, N, K, ksplit, la, lb, ep, st);
-      case 2: return launch_gemm_ms<128, 256, 2, 2, 2>(M, N, K, ksplit, la, lb, ep, st);
       case 3: return launch_gemm_ms<128, 128, 2, 2, 2>(M, N, K, ksplit, la, lb, ep, st);
       default: return launch_gemm_ms<256, 128, 4, 2, 2>(M, N, K, ksplit, la, lb, ep, st);
     }
@@ -782,8 +785,6 @@ inline int gemm_narrow(int M, int N, int K, int ksplit, const LA& la, const LB& 
   if constexpr (use_ms<T, LA, LB>()) {
     switch (gemm_variant()) {
       case 0: return launch_gemm<T, 256, 64, 4>(M, N, K, ksplit, la, lb, ep, st);
-      case 1: return launch_gemm_ms<256, 64, 4, 1, 3>(M, N, K, ksplit, la, lb, ep, st);
-      case 2: return launch_gemm_ms<512, 64, 8, 1, 2>(M, N, K, ksplit, la, lb, ep, st);
       case 3: return launch_gemm_ms<256, 64, 4, 1, 2>(M, N, K, ksplit, la, lb, ep, st);
       default: return launch_gemm_ms<256, 64, 4, 1, 4>(M, N, K, ksplit, la, lb, ep, st);
     }
@@ -798,10 +799,7 @@ inline int gemm_short(int M, int N, int K, int ksplit, const LA& la, const LB& l
   if constexpr (use_ms<T, LA, LB>()) {
     switch (gemm_variant()) {
       case 0: return launch_gemm<T, 64, 128, 1>(M, N, K, ksplit, la, lb, ep, st);
-      case 1: return launch_gemm_ms<64, 128, 1, 4, 3>(M, N, K, ksplit, la, lb, ep, st);
-      case 2: return launch_gemm_ms<64, 256, 1, 8, 3>(M, N, K, ksplit, la, lb, ep, st);
-      case 3: return launch_gemm_ms<64, 128, 1, 4, 2>(M, N, K, ksplit, la, lb, ep, st);
-      default: return launch_gemm_ms<64, 128, 1, 4, 4>(M, N, K, ksplit, la, lb, ep, st);
+      default: return launch_gemm_ms<64, 128, 1, 4, 2>(M, N, K, ksplit, la, lb, ep, st);
     }
   } else {
     return launch_gemm<T, 64, 128, 1>(M, N, K, ksplit, la, lb, ep, st);

@@ -38,7 +38,7 @@ LAYERS = (3, 4, 6, 3)
 WIDTHS = (64, 128, 256, 512)
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
-_USE_DYT = os.environ.get("VLP_WGRAD_DYT", "1") != "0"
+_USE_DYT = os.environ.get("VLP_WGRAD_DYT", "0") != "0"   # measured: the extra transposed write costs more than it saves
 STAT_REP = 64   # replicas of per-channel fp64 sums (see vlp_stat_reduce)
 
 
