@@ -248,14 +248,21 @@ struct EpiS2Remap {
   static constexpr bool kStats = EP::kStats;
   double* stat1; double* stat2; int stat_rep;
   EP inner; S2Class c; int H, W;
-  __device__ void operator()(int row, int col, v4f v, v4f& s1, v4f& s2) const {
+  __device__ int grow(int row) const {
     int n = fdiv(row, c.fd_hwc);
     int r = row - n * c.Hc * c.Wc;
     int i = fdiv(r, c.fd_wc);
     int j = r - i * c.Wc;
-    int grow = (n * H + 2 * i + c.ph) * W + 2 * j + c.pw;
-    inner(grow, col, v, s1, s2);
+    return (n * H + 2 * i + c.ph) * W + 2 * j + c.pw;
   }
+  __device__ void operator()(int row, int col, v4f v, v4f& s1, v4f& s2) const {
+    inner(grow(row), col, v, s1, s2);
+  }
+  static constexpr bool kStage = true;
+  __device__ v4f value(int row, int col, v4f v, v4f& s1, v4f& s2) const {
+    return inner.value(grow(row), col, v, s1, s2);
+  }
+  __device__ void store8(int row, int col, const uint4& u) const { inner.store8(grow(row), col, u); }
 };
 // class B operand: B(ci, k = (a, b, co)) = Wt[ci][kh0 + 2a][kw0 + 2b][co]
 template <typename T>
@@ -484,6 +491,14 @@ struct EpiConvFwd {
     s1 = v;
     s2 = v * v;
   }
+  // staged form (multi-stage kernel): value() -> LDS tile -> 16-B row stores
+  static constexpr bool kStage = true;
+  __device__ v4f value(int, int, v4f v, v4f& s1, v4f& s2) const {
+    s1 = v;
+    s2 = v * v;
+    return v;
+  }
+  __device__ void store8(int row, int col, const uint4& u) const { stg16(y + (size_t)row * Co + col, u); }
 };
 // data gradient through the producer's ReLU (mask from BN-applied y), plus
 // that BN's backward statistics: sum(g), sum(g * xhat).
@@ -506,6 +521,21 @@ struct EpiDgradBN {
     s1 = g;
     s2 = g * ((yv - mu) * is);
   }
+  static constexpr bool kStage = true;
+  __device__ v4f value(int row, int col, v4f v, v4f& s1, v4f& s2) const {
+    v4f yv = load4(y + (size_t)row * C + col);
+    v4f sc4 = *reinterpret_cast<const v4f*>(sc + col);
+    v4f sh4 = *reinterpret_cast<const v4f*>(sh + col);
+    v4f mu = *reinterpret_cast<const v4f*>(mean + col);
+    v4f is = *reinterpret_cast<const v4f*>(invstd + col);
+    v4f g;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) g[j] = (fmaf(yv[j], sc4[j], sh4[j]) > 0.f) ? v[j] : 0.f;
+    s1 = g;
+    s2 = g * ((yv - mu) * is);
+    return g;
+  }
+  __device__ void store8(int row, int col, const uint4& u) const { stg16(g_out + (size_t)row * C + col, u); }
 };
 // data gradient plus a residual-branch gradient
 template <typename T>
@@ -518,6 +548,12 @@ struct EpiDgradAdd {
     if (addend) v += load4(addend + o);
     store4(dx + o, v);
   }
+  static constexpr bool kStage = true;
+  __device__ v4f value(int row, int col, v4f v, v4f&, v4f&) const {
+    if (addend) v += load4(addend + (size_t)row * C + col);
+    return v;
+  }
+  __device__ void store8(int row, int col, const uint4& u) const { stg16(dx + (size_t)row * C + col, u); }
 };
 
 // ---------------- tile-config dispatch ----------------

@@ -159,6 +159,10 @@ static __device__ uint4 g_zero16;
 __device__ __forceinline__ const void* zero_page() { return &g_zero16; }
 
 template <class L, class = void> struct DirectTrait { static constexpr bool value = false; };
+template <class E, class = void> struct StageTrait { static constexpr bool value = false; };
+template <class E> struct StageTrait<E, std::void_t<decltype(E::kStage)>> {
+  static constexpr bool value = E::kStage;
+};
 template <class L> struct DirectTrait<L, std::void_t<decltype(L::kDirect)>> {
   static constexpr bool value = L::kDirect;
 };
@@ -620,16 +624,34 @@ gemm_ms_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   const int l = threadIdx.x & 63;
   const int li = l & 15, lg = l >> 4;
   float* red = reinterpret_cast<float*>(smem);
+  // staged epilogues: outputs go through a bf16 LDS tile (16-B chunks XOR-
+  // swizzled by row) and leave as full 16-B row segments, 4..8 rows per wave
+  // store instead of 32-B pieces of 16 rows
+  constexpr bool kStage = StageTrait<EP>::value;
+  constexpr int CPR = BN / 8;
+  bf16* stg = reinterpret_cast<bf16*>(smem + 4096);
+  static_assert(!kStage || 4096 + BM * BN * 2 <= S * STAGE, "staging tile fits the ring");
+  static_assert(WGM * BN * 2 * 4 <= 4096, "stats scratch");
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    const int col = col0 + wn * WTN + b * 16 + 4 * lg;
+    const int coll = wn * WTN + b * 16 + 4 * lg;
+    const int col = col0 + coll;
     v4f s1 = v4f{0.f, 0.f, 0.f, 0.f}, s2 = s1;
 #pragma unroll
     for (int a = 0; a < MB; ++a) {
-      const int row = row0 + wm * WTM + a * 16 + li;
+      const int rowl = wm * WTM + a * 16 + li;
+      const int row = row0 + rowl;
       if (row < sh.M && col < sh.N) {
         v4f c1 = v4f{0.f, 0.f, 0.f, 0.f}, c2 = c1;
-        ep(row, col, acc[a][b], c1, c2);
+        if constexpr (kStage) {
+          const v4f o = ep.value(row, col, acc[a][b], c1, c2);
+          v4bf ob;
+          ob[0] = (bf16)o[0]; ob[1] = (bf16)o[1]; ob[2] = (bf16)o[2]; ob[3] = (bf16)o[3];
+          *reinterpret_cast<v4bf*>(stg + rowl * BN + (((coll >> 3) ^ (rowl & (CPR - 1))) << 3) +
+                                   (coll & 4)) = ob;
+        } else {
+          ep(row, col, acc[a][b], c1, c2);
+        }
         if constexpr (EP::kStats) { s1 += c1; s2 += c2; }
       }
     }
@@ -643,6 +665,16 @@ gemm_ms_kernel(GemmShape sh, LA la, LB lb, EP ep) {
           red[(wm * BN + cl) * 2 + 1] = y;
         }
       }
+    }
+  }
+  if constexpr (kStage) {
+    __syncthreads();
+#pragma unroll 4
+    for (int q = threadIdx.x; q < BM * CPR; q += NT) {
+      const int r = q / CPR, c = q - r * CPR;
+      const int row = row0 + r, col = col0 + c * 8;
+      if (row < sh.M && col < sh.N)
+        ep.store8(row, col, *reinterpret_cast<const uint4*>(stg + r * BN + ((c ^ (r & (CPR - 1))) << 3)));
     }
   }
   if constexpr (EP::kStats) {
