@@ -34,7 +34,7 @@ def main():
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     res = {}
-    for ln in args.layers.split(","):
+    for ln in [l for l in args.layers.split(",") if l]:
         N, H, W, C, Co, KH, KW, S, P = LAYERS[ln]
         Ho, Wo = (H + 2 * P - KH) // S + 1, (W + 2 * P - KW) // S + 1
         x = (torch.randn(N, H, W, C, device=dev) * 0.5).to(torch.bfloat16)

@@ -1,0 +1,26 @@
+"""Summarise rocprofv3 --pmc counter_collection CSVs: per kernel (short name),
+mean value of each counter over its dispatches.
+  python tools/pmc_summary.py file1.csv [file2.csv ...]"""
+import csv
+import re
+import sys
+from collections import defaultdict
+
+
+def short(k):
+    m = re.search(r"gemm_ms_kernelILi(\d+)ELi(\d+)E.*?NS_\d+(\w+?)I", k)
+    if m:
+        return f"gemm{m.group(1)}x{m.group(2)}:{m.group(3)}"
+    return k[:60]
+
+
+vals = defaultdict(lambda: defaultdict(list))
+for path in sys.argv[1:]:
+    for r in csv.DictReader(open(path)):
+        vals[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, d in vals.items():
+    if "gemm" not in k and "conv" not in k.lower():
+        continue
+    print(k)
+    for c, v in sorted(d.items()):
+        print(f"   {c:28s} {sum(v) / len(v):16.1f}  (n={len(v)})")

@@ -113,6 +113,33 @@ struct ConvFwdA {
                    ((unsigned)(d.wi0 + s.kw) < (unsigned)g.W);
     return v ? (const void*)(x + d.off + s.delta) : zero_page();
   }
+  // buffer protocol (gemm_bk / gemm_big): the chunk's row is fixed, so the
+  // validity of all KH*KW taps is one bit mask computed once; a K-step is
+  // (tap, channel offset) -> one scalar byte delta
+  static constexpr bool kBuf = !XF;
+  struct BState { unsigned base; unsigned mask; };
+  struct BStep { unsigned delta; unsigned tap; };
+  __device__ rsrc_t rsrc() const { return buf_rsrc(x, (unsigned)((size_t)g.N * g.H * g.W * g.C * sizeof(T))); }
+  __device__ BState bstart(int m, int koff, int) const {
+    const State f = fixed(m);
+    unsigned mask = 0;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw)
+        if (kh < g.KH && kw < g.KW && (unsigned)(f.hi0 + kh) < (unsigned)g.H && (unsigned)(f.wi0 + kw) < (unsigned)g.W)
+          mask |= 1u << (kh * g.KW + kw);
+    const long long e = (long long)(f.base - x) + ((long long)f.hi0 * g.W + f.wi0) * g.C + koff;
+    return BState{(unsigned)(e * (long long)sizeof(T)), f.ok ? mask : 0u};
+  }
+  __device__ BStep bstep(int k0) const {
+    const int tap = fdiv(k0, g.fd_c), ci0 = k0 - tap * g.C;
+    const int kh = fdiv(tap, g.fd_kw), kw = tap - kh * g.KW;
+    return BStep{(unsigned)((((long long)kh * g.W + kw) * g.C + ci0) * (long long)sizeof(T)), (unsigned)tap};
+  }
+  __device__ unsigned boff(BState& s, const BStep& st) const {
+    return ((s.mask >> st.tap) & 1u) ? s.base + st.delta : kOOB;
+  }
 };
 
 // ---- data-gradient A operand (stride 1): output-gradient "patches", K-contiguous ----
@@ -169,6 +196,31 @@ struct ConvDgradA {
     const bool v = d.ok & s.kv & ((unsigned)(d.hp - s.kh) < (unsigned)g.Ho) &
                    ((unsigned)(d.wp - s.kw) < (unsigned)g.Wo);
     return v ? (const void*)(dy + d.off + s.delta) : zero_page();
+  }
+  // buffer protocol (stride 1): per-chunk tap mask, scalar byte delta per K-step
+  static constexpr bool kBuf = true;
+  struct BState { unsigned base; unsigned mask; };
+  struct BStep { unsigned delta; unsigned tap; };
+  __device__ rsrc_t rsrc() const { return buf_rsrc(dy, (unsigned)((size_t)g.N * g.Ho * g.Wo * g.Co * sizeof(T))); }
+  __device__ BState bstart(int m, int koff, int) const {
+    const State f = fixed(m);
+    unsigned mask = 0;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw)
+        if (kh < g.KH && kw < g.KW && (unsigned)(f.hp - kh) < (unsigned)g.Ho && (unsigned)(f.wp - kw) < (unsigned)g.Wo)
+          mask |= 1u << (kh * g.KW + kw);
+    const long long e = (long long)(f.base - dy) + ((long long)f.hp * g.Wo + f.wp) * g.Co + koff;
+    return BState{(unsigned)(e * (long long)sizeof(T)), f.ok ? mask : 0u};
+  }
+  __device__ BStep bstep(int k0) const {
+    const int tap = fdiv(k0, g.fd_co), co0 = k0 - tap * g.Co;
+    const int kh = fdiv(tap, g.fd_kw), kw = tap - kh * g.KW;
+    return BStep{(unsigned)((co0 - ((long long)kh * g.Wo + kw) * g.Co) * (long long)sizeof(T)), (unsigned)tap};
+  }
+  __device__ unsigned boff(BState& s, const BStep& st) const {
+    return ((s.mask >> st.tap) & 1u) ? s.base + st.delta : kOOB;
   }
 };
 
@@ -241,6 +293,31 @@ struct ConvDgradS2A {
                    ((unsigned)(d.wb - s.b) < (unsigned)g.Wo);
     return v ? (const void*)(dy + d.off + s.delta) : zero_page();
   }
+  // buffer protocol: tap (a, b) of the class -> bit a*ntw + b
+  static constexpr bool kBuf = true;
+  struct BState { unsigned base; unsigned mask; };
+  struct BStep { unsigned delta; unsigned tap; };
+  __device__ rsrc_t rsrc() const { return buf_rsrc(dy, (unsigned)((size_t)g.N * g.Ho * g.Wo * g.Co * sizeof(T))); }
+  __device__ BState bstart(int m, int koff, int) const {
+    const State f = fixed(m);
+    unsigned mask = 0;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        if (a < c.nth && b < c.ntw && (unsigned)(f.hb - a) < (unsigned)g.Ho && (unsigned)(f.wb - b) < (unsigned)g.Wo)
+          mask |= 1u << (a * c.ntw + b);
+    const long long e = (long long)(f.base - dy) + ((long long)f.hb * g.Wo + f.wb) * g.Co + koff;
+    return BState{(unsigned)(e * (long long)sizeof(T)), f.ok ? mask : 0u};
+  }
+  __device__ BStep bstep(int k0) const {
+    const int tap = fdiv(k0, g.fd_co), co0 = k0 - tap * g.Co;
+    const int a = fdiv(tap, c.fd_ntw), b = tap - a * c.ntw;
+    return BStep{(unsigned)((co0 - ((long long)a * g.Wo + b) * g.Co) * (long long)sizeof(T)), (unsigned)tap};
+  }
+  __device__ unsigned boff(BState& s, const BStep& st) const {
+    return ((s.mask >> st.tap) & 1u) ? s.base + st.delta : kOOB;
+  }
 };
 // class-local row -> global NHWC row, then the wrapped epilogue
 template <class EP>
@@ -296,6 +373,20 @@ struct WtS2B {
   __device__ const void* next(DState& d, const Step& s) const {
     return (d.ok & s.kv) ? (const void*)(d.p + s.delta) : zero_page();
   }
+  // buffer protocol (Kc is a multiple of the K-step: no per-chunk k check)
+  static constexpr bool kBuf = true;
+  struct BState { unsigned o; };
+  struct BStep { unsigned delta; };
+  __device__ rsrc_t rsrc() const { return buf_rsrc(wt, (unsigned)((size_t)g.C * g.KH * g.KW * g.Co * sizeof(T))); }
+  __device__ BState bstart(int ci, int koff, int) const {
+    return BState{ci < g.C ? (unsigned)(((size_t)ci * g.KH * g.KW * g.Co + koff) * sizeof(T)) : kOOB};
+  }
+  __device__ BStep bstep(int k0) const {
+    const int tap = fdiv(k0, g.fd_co), co0 = k0 - tap * g.Co;
+    const int a = fdiv(tap, c.fd_ntw), b = tap - a * c.ntw;
+    return BStep{(unsigned)((((long long)(c.kh0 + 2 * a) * g.KW + c.kw0 + 2 * b) * g.Co + co0) * (long long)sizeof(T))};
+  }
+  __device__ unsigned boff(BState& s, const BStep& st) const { return s.o + st.delta; }
 };
 
 // ---- weight-gradient B operand: input patches, MN-contiguous over (kh,kw,ci) ----
@@ -380,6 +471,65 @@ struct ConvWgradB {
     r.ho = ch ? r.ho - g.Ho : r.ho;
     r.poff = ch ? r.poff + ps.carry_h : r.poff;
   }
+  // buffer protocol: per pixel row a KH*KW tap-validity mask (recomputed as
+  // the row walks), per chunk column a fixed byte offset and tap index
+  static constexpr bool kBuf = !XF;
+  struct BRow { int poff, hs, ws, mm; unsigned tmask; };   // poff: bytes of (n, ho*S, wo*S)
+  struct BCol { unsigned ofs, tap; };
+  __device__ rsrc_t rsrc() const { return buf_rsrc(x, (unsigned)((size_t)g.N * g.H * g.W * g.C * sizeof(T))); }
+  __device__ unsigned tapmask(int hs, int ws, int mm) const {
+    unsigned wm = 0, m = 0;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw)
+      if (kw < g.KW && (unsigned)(ws - g.P + kw) < (unsigned)g.W) wm |= 1u << kw;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+      if (kh < g.KH && (unsigned)(hs - g.P + kh) < (unsigned)g.H) m |= wm << (kh * g.KW);
+    return mm < g.M ? m : 0u;
+  }
+  __device__ void blocate(BRow& r) const {
+    const int mm = r.mm < g.M ? r.mm : 0;
+    const int n = fdiv(mm, g.fd_howo);
+    const int rr = mm - n * g.Ho * g.Wo;
+    const int ho = fdiv(rr, g.fd_wo);
+    const int wo = rr - ho * g.Wo;
+    r.hs = ho * g.S;
+    r.ws = wo * g.S;
+    r.poff = ((n * g.H + r.hs) * g.W + r.ws) * g.C * (int)sizeof(T);
+    r.tmask = tapmask(r.hs, r.ws, r.mm);
+  }
+  __device__ BRow brstart(int k, int kb) const {
+    BRow r;
+    r.mm = kb + k;
+    blocate(r);
+    return r;
+  }
+  __device__ BCol bcstart(int col) const {
+    const State f = fixed(col);
+    return BCol{(unsigned)((((f.kh - g.P) * g.W + (f.kw - g.P)) * g.C + f.ci) * (int)sizeof(T)),
+                f.ok ? (unsigned)(f.kh * g.KW + f.kw) : 31u};
+  }
+  __device__ unsigned boff(const BRow& r, const BCol& c) const {
+    return ((r.tmask >> c.tap) & 1u) ? (unsigned)r.poff + c.ofs : kOOB;
+  }
+  __device__ void bradvance(BRow& r) const {
+    r.mm += Elem<T>::BK;
+    if (ps.small) {
+      blocate(r);
+      return;
+    }
+    r.ws += ps.dwo * g.S;
+    r.hs += ps.dho * g.S;
+    r.poff += ps.dpoff * (int)sizeof(T);
+    const bool cw = r.ws >= g.Wo * g.S;
+    r.ws = cw ? r.ws - g.Wo * g.S : r.ws;
+    r.hs = cw ? r.hs + g.S : r.hs;
+    r.poff = cw ? r.poff + ps.carry_w * (int)sizeof(T) : r.poff;
+    const bool ch = r.hs >= g.Ho * g.S;
+    r.hs = ch ? r.hs - g.Ho * g.S : r.hs;
+    r.poff = ch ? r.poff + ps.carry_h * (int)sizeof(T) : r.poff;
+    r.tmask = tapmask(r.hs, r.ws, r.mm);
+  }
 };
 static PixStep make_pixstep(const ConvGeom& g, int BK) {
   PixStep p;
@@ -431,6 +581,18 @@ struct StemA {
   __device__ const void* next(DState& d, const Step& s) const {
     return (d.ok & (s.kh + d.khc < 7)) ? (const void*)(d.p + s.delta) : zero_page();
   }
+  // buffer protocol: a chunk is valid while kh = k0/32 + its own kh stays < 7
+  static constexpr bool kBuf = true;
+  struct BState { unsigned base; int khlim; };
+  struct BStep { unsigned delta; int kh; };
+  __device__ rsrc_t rsrc() const { return buf_rsrc(xp, (unsigned)((size_t)g.N * g.Hp * g.Wp * 4 * sizeof(T))); }
+  __device__ BState bstart(int m, int koff, int) const {
+    const State f = fixed(m);
+    const size_t e = (size_t)(f.base - xp) + ((size_t)(koff >> 5) * g.Wp + ((koff & 31) >> 2)) * 4;
+    return BState{(unsigned)(e * sizeof(T)), f.ok ? 7 - (koff >> 5) : -1000};
+  }
+  __device__ BStep bstep(int k0) const { return BStep{(unsigned)((size_t)(k0 >> 5) * g.Wp * 4 * sizeof(T)), k0 >> 5}; }
+  __device__ unsigned boff(BState& s, const BStep& st) const { return st.kh < s.khlim ? s.base + st.delta : kOOB; }
 };
 template <typename T>
 struct StemWgradB {
@@ -477,7 +639,61 @@ struct StemWgradB {
     r.mm += Elem<T>::BK;
     locate(r);
   }
+  // buffer protocol: incremental pixel walk over (n, ho, wo) in the padded image
+  static constexpr bool kBuf = true;
+  PixStep ps;   // deltas in padded-image elements (make_stem_pixstep)
+  struct BRow { int poff, ho, wo, mm; };
+  typedef unsigned BCol;
+  __device__ rsrc_t rsrc() const { return buf_rsrc(xp, (unsigned)((size_t)g.N * g.Hp * g.Wp * 4 * sizeof(T))); }
+  __device__ void blocate(BRow& r) const {
+    const int m = r.mm < g.M ? r.mm : 0;
+    const int n = fdiv(m, g.fd_howo);
+    const int rr = m - n * g.Ho * g.Wo;
+    r.ho = fdiv(rr, g.fd_wo);
+    r.wo = rr - r.ho * g.Wo;
+    r.poff = ((n * g.Hp + 2 * r.ho) * g.Wp + 2 * r.wo) * 4 * (int)sizeof(T);
+  }
+  __device__ BRow brstart(int k, int kb) const {
+    BRow r;
+    r.mm = kb + k;
+    blocate(r);
+    return r;
+  }
+  __device__ BCol bcstart(int col) const {
+    const State f = fixed(col);
+    return f.ok ? (unsigned)(f.off * (int)sizeof(T)) : kOOB;
+  }
+  __device__ unsigned boff(const BRow& r, const BCol& c) const { return r.mm < g.M ? (unsigned)r.poff + c : kOOB; }
+  __device__ void bradvance(BRow& r) const {
+    r.mm += Elem<T>::BK;
+    if (ps.small) {
+      blocate(r);
+      return;
+    }
+    r.wo += ps.dwo;
+    r.ho += ps.dho;
+    r.poff += ps.dpoff * (int)sizeof(T);
+    const bool cw = r.wo >= g.Wo;
+    r.wo = cw ? r.wo - g.Wo : r.wo;
+    r.ho = cw ? r.ho + 1 : r.ho;
+    r.poff = cw ? r.poff + ps.carry_w * (int)sizeof(T) : r.poff;
+    const bool ch = r.ho >= g.Ho;
+    r.ho = ch ? r.ho - g.Ho : r.ho;
+    r.poff = ch ? r.poff + ps.carry_h * (int)sizeof(T) : r.poff;
+  }
 };
+// pixel-walk deltas of the stem's padded NHWC4 image (output pixel (n, ho, wo)
+// starts at padded (n, 2ho, 2wo))
+static PixStep make_stem_pixstep(const StemGeom& g, int BK) {
+  PixStep p;
+  p.small = g.Ho * g.Wo <= BK;
+  p.dho = BK / g.Wo;
+  p.dwo = BK % g.Wo;
+  p.dpoff = (p.dwo * 2 + p.dho * 2 * g.Wp) * 4;
+  p.carry_w = (2 * g.Wp - 2 * g.Wo) * 4;                 // wo -= Wo, ho += 1
+  p.carry_h = (g.Hp * g.Wp - 2 * g.Ho * g.Wp) * 4;       // ho -= Ho, n += 1
+  return p;
+}
 
 // ---------------- epilogues ----------------
 // raw conv output + BN batch statistics (sum, sum of squares)
@@ -561,7 +777,7 @@ template <typename T, class LA, class LB, class EP>
 static int gemm_auto(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
                      hipStream_t st) {
   if (N <= 64) return gemm_narrow<T>(M, N, K, ksplit, la, lb, ep, st);
-  return gemm_wide<T>(M, N, K, ksplit, la, lb, ep, st);
+  return gemm_conv_wide<T>(M, N, K, ksplit, la, lb, ep, st);
 }
 // weight-gradient GEMMs: rows = Co, cols = KH*KW*C, reduction = pixels.
 //  Co = 64 (stem, layer1): 64 x 128 tiles, split-K chosen by the launcher to
@@ -572,6 +788,10 @@ static int gemm_auto(int M, int N, int K, int ksplit, const LA& la, const LB& lb
 template <typename T, class LA, class LB, class EP>
 static int gemm_wgrad(int M, int N, int K, const LA& la, const LB& lb, const EP& ep, hipStream_t st) {
   if (M <= 64) return gemm_short<T>(M, N, K, -2048, la, lb, ep, st);
+  if constexpr (use_bk<T, LA, LB>()) {   // large tiles, one workgroup per CU: slot-balanced split
+    static const int mink5 = getenv("VLP_WGRAD_MINK") ? atoi(getenv("VLP_WGRAD_MINK")) : 2048;
+    if (gemm_variant() >= 5) return gemm_conv_wide<T>(M, N, K, -mink5, la, lb, ep, st);
+  }
   static const int balanced = getenv("VLP_WGRAD_BALANCED") ? atoi(getenv("VLP_WGRAD_BALANCED")) : 0;
   if (balanced) return gemm_wide<T>(M, N, K, -balanced, la, lb, ep, st);
   static const int target = getenv("VLP_WGRAD_TARGET") ? atoi(getenv("VLP_WGRAD_TARGET")) : 1024;
@@ -811,7 +1031,7 @@ VLP_EXPORT int vlp_stem_wgrad(int dtype, const void* dy, const void* xp, float* 
   if ((long long)N * g.Hp * g.Wp * 4 >= (1ll << 31)) return (int)hipErrorInvalidValue;
   EpiAtomic ep{nullptr, nullptr, dw_ws, 256, 1.0f};
   if (dtype == VLP_BF16) {
-    StemWgradB<bf16> lb{g, (const bf16*)xp};
+    StemWgradB<bf16> lb{g, (const bf16*)xp, make_stem_pixstep(g, Elem<bf16>::BK)};
     if (dyT) {   // dy^T [64][pixels]: K-contiguous A operand
       KMat<bf16> la{(const bf16*)dyT, g.M, 64, g.M};
       return gemm_wgrad<bf16>(64, 224, g.M, la, lb, ep, st);
@@ -820,6 +1040,6 @@ VLP_EXPORT int vlp_stem_wgrad(int dtype, const void* dy, const void* xp, float* 
     return gemm_wgrad<bf16>(64, 224, g.M, la, lb, ep, st);
   }
   MNMat<float> la{(const float*)dy, 64, 64, g.M};
-  StemWgradB<float> lb{g, (const float*)xp};
+  StemWgradB<float> lb{g, (const float*)xp, make_stem_pixstep(g, Elem<float>::BK)};
   return gemm_wgrad<float>(64, 224, g.M, la, lb, ep, st);
 }

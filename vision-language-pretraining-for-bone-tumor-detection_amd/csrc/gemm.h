@@ -39,6 +39,7 @@ struct GemmShape {
   int tiles_m, tiles_n;
   int xsplit;   // 1: split-K grid is 1-D and every split's tiles share one XCD
   int dbg;      // diagnostics (VLP_GEMM_DBG, ms kernel): 1 skip epilogue, 2/4 freeze A/B MN rows
+  int nsplit;   // K-splits (bk / big kernels: 1-D grid of nsplit * tiles)
 };
 
 // ---------------- LDS image addressing (bytes) ----------------
@@ -246,6 +247,39 @@ __device__ __forceinline__ v8bf frag_bf16(const char* lds, int rb, int s) {
     }
     return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   }
+}
+
+// MN-contig (blocked image) fragment through inline-asm transposing reads.
+// hipcc treats ds_read_b64_tr_b16 as possibly aliasing an in-flight LDS-DMA
+// and drains vmcnt(0) in front of it, which would empty a multi-tile
+// prefetch ring every K-step; asm reads are invisible to that analysis, so
+// the caller owns the wait: asm_lds_wait() before the first consumer.
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(unsigned long long)(const __attribute__((address_space(3))) char*)p;
+}
+template <int RB>
+__device__ __forceinline__ v8bf frag_tr_asm(const char* lds, int rb, int s) {
+  const int l = threadIdx.x & 63;
+  const int i = l & 15, g = l >> 4;
+  const int q = i >> 2, p = i & 3;
+  const int k1 = 32 * s + 8 * g + q;
+  const int mn = rb + 4 * p;
+  v4bf lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(lds_addr(lds + mn8_off<RB / 128>(k1, mn))));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(lds_addr(lds + mn8_off<RB / 128>(k1 + 4, mn))));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ void asm_lds_wait() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <bool KC, int RB>
+__device__ __forceinline__ v8bf frag_big(const char* lds, int rb, int s) {
+#ifdef VLP_DBG_NOTR   // timing-only experiment: MN images read as if K-contig (wrong values)
+  return frag_bf16<true, RB, true>(lds, rb, s);
+#endif
+  if constexpr (KC) return frag_bf16<true, RB, true>(lds, rb, s);
+  else return frag_tr_asm<RB>(lds, rb, s);
 }
 
 // fp32 fragment for 4 x MFMA 16x16x4f32 over a 16-k sub-step s (0/1) of BK=32.
@@ -506,6 +540,85 @@ __device__ __forceinline__ void wait_vmcnt() {
 }
 __device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
+// Epilogue shared by the multi-stage kernels: lane l = 16g + i owns
+// C[row = rbase + i][col = cbase + 4g .. 4g+3] of each 16x16 block.
+template <int BM, int BN, int WGM, int WGN, class EP, int MB, int NB>
+__device__ __forceinline__ void ms_epilogue(const GemmShape& sh, const EP& ep, v4f (&acc)[MB][NB], int row0,
+                                            int col0, int wid, int wm, int wn, char* smem) {
+  constexpr int NT = WGM * WGN * 64;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  const int l = threadIdx.x & 63;
+  const int li = l & 15, lg = l >> 4;
+  float* red = reinterpret_cast<float*>(smem);
+  // staged epilogues: outputs go through a bf16 LDS tile (16-B chunks XOR-
+  // swizzled by row) and leave as full 16-B row segments, 4..8 rows per wave
+  // store instead of 32-B pieces of 16 rows
+  constexpr bool kStage = StageTrait<EP>::value;
+  constexpr int CPR = BN / 8;
+  bf16* stg = reinterpret_cast<bf16*>(smem + 4096);
+  
+  static_assert(WGM * BN * 2 * 4 <= 4096, "stats scratch");
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int coll = wn * WTN + b * 16 + 4 * lg;
+    const int col = col0 + coll;
+    v4f s1 = v4f{0.f, 0.f, 0.f, 0.f}, s2 = s1;
+#pragma unroll
+    for (int a = 0; a < MB; ++a) {
+      const int rowl = wm * WTM + a * 16 + li;
+      const int row = row0 + rowl;
+      if (row < sh.M && col < sh.N) {
+        v4f c1 = v4f{0.f, 0.f, 0.f, 0.f}, c2 = c1;
+        if constexpr (kStage) {
+          const v4f o = ep.value(row, col, acc[a][b], c1, c2);
+          v4bf ob;
+          ob[0] = (bf16)o[0]; ob[1] = (bf16)o[1]; ob[2] = (bf16)o[2]; ob[3] = (bf16)o[3];
+          *reinterpret_cast<v4bf*>(stg + rowl * BN + (((coll >> 3) ^ (rowl & (CPR - 1))) << 3) +
+                                   (coll & 4)) = ob;
+        } else {
+          ep(row, col, acc[a][b], c1, c2);
+        }
+        if constexpr (EP::kStats) { s1 += c1; s2 += c2; }
+      }
+    }
+    if constexpr (EP::kStats) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float x = row16_sum(s1[j]), y = row16_sum(s2[j]);
+        if (li == 15) {
+          const int cl = wn * WTN + b * 16 + 4 * lg + j;
+          red[(wm * BN + cl) * 2 + 0] = x;
+          red[(wm * BN + cl) * 2 + 1] = y;
+        }
+      }
+    }
+  }
+  if constexpr (kStage) {
+    __syncthreads();
+#pragma unroll 4
+    for (int q = threadIdx.x; q < BM * CPR; q += NT) {
+      const int r = q / CPR, c = q - r * CPR;
+      const int row = row0 + r, col = col0 + c * 8;
+      if (row < sh.M && col < sh.N)
+        ep.store8(row, col, *reinterpret_cast<const uint4*>(stg + r * BN + ((c ^ (r & (CPR - 1))) << 3)));
+    }
+  }
+  if constexpr (EP::kStats) {
+    __syncthreads();
+    const int rep = ep.stat_rep > 1 ? (wid % ep.stat_rep) : 0;
+    for (int cl = threadIdx.x; cl < BN; cl += NT) {
+      const int col = col0 + cl;
+      if (col < sh.N) {
+        float x = 0.f, y = 0.f;
+#pragma unroll
+        for (int w = 0; w < WGM; ++w) { x += red[(w * BN + cl) * 2]; y += red[(w * BN + cl) * 2 + 1]; }
+        atomicAdd(ep.stat1 + (size_t)rep * sh.N + col, (double)x);
+        atomicAdd(ep.stat2 + (size_t)rep * sh.N + col, (double)y);
+      }
+    }
+  }
+}
+
 template <int BM, int BN, int WGM, int WGN, int S, class LA, class LB, class EP>
 __global__ void __launch_bounds__(WGM * WGN * 64)
 gemm_ms_kernel(GemmShape sh, LA la, LB lb, EP ep) {
@@ -621,76 +734,317 @@ gemm_ms_kernel(GemmShape sh, LA la, LB lb, EP ep) {
     return;
   }
 
-  const int l = threadIdx.x & 63;
-  const int li = l & 15, lg = l >> 4;
-  float* red = reinterpret_cast<float*>(smem);
-  // staged epilogues: outputs go through a bf16 LDS tile (16-B chunks XOR-
-  // swizzled by row) and leave as full 16-B row segments, 4..8 rows per wave
-  // store instead of 32-B pieces of 16 rows
-  constexpr bool kStage = StageTrait<EP>::value;
-  constexpr int CPR = BN / 8;
-  bf16* stg = reinterpret_cast<bf16*>(smem + 4096);
-  static_assert(!kStage || 4096 + BM * BN * 2 <= S * STAGE, "staging tile fits the ring");
-  static_assert(WGM * BN * 2 * 4 <= 4096, "stats scratch");
+  static_assert(!StageTrait<EP>::value || 4096 + BM * BN * 2 <= S * STAGE, "staging tile fits the ring");
+  ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep, acc, row0, col0, wid, wm, wn, smem);
+}
+
+// ---------------- buffer-DMA two-slot kernel (bf16) ----------------
+// The same engine as gemm_ms_kernel with S = 2, restated for a lower VALU
+// cost per K-step (profiling: 4-8 VALU per MFMA in the direct kernels, more
+// than the two-waves-per-SIMD issue budget of ~2):
+//  * operands are fetched with buffer_load ... lds through a buffer resource
+//    (base + 32-bit byte offset): an out-of-range chunk is an offset past
+//    num_records (kOOB), which the hardware returns as zeros, so no zero-page
+//    pointer select and no 64-bit address arithmetic;
+//  * the K loop is unrolled by the two ring slots, so every LDS address
+//    (fragment reads, DMA destinations) is a compile-time offset from a
+//    wave-uniform base held in SGPRs;
+//  * a K-step past the end issues through a null resource (num_records = 0)
+//    instead of branching, so the loop body stays one basic block.
+// Loader protocol (kBuf = true):
+//   rsrc_t rsrc() const                                     whole-operand resource
+//   K-contig: BState bstart(int row, int koff, int kb); BStep bstep(int k0);
+//             unsigned boff(BState&, const BStep&)          byte offset | kOOB
+//   MN-contig: BRow brstart(int k, int kb); BCol bcstart(int mn);
+//             unsigned boff(const BRow&, const BCol&); void bradvance(BRow&)
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr unsigned kOOB = 0x80000000u;   // every operand is < 2 GiB (checked on the host)
+
+__device__ __forceinline__ rsrc_t buf_rsrc(const void* p, unsigned bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  void* q = (void*)(((unsigned long long)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+__device__ __forceinline__ rsrc_t null_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0, 0x00020000);
+}
+__device__ __forceinline__ void dma16(rsrc_t r, unsigned voff, char* lds) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, (int)voff, 0, 0, 0);
+}
+
+template <class L, class = void> struct BufTrait { static constexpr bool value = false; };
+template <class L> struct BufTrait<L, std::void_t<decltype(L::kBuf)>> { static constexpr bool value = L::kBuf; };
+
+template <int BM, class L, int NT, bool KC = L::kKContig>
+struct BStager;
+// K-contig operand: [BM rows][128 B] image, chunk p of row r at p ^ ((r>>1)&7).
+template <int BM, class L, int NT>
+struct BStager<BM, L, NT, true> {
+  static constexpr int NI = BM * 8 / NT;
+  static_assert(NI >= 1 && (BM * 8) % NT == 0, "tile / thread geometry");
+  typename L::BState st[NI];
+  __device__ __forceinline__ void init(const L& ld, int row0, int kb, int wv) {
+    const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    const int coll = wn * WTN + b * 16 + 4 * lg;
-    const int col = col0 + coll;
-    v4f s1 = v4f{0.f, 0.f, 0.f, 0.f}, s2 = s1;
-#pragma unroll
-    for (int a = 0; a < MB; ++a) {
-      const int rowl = wm * WTM + a * 16 + li;
-      const int row = row0 + rowl;
-      if (row < sh.M && col < sh.N) {
-        v4f c1 = v4f{0.f, 0.f, 0.f, 0.f}, c2 = c1;
-        if constexpr (kStage) {
-          const v4f o = ep.value(row, col, acc[a][b], c1, c2);
-          v4bf ob;
-          ob[0] = (bf16)o[0]; ob[1] = (bf16)o[1]; ob[2] = (bf16)o[2]; ob[3] = (bf16)o[3];
-          *reinterpret_cast<v4bf*>(stg + rowl * BN + (((coll >> 3) ^ (rowl & (CPR - 1))) << 3) +
-                                   (coll & 4)) = ob;
-        } else {
-          ep(row, col, acc[a][b], c1, c2);
-        }
-        if constexpr (EP::kStats) { s1 += c1; s2 += c2; }
-      }
+    for (int i = 0; i < NI; ++i) {
+      const int q = (wv * NI + i) * 64 + lane;
+      const int r = q >> 3, p = q & 7;
+      st[i] = ld.bstart(row0 + r, (p ^ ((r >> 1) & 7)) * 8, kb);
     }
-    if constexpr (EP::kStats) {
+  }
+  __device__ __forceinline__ void issue(const L& ld, rsrc_t rs, int k0, char* lds, int wv) {
+    const auto stp = ld.bstep(k0);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float x = row16_sum(s1[j]), y = row16_sum(s2[j]);
-        if (li == 15) {
-          const int cl = wn * WTN + b * 16 + 4 * lg + j;
-          red[(wm * BN + cl) * 2 + 0] = x;
-          red[(wm * BN + cl) * 2 + 1] = y;
-        }
+    for (int i = 0; i < NI; ++i) dma16(rs, ld.boff(st[i], stp), lds + (wv * NI + i) * 1024);
+  }
+};
+// MN-contig operand, blocked image (mn8_off), as GStagerN.
+template <int BM, class L, int NT>
+struct BStager<BM, L, NT, false> {
+  static constexpr int NW = NT / 64;
+  static constexpr int CPB = BM / 64;
+  static constexpr int NI = 8 * CPB / NW;
+  static constexpr int NR = NI >= CPB ? NI / CPB : 1;
+  static_assert(NI >= 1 && (8 * CPB) % NW == 0 && (NI % CPB == 0 || CPB % NI == 0), "tile / thread geometry");
+  typename L::BRow rs[NR];
+  typename L::BCol cs[NI];
+  __device__ __forceinline__ void init(const L& ld, int row0, int kb, int wv) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int b = wv * NI + i;
+      const int k = 8 * (b / CPB) + (lane >> 3);
+      const int c = 8 * (b % CPB) + ((lane & 7) ^ mn8_h(k));
+      cs[i] = ld.bcstart(row0 + c * 8);
+      if (i % CPB == 0 || NI < CPB) {
+        if (i / CPB < NR) rs[i / CPB] = ld.brstart(k, kb);
       }
     }
   }
-  if constexpr (kStage) {
-    __syncthreads();
-#pragma unroll 4
-    for (int q = threadIdx.x; q < BM * CPR; q += NT) {
-      const int r = q / CPR, c = q - r * CPR;
-      const int row = row0 + r, col = col0 + c * 8;
-      if (row < sh.M && col < sh.N)
-        ep.store8(row, col, *reinterpret_cast<const uint4*>(stg + r * BN + ((c ^ (r & (CPR - 1))) << 3)));
-    }
-  }
-  if constexpr (EP::kStats) {
-    __syncthreads();
-    const int rep = ep.stat_rep > 1 ? (wid % ep.stat_rep) : 0;
-    for (int cl = threadIdx.x; cl < BN; cl += NT) {
-      const int col = col0 + cl;
-      if (col < sh.N) {
-        float x = 0.f, y = 0.f;
+  __device__ __forceinline__ void issue(const L& ld, rsrc_t r, int, char* lds, int wv) {
 #pragma unroll
-        for (int w = 0; w < WGM; ++w) { x += red[(w * BN + cl) * 2]; y += red[(w * BN + cl) * 2 + 1]; }
-        atomicAdd(ep.stat1 + (size_t)rep * sh.N + col, (double)x);
-        atomicAdd(ep.stat2 + (size_t)rep * sh.N + col, (double)y);
-      }
-    }
+    for (int i = 0; i < NI; ++i) dma16(r, ld.boff(rs[NI >= CPB ? i / CPB : 0], cs[i]), lds + (wv * NI + i) * 1024);
+#pragma unroll
+    for (int j = 0; j < NR; ++j) ld.bradvance(rs[j]);
   }
+};
+
+template <int BM, int BN, int WGM, int WGN, class LA, class LB, class EP>
+__global__ void __launch_bounds__(WGM * WGN * 64)
+gemm_bk_kernel(GemmShape sh, LA la, LB lb, EP ep) {
+  constexpr int NT = WGM * WGN * 64;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int MB = WTM / 16, NB = WTN / 16;
+  constexpr int BK = 64;
+  constexpr int ABYTES = BM * 128;
+  constexpr int STAGE = (BM + BN) * 128;
+  using SA = BStager<BM, LA, NT>;
+  using SB = BStager<BN, LB, NT>;
+  static_assert(!StageTrait<EP>::value || 4096 + BM * BN * 2 <= 2 * STAGE, "staging tile fits the ring");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  // 1-D grid over (split, tile), split-major, bijectively remapped so each
+  // XCD owns a contiguous run: the tiles of one K-split (which share its
+  // operand slab) sit on one or two XCDs and hit one L2
+  const int nwg = sh.tiles_m * sh.tiles_n;
+  const int ntot = nwg * sh.nsplit;
+  const int bid = blockIdx.x;
+  int g = bid;
+  if (ntot >= 16) {
+    const int xcd = bid & 7, idx = bid >> 3, q = ntot >> 3, rr = ntot & 7;
+    g = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
+  }
+  const int split = g / nwg;
+  const int wid = g - split * nwg;
+  const int tm = wid / sh.tiles_n, tn = wid - tm * sh.tiles_n;
+  const int row0 = tm * BM, col0 = tn * BN;
+  const int kb = split * sh.kchunk;
+  int ke = kb + sh.kchunk;
+  if (ke > sh.K) ke = sh.K;
+  const int nk = (ke - kb + BK - 1) / BK;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wm = wv / WGN, wn = wv - wm * WGN;
+
+  SA sa;
+  SB sb;
+  sa.init(la, row0, kb, wv);
+  sb.init(lb, col0, kb, wv);
+  const rsrc_t ra = la.rsrc(), rb = lb.rsrc();
+  const rsrc_t rz = null_rsrc(zero_page());
+  v4f acc[MB][NB];
+#pragma unroll
+  for (int a = 0; a < MB; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[a][b] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  // odd nk: tile 0 goes to slot 1 so the main loop always runs slot pairs
+  const int s0 = (nk & 1) * STAGE;
+  sa.issue(la, nk > 0 ? ra : rz, kb, smem + s0, wv);
+  sb.issue(lb, nk > 0 ? rb : rz, kb, smem + s0 + ABYTES, wv);
+
+  // one K-step: tile t sits in ring slot SL; tile t+1 is fetched into 1-SL
+  auto body = [&](auto slc, int t) {
+    constexpr int SL = decltype(slc)::value;
+    wait_vmcnt<0>();
+    raw_barrier();
+    const char* ia = smem + SL * STAGE;
+    const char* ib = ia + ABYTES;
+    v8bf fa[2][MB], fb[2][NB];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int a = 0; a < MB; ++a) fa[s][a] = frag_bf16<LA::kKContig, BM * 2, true>(ia, wm * WTM + a * 16, s);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) fb[s][b] = frag_bf16<LB::kKContig, BN * 2, true>(ib, wn * WTN + b * 16, s);
+    }
+    const bool live = t + 1 < nk;
+    char* f = smem + (1 - SL) * STAGE;
+    sa.issue(la, live ? ra : rz, kb + (t + 1) * BK, f, wv);
+    sb.issue(lb, live ? rb : rz, kb + (t + 1) * BK, f + ABYTES, wv);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[s][b], fa[s][a], acc[a][b], 0, 0, 0);
+  };
+  int t = 0;
+  if (nk & 1) {
+    body(std::integral_constant<int, 1>{}, 0);
+    t = 1;
+  }
+  for (; t < nk; t += 2) {
+    body(std::integral_constant<int, 0>{}, t);
+    body(std::integral_constant<int, 1>{}, t + 1);
+  }
+  __syncthreads();   // ring drained (incl. the null-resource tail fetch) before LDS is reused
+  ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep, acc, row0, col0, wid, wm, wn, smem);
+}
+
+// ---------------- 8-wave large-tile kernel (bf16) ----------------
+// The 128x128 / two-barrier / one-tile-in-flight structure tops out near
+// 900 TF/s (its per-K-step vmcnt(0) drains the prefetch; measured: halving
+// the VALU per MFMA did not move it).  This kernel runs one 512-thread
+// workgroup per CU on a 256-row tile, with TWO K-tiles in flight:
+//   iteration t (tile t in ring slot t&1):
+//     vmcnt(NI) + barrier          tile t landed (tile t+1 still in flight)
+//     read all fragments of tile t (k-substeps 0 and 1) into registers
+//     MFMAs of k-substep 0         (overlap the substep-1 reads)
+//     lgkmcnt(0) + barrier         every wave is done with slot t&1
+//     fetch tile t+2 into slot t&1 (null resource past the end)
+//     MFMAs of k-substep 1
+// so each fetch has ~two iterations of MFMA work to land in, and the
+// operand traffic per FLOP halves against 128x128 (256x256: 128 FLOP/B).
+template <int BM, int BN, int WGM, int WGN, class LA, class LB, class EP>
+__global__ void __launch_bounds__(WGM * WGN * 64)
+gemm_big_kernel(GemmShape sh, LA la, LB lb, EP ep) {
+  constexpr int NT = WGM * WGN * 64;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int MB = WTM / 16, NB = WTN / 16;
+  constexpr int BK = 64;
+  constexpr int ABYTES = BM * 128;
+  constexpr int STAGE = (BM + BN) * 128;
+  using SA = BStager<BM, LA, NT>;
+  using SB = BStager<BN, LB, NT>;
+  constexpr int NI = SA::NI + SB::NI;   // LDS-DMA ops per thread per K-tile
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  // 1-D grid over (split, tile), split-major, bijectively remapped so each
+  // XCD owns a contiguous run: the tiles of one K-split (which share its
+  // operand slab) sit on one or two XCDs and hit one L2
+  const int nwg = sh.tiles_m * sh.tiles_n;
+  const int ntot = nwg * sh.nsplit;
+  const int bid = blockIdx.x;
+  int g = bid;
+  if (ntot >= 16) {
+    const int xcd = bid & 7, idx = bid >> 3, q = ntot >> 3, rr = ntot & 7;
+    g = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
+  }
+  const int split = g / nwg;
+  const int wid = g - split * nwg;
+  const int tm = wid / sh.tiles_n, tn = wid - tm * sh.tiles_n;
+  const int row0 = tm * BM, col0 = tn * BN;
+  const int kb = split * sh.kchunk;
+  int ke = kb + sh.kchunk;
+  if (ke > sh.K) ke = sh.K;
+  const int nk = (ke - kb + BK - 1) / BK;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wm = wv / WGN, wn = wv - wm * WGN;
+
+  SA sa;
+  SB sb;
+  sa.init(la, row0, kb, wv);
+  sb.init(lb, col0, kb, wv);
+  const rsrc_t ra = la.rsrc(), rb = lb.rsrc();
+  const rsrc_t rz = null_rsrc(zero_page());
+  v4f acc[MB][NB];
+#pragma unroll
+  for (int a = 0; a < MB; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[a][b] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  // odd nk: tile 0 goes to slot 1 so the main loop always runs slot pairs
+  const int s0 = (nk & 1) * STAGE;
+  sa.issue(la, nk > 0 ? ra : rz, kb, smem + s0, wv);
+  sb.issue(lb, nk > 0 ? rb : rz, kb, smem + s0 + ABYTES, wv);
+  sa.issue(la, nk > 1 ? ra : rz, kb + BK, smem + (STAGE - s0), wv);
+  sb.issue(lb, nk > 1 ? rb : rz, kb + BK, smem + (STAGE - s0) + ABYTES, wv);
+
+  auto body = [&](auto slc, int t) {
+    constexpr int SL = decltype(slc)::value;
+    wait_vmcnt<NI>();
+    raw_barrier();
+    const char* ia = smem + SL * STAGE;
+    const char* ib = ia + ABYTES;
+    v8bf fa[2][MB], fb[2][NB];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+      for (int a = 0; a < MB; ++a) fa[s][a] = frag_big<LA::kKContig, BM * 2>(ia, wm * WTM + a * 16, s);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) fb[s][b] = frag_big<LB::kKContig, BN * 2>(ib, wn * WTN + b * 16, s);
+    }
+    if constexpr (!LA::kKContig || !LB::kKContig) asm_lds_wait();
+#pragma unroll
+    for (int a = 0; a < MB; ++a)
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[0][b], fa[0][a], acc[a][b], 0, 0, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+    const bool live = t + 2 < nk;
+    char* f = smem + SL * STAGE;
+    sa.issue(la, live ? ra : rz, kb + (t + 2) * BK, f, wv);
+    sb.issue(lb, live ? rb : rz, kb + (t + 2) * BK, f + ABYTES, wv);
+#pragma unroll
+    for (int a = 0; a < MB; ++a)
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[1][b], fa[1][a], acc[a][b], 0, 0, 0);
+  };
+  int t = 0;
+  if (nk & 1) {
+    body(std::integral_constant<int, 1>{}, 0);
+    t = 1;
+  }
+  for (; t < nk; t += 2) {
+    body(std::integral_constant<int, 0>{}, t);
+    body(std::integral_constant<int, 1>{}, t + 1);
+  }
+  __syncthreads();   // ring drained (incl. the null-resource tail fetches) before LDS is reused
+  ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep, acc, row0, col0, wid, wm, wn, smem);
+}
+
+template <int BM, int BN, class EP>
+constexpr int big_lds_bytes() {
+  constexpr int ring = 2 * (BM + BN) * 128;
+  constexpr int stg = StageTrait<EP>::value ? 4096 + BM * BN * 2 : 4096;
+  return ring > stg ? ring : stg;
 }
 
 // Split-K count for a reduction of K over `tiles` output tiles, given the
@@ -705,7 +1059,13 @@ inline int balanced_ksplit(int tiles, int K, int slots, int min_k) {
   for (int r = 1; r <= 4; ++r) {
     int ks = r * slots / tiles;
     if (ks < 1) continue;
-    if (ks > 1 && K / ks < min_k) break;
+    if (ks > 1 && K / ks < min_k) {   // too shallow: the deepest split that keeps min_k
+      ks = K / min_k > 1 ? K / min_k : 1;
+      const long long wg = (long long)ks * tiles;
+      const double eff = (double)wg / (double)(((wg + slots - 1) / slots) * slots);
+      if (ks > best && (eff > best_eff + 0.01 || best == 1)) best = ks;
+      break;
+    }
     const long long wg = (long long)ks * tiles;
     const double eff = (double)wg / (double)(((wg + slots - 1) / slots) * slots);
     if (eff > best_eff + 0.01) { best_eff = eff; best = ks; }
@@ -729,6 +1089,7 @@ inline int launch_gemm_ms(int M, int N, int K, int ksplit, const LA& la, const L
   if (M <= 0 || N <= 0) return 0;
   GemmShape sh;
   sh.xsplit = 0;
+  sh.nsplit = 1;
   sh.dbg = 0;
   sh.M = M; sh.N = N; sh.K = K;
   sh.tiles_m = (M + BM - 1) / BM;
@@ -774,6 +1135,114 @@ inline int launch_gemm_ms(int M, int N, int K, int ksplit, const LA& la, const L
   return (int)hipGetLastError();
 }
 
+template <int BM, int BN, int WGM, int WGN, class LA, class LB, class EP>
+inline int launch_gemm_bk(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
+                          hipStream_t stream) {
+  constexpr int BK = 64;
+  constexpr int S = 2;
+  if (M <= 0 || N <= 0) return 0;
+  GemmShape sh;
+  sh.xsplit = 0;
+  sh.nsplit = 1;
+  sh.dbg = 0;
+  sh.M = M; sh.N = N; sh.K = K;
+  sh.tiles_m = (M + BM - 1) / BM;
+  sh.tiles_n = (N + BN - 1) / BN;
+  if (ksplit <= 0) {   // auto: fill whole rounds of resident workgroups
+    static int occ = 0;
+    if (!occ) {
+      constexpr int lds_b = S * (BM + BN) * 128;
+      if (lds_b > 65536)
+        (void)hipFuncSetAttribute((const void*)&gemm_bk_kernel<BM, BN, WGM, WGN, LA, LB, EP>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_b);
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+              &occ, (const void*)&gemm_bk_kernel<BM, BN, WGM, WGN, LA, LB, EP>, WGM * WGN * 64,
+              lds_b) != hipSuccess || occ <= 0)
+        occ = 1;
+    }
+    ksplit = balanced_ksplit(sh.tiles_m * sh.tiles_n, K, occ * device_cus(), -ksplit > 0 ? -ksplit : 2048);
+  }
+  if (ksplit < 1) ksplit = 1;
+  int kc = (K + ksplit - 1) / ksplit;
+  kc = ((kc + BK - 1) / BK) * BK;
+  if (kc < BK) kc = BK;
+  ksplit = (K + kc - 1) / kc;
+  if (ksplit < 1) ksplit = 1;
+  sh.kchunk = kc;
+  sh.xsplit = 0;
+  sh.nsplit = ksplit;
+  static const int dbg = getenv("VLP_GEMM_DBG") ? atoi(getenv("VLP_GEMM_DBG")) : 0;
+  sh.dbg = dbg;
+  dim3 grid(sh.tiles_m * sh.tiles_n * ksplit, 1, 1);
+  constexpr int lds = S * (BM + BN) * 128;
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  if constexpr (lds > 65536) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)&gemm_bk_kernel<BM, BN, WGM, WGN, LA, LB, EP>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      attr_set = true;
+    }
+  }
+  hipLaunchKernelGGL((gemm_bk_kernel<BM, BN, WGM, WGN, LA, LB, EP>), grid, dim3(WGM * WGN * 64), lds,
+                     stream, sh, la, lb, ep);
+  return (int)hipGetLastError();
+}
+
+template <int BM, int BN, int WGM, int WGN, class LA, class LB, class EP>
+inline int launch_gemm_big(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
+                          hipStream_t stream) {
+  constexpr int BK = 64;
+  constexpr int S = 2;
+  if (M <= 0 || N <= 0) return 0;
+  GemmShape sh;
+  sh.xsplit = 0;
+  sh.nsplit = 1;
+  sh.dbg = 0;
+  sh.M = M; sh.N = N; sh.K = K;
+  sh.tiles_m = (M + BM - 1) / BM;
+  sh.tiles_n = (N + BN - 1) / BN;
+  if (ksplit <= 0) {   // auto: fill whole rounds of resident workgroups
+    static int occ = 0;
+    if (!occ) {
+      constexpr int lds_b = big_lds_bytes<BM, BN, EP>();
+      if (lds_b > 65536)
+        (void)hipFuncSetAttribute((const void*)&gemm_big_kernel<BM, BN, WGM, WGN, LA, LB, EP>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_b);
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+              &occ, (const void*)&gemm_big_kernel<BM, BN, WGM, WGN, LA, LB, EP>, WGM * WGN * 64,
+              lds_b) != hipSuccess || occ <= 0)
+        occ = 1;
+    }
+    ksplit = balanced_ksplit(sh.tiles_m * sh.tiles_n, K, occ * device_cus(), -ksplit > 0 ? -ksplit : 2048);
+  }
+  if (ksplit < 1) ksplit = 1;
+  int kc = (K + ksplit - 1) / ksplit;
+  kc = ((kc + BK - 1) / BK) * BK;
+  if (kc < BK) kc = BK;
+  ksplit = (K + kc - 1) / kc;
+  if (ksplit < 1) ksplit = 1;
+  sh.kchunk = kc;
+  sh.xsplit = 0;
+  sh.nsplit = ksplit;
+  static const int dbg = getenv("VLP_GEMM_DBG") ? atoi(getenv("VLP_GEMM_DBG")) : 0;
+  sh.dbg = dbg;
+  dim3 grid(sh.tiles_m * sh.tiles_n * ksplit, 1, 1);
+  constexpr int lds = big_lds_bytes<BM, BN, EP>();
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  if constexpr (lds > 65536) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)&gemm_big_kernel<BM, BN, WGM, WGN, LA, LB, EP>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      attr_set = true;
+    }
+  }
+  hipLaunchKernelGGL((gemm_big_kernel<BM, BN, WGM, WGN, LA, LB, EP>), grid, dim3(WGM * WGN * 64), lds,
+                     stream, sh, la, lb, ep);
+  return (int)hipGetLastError();
+}
+
 template <typename T, int BM, int BN>
 constexpr int gemm_lds_bytes() { return 2 * (BM + BN) * 128; }
 
@@ -782,7 +1251,7 @@ constexpr int gemm_lds_bytes() { return 2 * (BM + BN) * 128; }
 // register-staged 2-stage kernel.  VLP_GEMM_VARIANT selects among tile /
 // stage configurations (for on-device A/B runs; the default is the measured best).
 #ifndef VLP_GEMM_DEFAULT_VARIANT
-#define VLP_GEMM_DEFAULT_VARIANT 3
+#define VLP_GEMM_DEFAULT_VARIANT 5
 #endif
 inline int gemm_variant() {
   static int v = -1;
@@ -796,10 +1265,29 @@ template <typename T, class LA, class LB>
 constexpr bool use_ms() {
   return std::is_same<T, bf16>::value && DirectTrait<LA>::value && DirectTrait<LB>::value;
 }
+template <typename T, class LA, class LB>
+constexpr bool use_bk() {
+  return std::is_same<T, bf16>::value && BufTrait<LA>::value && BufTrait<LB>::value;
+}
+// large-tile shape choice (8 waves, one workgroup per CU): 256x256 when both
+// dimensions allow it, else 128x256 / 256x128 (64x64 wave tiles)
+template <class LA, class LB, class EP>
+inline int gemm_big_auto(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep, hipStream_t st) {
+  // (256x256 keeps 128x64 fragments per wave live: only the all-K-contig case
+  // fits the 256-VGPR budget without spilling)
+  if constexpr (LA::kKContig && LB::kKContig) {
+    if (M >= 256 && N >= 256) return launch_gemm_big<256, 256, 2, 4>(M, N, K, ksplit, la, lb, ep, st);
+  }
+  if (N >= 256) return launch_gemm_big<128, 256, 2, 4>(M, N, K, ksplit, la, lb, ep, st);
+  return launch_gemm_big<256, 128, 4, 2>(M, N, K, ksplit, la, lb, ep, st);
+}
 // N >= 128 columns
 template <typename T, class LA, class LB, class EP>
 inline int gemm_wide(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
                      hipStream_t st) {
+  if constexpr (use_bk<T, LA, LB>()) {
+    if (gemm_variant() >= 4) return launch_gemm_bk<128, 128, 2, 2>(M, N, K, ksplit, la, lb, ep, st);
+  }
   if constexpr (use_ms<T, LA, LB>()) {
     switch (gemm_variant()) {
       case 0: return launch_gemm<T, 128, 128, 2>(M, N, K, ksplit, la, lb, ep, st);
@@ -810,10 +1298,23 @@ inline int gemm_wide(int M, int N, int K, int ksplit, const LA& la, const LB& lb
     return launch_gemm<T, 128, 128, 2>(M, N, K, ksplit, la, lb, ep, st);
   }
 }
+// convolution GEMMs with N >= 128 (and M >= 128): the 8-wave large-tile
+// kernel where both loaders speak the buffer protocol (VLP_GEMM_VARIANT >= 5)
+template <typename T, class LA, class LB, class EP>
+inline int gemm_conv_wide(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
+                          hipStream_t st) {
+  if constexpr (use_bk<T, LA, LB>()) {
+    if (gemm_variant() >= 5) return gemm_big_auto(M, N, K, ksplit, la, lb, ep, st);
+  }
+  return gemm_wide<T>(M, N, K, ksplit, la, lb, ep, st);
+}
 // N <= 64 columns (Co = 64 convs)
 template <typename T, class LA, class LB, class EP>
 inline int gemm_narrow(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
                        hipStream_t st) {
+  if constexpr (use_bk<T, LA, LB>()) {
+    if (gemm_variant() >= 4) return launch_gemm_bk<256, 64, 4, 1>(M, N, K, ksplit, la, lb, ep, st);
+  }
   if constexpr (use_ms<T, LA, LB>()) {
     switch (gemm_variant()) {
       case 0: return launch_gemm<T, 256, 64, 4>(M, N, K, ksplit, la, lb, ep, st);
@@ -828,6 +1329,9 @@ inline int gemm_narrow(int M, int N, int K, int ksplit, const LA& la, const LB& 
 template <typename T, class LA, class LB, class EP>
 inline int gemm_short(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
                       hipStream_t st) {
+  if constexpr (use_bk<T, LA, LB>()) {
+    if (gemm_variant() >= 4) return launch_gemm_bk<64, 128, 1, 4>(M, N, K, ksplit, la, lb, ep, st);
+  }
   if constexpr (use_ms<T, LA, LB>()) {
     switch (gemm_variant()) {
       case 0: return launch_gemm<T, 64, 128, 1>(M, N, K, ksplit, la, lb, ep, st);
@@ -847,6 +1351,7 @@ inline int launch_gemm(int M, int N, int K, int ksplit, const LA& la, const LB& 
   if (M <= 0 || N <= 0) return 0;
   GemmShape sh;
   sh.xsplit = 0;
+  sh.nsplit = 1;
   sh.dbg = 0;
   sh.M = M; sh.N = N; sh.K = K;
   sh.tiles_m = (M + BM - 1) / BM;
@@ -902,6 +1407,16 @@ struct KMat {
     s.kk += Elem<T>::BK;
     return r;
   }
+  // buffer protocol (gemm_bk_kernel): o = chunk byte offset at k = 0
+  static constexpr bool kBuf = true;
+  struct BState { unsigned o; int koff; };
+  struct BStep { unsigned kbytes; int klim; };
+  __device__ rsrc_t rsrc() const { return buf_rsrc(p, (unsigned)(((size_t)(M - 1) * ld + K) * sizeof(T))); }
+  __device__ BState bstart(int m, int koff, int) const {
+    return BState{m < M ? (unsigned)(((size_t)m * ld + koff) * sizeof(T)) : kOOB, koff};
+  }
+  __device__ BStep bstep(int k0) const { return BStep{(unsigned)(k0 * sizeof(T)), K - k0}; }
+  __device__ unsigned boff(BState& s, const BStep& st) const { return s.koff < st.klim ? s.o + st.kbytes : kOOB; }
 };
 // MN contiguous: A(m,k) = p[k*ld + m].  Requires M % EPC == 0.
 template <typename T>
@@ -923,6 +1438,18 @@ struct MNMat {
   }
   __device__ void radvance(RState& r) const {
     r.p += (size_t)Elem<T>::BK * ld;
+    r.kk += Elem<T>::BK;
+  }
+  // buffer protocol (gemm_bk_kernel)
+  static constexpr bool kBuf = true;
+  __device__ rsrc_t rsrc() const { return buf_rsrc(p, (unsigned)(((size_t)(K - 1) * ld + M) * sizeof(T))); }
+  struct BRow { unsigned o; int kk; };
+  typedef unsigned BCol;
+  __device__ BRow brstart(int k, int kb) const { return BRow{(unsigned)((size_t)(kb + k) * ld * sizeof(T)), kb + k}; }
+  __device__ unsigned bcstart(int m) const { return m < M ? (unsigned)(m * sizeof(T)) : kOOB; }
+  __device__ unsigned boff(const BRow& r, unsigned c) const { return r.kk < K ? r.o + c : kOOB; }
+  __device__ void bradvance(BRow& r) const {
+    r.o += (unsigned)(Elem<T>::BK * ld * sizeof(T));
     r.kk += Elem<T>::BK;
   }
 };
