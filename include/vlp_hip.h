@@ -55,6 +55,14 @@ int vlp_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, int N, i
                    const float* bn_scale, const float* bn_shift, const float* bn_mean,
                    const float* bn_invstd, double* stat1, double* stat2, int stat_rep,
                    void* stream);
+/* dgrad fused with the next block's output ReLU and BN2 backward sums:
+ * g = (dgrad + addend) * (relu_out > 0); stat1 += sum g, stat2 += sum g*(y-mean)*invstd
+ * (replaces the separate bn_bwd_reduce pass over dx, out, y2) */
+int vlp_conv_dgrad_relu(int dtype, const void* dy, const void* wt, void* g, int N, int H, int W,
+                        int C, int Co, int KH, int KW, int S, int P, const void* addend,
+                        const void* relu_out, const void* y, const float* mean,
+                        const float* invstd, double* stat1, double* stat2, int stat_rep,
+                        void* stream);
 /* dw_ws[Co][KH][KW][C] += sum over pixels dy x_patch (fp32 atomics; zero first).
  * Optional BN+ReLU-on-load of x as in vlp_conv_fwd.  dyT (optional, bf16): the
  * same gradient transposed to [Co][N*Ho*Wo] (vlp_bn_bwd_apply writes it); when
@@ -115,10 +123,18 @@ int vlp_bn_param_grad(int C, const double* sum_g, const double* sum_gx, float* d
                       float* dbeta, void* stream);
 int vlp_maxpool_fwd(int dtype, int N, int H, int W, int C, const void* y, const float* sc,
                     const float* sh, void* out, uint8_t* idx, void* stream);
+/* stem backward, pass 1: g = dp routed to each window's recorded argmax, masked by
+ * the stem ReLU; accumulates sum g and sum g*xhat(y) (g itself is not stored) */
 int vlp_maxpool_bwd(int dtype, int N, int H, int W, int C, const void* dp, const uint8_t* idx,
                     const void* y, const float* sc, const float* sh, const float* mean,
-                    const float* istd, void* g_out, double* sum_g, double* sum_gx, int stat_rep,
+                    const float* istd, double* sum_g, double* sum_gx, int stat_rep,
                     void* stream);
+/* stem backward, pass 2: recomputes g and writes the BatchNorm input gradient
+ * dy = gamma*istd*(g - mean(g) - xhat*mean(g*xhat)) in one stream over y */
+int vlp_maxpool_bwd_apply(int dtype, int N, int H, int W, int C, const void* dp,
+                          const uint8_t* idx, const void* y, const float* sc, const float* sh,
+                          const float* mean, const float* istd, const float* gamma,
+                          const double* sum_g, const double* sum_gx, void* dy, void* stream);
 int vlp_avgpool_fwd(int dtype, int N, int HW, int C, const void* x, void* feat, void* stream);
 
 /* ---------------- text tower (TinyBERT) ----------------

@@ -398,85 +398,144 @@ maxpool_fwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const T* __restri
 }
 
 // ---- stem backward: route pooled gradient to argmax, ReLU mask, BN stats ----
+// g[n,h,w,c] = sum of dp over the pooled outputs whose recorded argmax is
+// (h, w), masked by the stem ReLU (relu(sc*y + sh) > 0).  A block owns
+// kMpRows input rows of one image; each thread a FIXED 8-channel chunk column
+// and a strided set of pixels, so all index math is shifts and adds.
+constexpr int kMpRows = 16;
+
+// An input row h is covered by pooled rows ho = (h + 1 - dh) / 2 for the
+// dh in {0,1,2} of matching parity: one candidate (dh = 1) for even h, two
+// (dh = 0, 2) for odd h; the same for columns.  All four candidate gathers
+// are issued unconditionally (clamped in-bounds addresses, zeroed by their
+// validity) so the loads of a pixel fly together instead of one round trip
+// per tap.
+struct MpCand { int a, b, ta, tb; bool va, vb; };
+__device__ __forceinline__ MpCand mp_cand(int h, int Ho) {
+  MpCand c;
+  if (h & 1) {
+    c.a = (h + 1) >> 1; c.ta = 0; c.va = c.a < Ho;
+    c.b = (h - 1) >> 1; c.tb = 2; c.vb = true;
+  } else {
+    c.a = h >> 1; c.ta = 1; c.va = c.a < Ho;
+    c.b = c.a; c.tb = 1; c.vb = false;
+  }
+  c.a = c.a < Ho ? c.a : Ho - 1;
+  c.b = c.b < Ho ? c.b : Ho - 1;
+  return c;
+}
+
 template <typename T>
+__device__ __forceinline__ void mp_route(const T* __restrict__ dp, const uint8_t* __restrict__ idx, int n,
+                                         const MpCand& ch, int w, int c0, int C, int Ho, int Wo, float* g) {
+  constexpr int E = Chunk<T>::N;
+  const MpCand cw = mp_cand(w, Wo);
+  uint4 v[4];
+  uint2 ib[4];
+  int tap[4];
+  bool ok[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int ho = (q >> 1) ? ch.b : ch.a, wo = (q & 1) ? cw.b : cw.a;
+    tap[q] = ((q >> 1) ? ch.tb : ch.ta) * 3 + ((q & 1) ? cw.tb : cw.ta);
+    ok[q] = ((q >> 1) ? ch.vb : ch.va) && ((q & 1) ? cw.vb : cw.va);
+    const size_t po = (((size_t)n * Ho + ho) * Wo + wo) * C + c0;
+    v[q] = ldg16(dp + po);
+    if constexpr (E == 8) {
+      ib[q] = *reinterpret_cast<const uint2*>(idx + po);
+    } else {
+      ib[q].x = *reinterpret_cast<const unsigned*>(idx + po);
+      ib[q].y = 0;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < E; ++j) g[j] = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float f[E];
+    Chunk<T>::unpack(v[q], f);
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const unsigned b = (((j >> 2) ? ib[q].y : ib[q].x) >> (8 * (j & 3))) & 255u;
+      g[j] += (ok[q] && b == (unsigned)tap[q]) ? f[j] : 0.f;
+    }
+  }
+}
+
+// APPLY = false: BN backward sums only (sum g, sum g*xhat), nothing written.
+// APPLY = true : dy = k*g + b*y + c (the folded BN backward), written in place
+//                of the routed gradient, which is never materialised.
+template <typename T, bool APPLY>
 __global__ void __launch_bounds__(256)
 maxpool_bwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const T* __restrict__ dp,
                    const uint8_t* __restrict__ idx, const T* __restrict__ y,
                    const float* __restrict__ sc, const float* __restrict__ sh,
                    const float* __restrict__ mean, const float* __restrict__ istd,
-                   T* __restrict__ g_out, double* sum_g, double* sum_gx, int rep) {
+                   const float* __restrict__ gamma, const double* __restrict__ sg,
+                   const double* __restrict__ sgx, T* __restrict__ dy, double* sum_g, double* sum_gx,
+                   int rep) {
   constexpr int E = Chunk<T>::N;
   const int cpr = C / E;
-  const int rows_per_iter = 256 / cpr;
   const int t = threadIdx.x;
-  const int cc = t % cpr, rr = t / cpr;
-  const int c0 = cc * E;
-  const int M = N * H * W;
-  float ag[E], ax[E], a[E], b[E], mu[E], is[E];
+  const int cc = t % cpr, c0 = cc * E;
+  const int wstep = 256 / cpr;
+  const int rb = blockIdx.x % ((H + kMpRows - 1) / kMpRows);
+  const int n = blockIdx.x / ((H + kMpRows - 1) / kMpRows);
+  float a[E], b[E], mu[E], is[E], ka[E], ba[E], ca[E], ag[E], ax[E];
+  const float inv_count = 1.f / (float)((double)N * H * W);
 #pragma unroll
   for (int j = 0; j < E; ++j) {
+    const int c = c0 + j;
+    a[j] = sc[c]; b[j] = sh[c]; mu[j] = mean[c]; is[j] = istd[c];
     ag[j] = ax[j] = 0.f;
-    a[j] = sc[c0 + j]; b[j] = sh[c0 + j]; mu[j] = mean[c0 + j]; is[j] = istd[c0 + j];
+    if constexpr (APPLY) {
+      const float k = gamma[c] * is[j];
+      const float mg = (float)(sg[c] * (double)inv_count), mgx = (float)(sgx[c] * (double)inv_count);
+      ka[j] = k; ba[j] = -k * is[j] * mgx; ca[j] = -k * mg + k * is[j] * mgx * mu[j];
+    }
   }
-  for (int m = blockIdx.x * rows_per_iter + rr; m < M; m += gridDim.x * rows_per_iter) {
-    int w = m % W;
-    int tt = m / W;
-    int h = tt % H;
-    int n = tt / H;
-    float g[E], v[E], yv[E];
+  for (int r = 0; r < kMpRows; ++r) {
+    const int h = rb * kMpRows + r;
+    if (h >= H) break;
+    const MpCand ch = mp_cand(h, Ho);
+    for (int w = t / cpr; w < W; w += wstep) {
+      float g[E], yv[E];
+      mp_route<T>(dp, idx, n, ch, w, c0, C, Ho, Wo, g);
+      const size_t o = (((size_t)n * H + h) * W + w) * C + c0;
+      Chunk<T>::unpack(ldg16(y + o), yv);
+      if constexpr (APPLY) {
+        float d[E];
 #pragma unroll
-    for (int j = 0; j < E; ++j) g[j] = 0.f;
-    for (int dh = 0; dh < 3; ++dh) {
-      int th = h + 1 - dh;
-      if (th < 0 || (th & 1)) continue;
-      int ho = th >> 1;
-      if (ho >= Ho) continue;
-      for (int dw = 0; dw < 3; ++dw) {
-        int tw = w + 1 - dw;
-        if (tw < 0 || (tw & 1)) continue;
-        int wo = tw >> 1;
-        if (wo >= Wo) continue;
-        size_t po = (((size_t)n * Ho + ho) * Wo + wo) * C + c0;
-        Chunk<T>::unpack(ldg16(dp + po), v);
-        uint8_t ib[E];
-        if constexpr (E == 8) {
-          uint2 u = *reinterpret_cast<const uint2*>(idx + po);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) { ib[j] = (u.x >> (8 * j)) & 255; ib[4 + j] = (u.y >> (8 * j)) & 255; }
-        } else {
-          unsigned u = *reinterpret_cast<const unsigned*>(idx + po);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) ib[j] = (u >> (8 * j)) & 255;
+        for (int j = 0; j < E; ++j) {
+          const float gg = fmaf(yv[j], a[j], b[j]) > 0.f ? g[j] : 0.f;
+          d[j] = fmaf(ka[j], gg, fmaf(ba[j], yv[j], ca[j]));
         }
-        const uint8_t tap = (uint8_t)(dh * 3 + dw);
+        stg16(dy + o, Chunk<T>::pack(d));
+      } else {
 #pragma unroll
-        for (int j = 0; j < E; ++j)
-          if (ib[j] == tap) g[j] += v[j];
+        for (int j = 0; j < E; ++j) {
+          const float gg = fmaf(yv[j], a[j], b[j]) > 0.f ? g[j] : 0.f;
+          ag[j] += gg;
+          ax[j] += gg * ((yv[j] - mu[j]) * is[j]);
+        }
       }
     }
-    size_t o = (size_t)m * C + c0;
-    Chunk<T>::unpack(ldg16(y + o), yv);
-#pragma unroll
-    for (int j = 0; j < E; ++j) {
-      if (!(fmaf(yv[j], a[j], b[j]) > 0.f)) g[j] = 0.f;
-      ag[j] += g[j];
-      ax[j] += g[j] * ((yv[j] - mu[j]) * is[j]);
-    }
-    stg16(g_out + o, Chunk<T>::pack(g));
   }
-  __shared__ float red[2][256][E];
+  if constexpr (!APPLY) {
+    __shared__ float red[2][256][E];
 #pragma unroll
-  for (int j = 0; j < E; ++j) { red[0][t][j] = ag[j]; red[1][t][j] = ax[j]; }
-  __syncthreads();
-  if (t < cpr) {
-    for (int r = 1; r < rows_per_iter; ++r)
+    for (int j = 0; j < E; ++j) { red[0][t][j] = ag[j]; red[1][t][j] = ax[j]; }
+    __syncthreads();
+    if (t < cpr) {
+      for (int q = t + cpr; q < 256; q += cpr)
 #pragma unroll
-      for (int j = 0; j < E; ++j) { ag[j] += red[0][t + r * cpr][j]; ax[j] += red[1][t + r * cpr][j]; }
-    const size_t ro = (size_t)(blockIdx.x % rep) * C + c0;
+        for (int j = 0; j < E; ++j) { ag[j] += red[0][q][j]; ax[j] += red[1][q][j]; }
+      const size_t ro = (size_t)(blockIdx.x % rep) * C + c0;
 #pragma unroll
-    for (int j = 0; j < E; ++j) {
-      atomicAdd(sum_g + ro + j, (double)ag[j]);
-      atomicAdd(sum_gx + ro + j, (double)ax[j]);
+      for (int j = 0; j < E; ++j) {
+        atomicAdd(sum_g + ro + j, (double)ag[j]);
+        atomicAdd(sum_gx + ro + j, (double)ax[j]);
+      }
     }
   }
 }
@@ -644,22 +703,43 @@ VLP_EXPORT int vlp_maxpool_fwd(int dtype, int N, int H, int W, int C, const void
 
 VLP_EXPORT int vlp_maxpool_bwd(int dtype, int N, int H, int W, int C, const void* dp,
                                const uint8_t* idx, const void* y, const float* sc, const float* sh,
-                               const float* mean, const float* istd, void* g_out, double* sum_g,
+                               const float* mean, const float* istd, double* sum_g,
                                double* sum_gx, int stat_rep, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
   int epc = dtype == VLP_BF16 ? 8 : 4;
-  int rows_per_iter = 256 / (C / epc);
-  int blocks = ew_blocks((size_t)N * H * W, rows_per_iter * 16, 4096);
+  if (256 % (C / epc)) return (int)hipErrorInvalidValue;
+  dim3 grid((unsigned)(N * ((H + kMpRows - 1) / kMpRows)));
   if (stat_rep < 1) stat_rep = 1;
   if (dtype == VLP_BF16)
-    hipLaunchKernelGGL(maxpool_bwd_kernel<bf16>, dim3(blocks), dim3(256), 0, st, N, H, W, C, Ho, Wo,
-                       (const bf16*)dp, idx, (const bf16*)y, sc, sh, mean, istd, (bf16*)g_out, sum_g,
-                       sum_gx, stat_rep);
+    hipLaunchKernelGGL((maxpool_bwd_kernel<bf16, false>), grid, dim3(256), 0, st, N, H, W, C, Ho, Wo,
+                       (const bf16*)dp, idx, (const bf16*)y, sc, sh, mean, istd, nullptr, nullptr, nullptr,
+                       nullptr, sum_g, sum_gx, stat_rep);
   else
-    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, dim3(blocks), dim3(256), 0, st, N, H, W, C, Ho, Wo,
-                       (const float*)dp, idx, (const float*)y, sc, sh, mean, istd, (float*)g_out,
-                       sum_g, sum_gx, stat_rep);
+    hipLaunchKernelGGL((maxpool_bwd_kernel<float, false>), grid, dim3(256), 0, st, N, H, W, C, Ho, Wo,
+                       (const float*)dp, idx, (const float*)y, sc, sh, mean, istd, nullptr, nullptr,
+                       nullptr, nullptr, sum_g, sum_gx, stat_rep);
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_maxpool_bwd_apply(int dtype, int N, int H, int W, int C, const void* dp,
+                                     const uint8_t* idx, const void* y, const float* sc,
+                                     const float* sh, const float* mean, const float* istd,
+                                     const float* gamma, const double* sum_g, const double* sum_gx,
+                                     void* dy, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  int epc = dtype == VLP_BF16 ? 8 : 4;
+  if (256 % (C / epc)) return (int)hipErrorInvalidValue;
+  dim3 grid((unsigned)(N * ((H + kMpRows - 1) / kMpRows)));
+  if (dtype == VLP_BF16)
+    hipLaunchKernelGGL((maxpool_bwd_kernel<bf16, true>), grid, dim3(256), 0, st, N, H, W, C, Ho, Wo,
+                       (const bf16*)dp, idx, (const bf16*)y, sc, sh, mean, istd, gamma, sum_g, sum_gx,
+                       (bf16*)dy, nullptr, nullptr, 1);
+  else
+    hipLaunchKernelGGL((maxpool_bwd_kernel<float, true>), grid, dim3(256), 0, st, N, H, W, C, Ho, Wo,
+                       (const float*)dp, idx, (const float*)y, sc, sh, mean, istd, gamma, sum_g, sum_gx,
+                       (float*)dy, nullptr, nullptr, 1);
   return (int)hipGetLastError();
 }
 

@@ -335,9 +335,13 @@ struct EpiS2Remap {
   __device__ void operator()(int row, int col, v4f v, v4f& s1, v4f& s2) const {
     inner(grow(row), col, v, s1, s2);
   }
-  static constexpr bool kStage = true;
+  static constexpr bool kStage = StageTrait<EP>::value;
+  static constexpr bool kRow = RowTrait<EP>::value;
   __device__ v4f value(int row, int col, v4f v, v4f& s1, v4f& s2) const {
     return inner.value(grow(row), col, v, s1, s2);
+  }
+  __device__ void row8(int row, int col, const float (&v)[8], float (&s1)[8], float (&s2)[8]) const {
+    inner.row8(grow(row), col, v, s1, s2);
   }
   __device__ void store8(int row, int col, const uint4& u) const { inner.store8(grow(row), col, u); }
 };
@@ -737,7 +741,20 @@ struct EpiDgradBN {
     s1 = g;
     s2 = g * ((yv - mu) * is);
   }
-  static constexpr bool kStage = true;
+  static constexpr bool kRow = true;
+  __device__ void row8(int row, int col, const float (&v)[8], float (&s1)[8], float (&s2)[8]) const {
+    const size_t o = (size_t)row * C + col;
+    float yv[8], g[8];
+    Chunk<bf16>::unpack(ldg16(y + o), yv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      g[j] = fmaf(yv[j], sc[col + j], sh[col + j]) > 0.f ? v[j] : 0.f;
+      s1[j] += g[j];
+      s2[j] += g[j] * ((yv[j] - mean[col + j]) * invstd[col + j]);
+    }
+    stg16(g_out + o, Chunk<bf16>::pack(g));
+  }
+  static constexpr bool kStage = false;
   __device__ v4f value(int row, int col, v4f v, v4f& s1, v4f& s2) const {
     v4f yv = load4(y + (size_t)row * C + col);
     v4f sc4 = *reinterpret_cast<const v4f*>(sc + col);
@@ -764,12 +781,78 @@ struct EpiDgradAdd {
     if (addend) v += load4(addend + o);
     store4(dx + o, v);
   }
-  static constexpr bool kStage = true;
+  static constexpr bool kRow = true;
+  __device__ void row8(int row, int col, const float (&v)[8], float (&)[8], float (&)[8]) const {
+    const size_t o = (size_t)row * C + col;
+    float d[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = v[j];
+    if (addend) {
+      float a[8];
+      Chunk<bf16>::unpack(ldg16(addend + o), a);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] += a[j];
+    }
+    stg16(dx + o, Chunk<bf16>::pack(d));
+  }
+  static constexpr bool kStage = false;
   __device__ v4f value(int row, int col, v4f v, v4f&, v4f&) const {
     if (addend) v += load4(addend + (size_t)row * C + col);
     return v;
   }
   __device__ void store8(int row, int col, const uint4& u) const { stg16(dx + (size_t)row * C + col, u); }
+};
+
+// data gradient (+ residual-branch addend) through the NEXT block's output
+// ReLU, plus that block's BN2 backward sums: the gradient reaching block b-1
+// is g = (conv_dgrad + addend) * (out_{b-1} > 0), and its bn2 needs sum(g),
+// sum(g * xhat(y2_{b-1})).  Fusing this here removes the separate reduction
+// pass over (dx, out, y2) and lets the next BN-backward apply read g directly.
+template <typename T>
+struct EpiDgradRelu {
+  static constexpr bool kStats = true;
+  double* stat1; double* stat2; int stat_rep;
+  T* g_out; const T* addend; int C;
+  const T* relu_out; const T* y; const float* mean; const float* invstd;
+  __device__ v4f grad(int row, int col, v4f v, v4f& s1, v4f& s2) const {
+    const size_t o = (size_t)row * C + col;
+    if (addend) v += load4(addend + o);
+    const v4f r = load4(relu_out + o);
+    const v4f yv = load4(y + o);
+    const v4f mu = *reinterpret_cast<const v4f*>(mean + col);
+    const v4f is = *reinterpret_cast<const v4f*>(invstd + col);
+    v4f g;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) g[j] = r[j] > 0.f ? v[j] : 0.f;
+    s1 = g;
+    s2 = g * ((yv - mu) * is);
+    return g;
+  }
+  __device__ void operator()(int row, int col, v4f v, v4f& s1, v4f& s2) const {
+    store4(g_out + (size_t)row * C + col, grad(row, col, v, s1, s2));
+  }
+  static constexpr bool kRow = true;
+  __device__ void row8(int row, int col, const float (&v)[8], float (&s1)[8], float (&s2)[8]) const {
+    const size_t o = (size_t)row * C + col;
+    float a[8], r[8], yv[8], g[8];
+    if (addend) Chunk<bf16>::unpack(ldg16(addend + o), a);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] = 0.f;
+    }
+    Chunk<bf16>::unpack(ldg16(relu_out + o), r);
+    Chunk<bf16>::unpack(ldg16(y + o), yv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      g[j] = r[j] > 0.f ? v[j] + a[j] : 0.f;
+      s1[j] += g[j];
+      s2[j] += g[j] * ((yv[j] - mean[col + j]) * invstd[col + j]);
+    }
+    stg16(g_out + o, Chunk<bf16>::pack(g));
+  }
+  static constexpr bool kStage = false;
+  __device__ v4f value(int row, int col, v4f v, v4f& s1, v4f& s2) const { return grad(row, col, v, s1, s2); }
+  __device__ void store8(int row, int col, const uint4& u) const { stg16(g_out + (size_t)row * C + col, u); }
 };
 
 // ---------------- tile-config dispatch ----------------
@@ -856,6 +939,34 @@ static int conv_dgrad_t(const void* dy, const void* wt, void* dx, ConvGeom g, co
   }
   EpiDgradAdd<T> ep{nullptr, nullptr, (T*)dx, (const T*)addend, g.C};
   return gemm_auto<T>(g.M, g.C, g.K, 1, la, lb, ep, st);
+}
+
+// dgrad whose output is masked by a ReLU output and reduced for a BN backward
+template <typename T>
+static int conv_dgrad_relu_t(const void* dy, const void* wt, void* gout, ConvGeom g0, const void* addend,
+                             const void* relu_out, const void* y, const float* mean, const float* invstd,
+                             double* s1, double* s2, int rep, hipStream_t st) {
+  ConvGeom g = g0;
+  g.M = g.N * g.H * g.W;
+  g.K = g.KH * g.KW * g.Co;
+  EpiDgradRelu<T> in{s1, s2, rep, (T*)gout, (const T*)addend, g.C, (const T*)relu_out, (const T*)y, mean, invstd};
+  if (g.S == 2) {
+    for (int ph = 0; ph < 2; ++ph)
+      for (int pw = 0; pw < 2; ++pw) {
+        S2Class c = make_s2class(g, ph, pw);
+        const int Mc = g.N * c.Hc * c.Wc, Kc = c.nth * c.ntw * g.Co;
+        if (Mc <= 0) continue;
+        ConvDgradS2A<T> la{g, c, (const T*)dy, Mc, Kc};
+        WtS2B<T> lb{(const T*)wt, g, c, Kc};
+        EpiS2Remap<EpiDgradRelu<T>> ep{s1, s2, rep, in, c, g.H, g.W};
+        const int r = gemm_auto<T>(Mc, g.C, Kc, 1, la, lb, ep, st);
+        if (r) return r;
+      }
+    return 0;
+  }
+  ConvDgradA<T> la{g, (const T*)dy};
+  KMat<T> lb{(const T*)wt, g.K, g.C, g.K};
+  return gemm_auto<T>(g.M, g.C, g.K, 1, la, lb, in, st);
 }
 
 template <typename T>
@@ -961,6 +1072,18 @@ VLP_EXPORT int vlp_conv_dgrad(int dtype, const void* dy, const void* wt, void* d
                               stat1, stat2, stat_rep, st);
   return conv_dgrad_t<float>(dy, wt, dx, g, addend, y_bn, bn_scale, bn_shift, bn_mean, bn_invstd,
                              stat1, stat2, stat_rep, st);
+}
+
+VLP_EXPORT int vlp_conv_dgrad_relu(int dtype, const void* dy, const void* wt, void* g, int N, int H,
+                                   int W, int C, int Co, int KH, int KW, int S, int P,
+                                   const void* addend, const void* relu_out, const void* y,
+                                   const float* mean, const float* invstd, double* stat1,
+                                   double* stat2, int stat_rep, void* stream) {
+  ConvGeom geo = make_geom(N, H, W, C, Co, KH, KW, S, P);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == VLP_BF16)
+    return conv_dgrad_relu_t<bf16>(dy, wt, g, geo, addend, relu_out, y, mean, invstd, stat1, stat2, stat_rep, st);
+  return conv_dgrad_relu_t<float>(dy, wt, g, geo, addend, relu_out, y, mean, invstd, stat1, stat2, stat_rep, st);
 }
 
 VLP_EXPORT int vlp_conv_wgrad(int dtype, const void* dy, const void* x, float* dw_ws, int N, int H,

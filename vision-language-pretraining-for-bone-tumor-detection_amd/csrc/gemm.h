@@ -164,6 +164,10 @@ template <class E, class = void> struct StageTrait { static constexpr bool value
 template <class E> struct StageTrait<E, std::void_t<decltype(E::kStage)>> {
   static constexpr bool value = E::kStage;
 };
+template <class E, class = void> struct RowTrait { static constexpr bool value = false; };
+template <class E> struct RowTrait<E, std::void_t<decltype(E::kRow)>> {
+  static constexpr bool value = E::kRow;
+};
 template <class L> struct DirectTrait<L, std::void_t<decltype(L::kDirect)>> {
   static constexpr bool value = L::kDirect;
 };
@@ -549,6 +553,61 @@ __device__ __forceinline__ void ms_epilogue(const GemmShape& sh, const EP& ep, v
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   const int l = threadIdx.x & 63;
   const int li = l & 15, lg = l >> 4;
+  if constexpr (RowTrait<EP>::value) {
+    // row-chunk epilogue: the raw accumulators are staged as a bf16 tile, then
+    // every thread walks 16-B row chunks of ONE fixed 8-column group, so the
+    // epilogue's own operand loads (residual, ReLU mask, BN input) are
+    // row-contiguous 16-B loads like its stores, and the per-column statistic
+    // partials stay in 16 registers per thread until one LDS reduction.
+    constexpr int CPR = BN / 8;
+    static_assert(NT % CPR == 0, "row-chunk geometry");
+    bf16* stg = reinterpret_cast<bf16*>(smem);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int coll = wn * WTN + b * 16 + 4 * lg;
+#pragma unroll
+      for (int a = 0; a < MB; ++a) {
+        const int rowl = wm * WTM + a * 16 + li;
+        v4bf ob;
+        ob[0] = (bf16)acc[a][b][0]; ob[1] = (bf16)acc[a][b][1];
+        ob[2] = (bf16)acc[a][b][2]; ob[3] = (bf16)acc[a][b][3];
+        *reinterpret_cast<v4bf*>(stg + rowl * BN + (((coll >> 3) ^ (rowl & (CPR - 1))) << 3) + (coll & 4)) = ob;
+      }
+    }
+    __syncthreads();
+    const int c = threadIdx.x % CPR;
+    const int col = col0 + c * 8;
+    float s1[8], s2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+    for (int r = threadIdx.x / CPR; r < BM; r += NT / CPR) {
+      const int row = row0 + r;
+      if (row < sh.M && col < sh.N) {
+        float v[8];
+        Chunk<bf16>::unpack(*reinterpret_cast<const uint4*>(stg + r * BN + ((c ^ (r & (CPR - 1))) << 3)), v);
+        ep.row8(row, col, v, s1, s2);
+      }
+    }
+    if constexpr (EP::kStats) {
+      __syncthreads();
+      float* red = reinterpret_cast<float*>(smem);   // [NT][16]
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[threadIdx.x * 16 + j] = s1[j];
+        red[threadIdx.x * 16 + 8 + j] = s2[j];
+      }
+      __syncthreads();
+      const int rep = ep.stat_rep > 1 ? (wid % ep.stat_rep) : 0;
+      for (int q = threadIdx.x; q < 2 * BN; q += NT) {
+        const int cl = q >> 1, stt = q & 1;
+        const int cc = cl >> 3, j = cl & 7;
+        float x = 0.f;
+        for (int k = cc; k < NT; k += CPR) x += red[k * 16 + stt * 8 + j];
+        if (col0 + cl < sh.N) atomicAdd((stt ? ep.stat2 : ep.stat1) + (size_t)rep * sh.N + col0 + cl, (double)x);
+      }
+    }
+    return;
+  }
   float* red = reinterpret_cast<float*>(smem);
   // staged epilogues: outputs go through a bf16 LDS tile (16-B chunks XOR-
   // swizzled by row) and leave as full 16-B row segments, 4..8 rows per wave

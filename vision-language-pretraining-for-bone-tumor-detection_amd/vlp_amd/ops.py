@@ -75,6 +75,20 @@ def conv_dgrad(dy, wt, H, W, C, KH, KW, S, P, addend=None, y_bn=None, bn=None, s
     return dx
 
 
+def conv_dgrad_relu(dy, wt, H, W, C, KH, KW, S, P, relu_out, y, mean, invstd, stat1, stat2,
+                    addend=None, stat_rep=1):
+    """g = (dgrad(dy) + addend) * (relu_out > 0), plus the BN backward sums of g
+    against y (the next block's bn2 input)."""
+    N, Ho, Wo, Co = dy.shape
+    g = torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
+    tk = ktimer.begin(f"conv_dgrad[relu]{_tile_auto(C)}", 2.0 * N * Ho * Wo * Co * C * KH * KW)
+    lib().vlp_conv_dgrad_relu(dcode(dy), ptr(dy), ptr(wt), ptr(g), N, H, W, C, Co, KH, KW, S, P,
+                              ptr(addend), ptr(relu_out), ptr(y), ptr(mean), ptr(invstd), ptr(stat1),
+                              ptr(stat2), int(stat_rep), _s())
+    ktimer.end(tk)
+    return g
+
+
 def conv_wgrad(dy, x, KH, KW, S, P, dw_ws, in_scale=None, in_shift=None, dyT=None):
     N, H, W, C = x.shape
     Co = dy.shape[-1]
@@ -168,10 +182,18 @@ def maxpool_fwd(y, sc, sh, out, idx):
     lib().vlp_maxpool_fwd(dcode(y), N, H, W, C, ptr(y), ptr(sc), ptr(sh), ptr(out), ptr(idx), _s())
 
 
-def maxpool_bwd(dp, idx, y, sc, sh, mean, istd, g_out, sum_g, sum_gx, stat_rep=1):
+def maxpool_bwd(dp, idx, y, sc, sh, mean, istd, sum_g, sum_gx, stat_rep=1):
+    """BN backward sums of the routed, ReLU-masked stem gradient (nothing stored)."""
     N, H, W, C = y.shape
     lib().vlp_maxpool_bwd(dcode(y), N, H, W, C, ptr(dp), ptr(idx), ptr(y), ptr(sc), ptr(sh),
-                          ptr(mean), ptr(istd), ptr(g_out), ptr(sum_g), ptr(sum_gx), int(stat_rep), _s())
+                          ptr(mean), ptr(istd), ptr(sum_g), ptr(sum_gx), int(stat_rep), _s())
+
+
+def maxpool_bwd_apply(dp, idx, y, sc, sh, mean, istd, gamma, sum_g, sum_gx, dy):
+    """dy = BN1'(relu-masked routed gradient), recomputing the routing."""
+    N, H, W, C = y.shape
+    lib().vlp_maxpool_bwd_apply(dcode(y), N, H, W, C, ptr(dp), ptr(idx), ptr(y), ptr(sc), ptr(sh),
+                                ptr(mean), ptr(istd), ptr(gamma), ptr(sum_g), ptr(sum_gx), ptr(dy), _s())
 
 
 def avgpool_fwd(x, feat):

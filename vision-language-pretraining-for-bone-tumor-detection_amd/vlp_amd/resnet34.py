@@ -319,6 +319,7 @@ class ResNet34Tower(ArenaModule):
         dfeat = dfeat.float().contiguous()
         blocks = saved["blocks"]
         dout = None
+        dout_masked = False   # dout already = g (ReLU-masked) with bn2 sums accumulated by the dgrad epilogue
         for bi in range(len(self._blocks) - 1, -1, -1):
             pre, has_ds = self._blocks[bi]
             B = blocks[bi]
@@ -338,8 +339,9 @@ class ResNet34Tower(ArenaModule):
                 kd = pre + ".downsample.1"
                 _, _, mud, isd = self._coef(ws, kd)
                 sgxdf = self._bstat_ds(ws, k2, full=True)
-            ops.bn_bwd_reduce(M, C, dout, dbc, HW, out, y2, mu2, is2, yd, mud, isd, sg2f, sgx2f, sgxdf, out,
-                              stat_rep=STAT_REP)
+            if not dout_masked:
+                ops.bn_bwd_reduce(M, C, dout, dbc, HW, out, y2, mu2, is2, yd, mud, isd, sg2f, sgx2f, sgxdf,
+                                  out, stat_rep=STAT_REP)
             ops.stat_reduce(STAT_REP, C, sg2f, sgx2f, sgxdf)
             sg2, sgx2 = sg2f[:C], sgx2f[:C]
             sgxd = sgxdf[:C] if has_ds else None
@@ -351,11 +353,14 @@ class ResNet34Tower(ArenaModule):
                 dyd = torch.empty_like(yd)
                 Bside = (yd, mud, isd, self.arena.view(kd + ".weight"), sg2, sgxd, dyd)
                 ops.bn_param_grad(sg2, sgxd, self.arena.gview(kd + ".weight"), self.arena.gview(kd + ".bias"))
+            elif dout_masked:
+                g_id = dout          # the identity branch's gradient is g itself
             else:
                 g_id = torch.empty_like(out)
             tA = self._tbuf(ws, "tA", C, M)
             tB = self._tbuf(ws, "tB", C, M) if (has_ds and tA is not None) else None
-            ops.bn_bwd_apply(M, C, dout, dbc, HW, out, A, Bside, g_id, out, dyT_a=tA, dyT_b=tB)
+            ops.bn_bwd_apply(M, C, dout, dbc, HW, None if dout_masked else out, A, Bside,
+                             None if dout_masked else g_id, out, dyT_a=tA, dyT_b=tB)
             # conv2: dgrad through relu(bn1(y1)) with BN1 backward sums; wgrad on relu(bn1(y1))
             sc1, sh1, mu1, is1 = self._coef(ws, k1)
             sg1f, sgx1f = self._bstat(ws, k1, full=True)
@@ -375,24 +380,33 @@ class ResNet34Tower(ArenaModule):
                 cd = self._convs[pre + ".downsample.0"]
                 addend = ops.conv_dgrad(dyd, ws[cd.key + ".wt"], Hi, Wi, Cin, 1, 1, cd.S, 0)
                 self._wgrad(ws, cd, dyd, x, dyT=tB)
-            dx = ops.conv_dgrad(dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, addend=addend)
+            # the gradient reaching block bi-1 passes its output ReLU and feeds its bn2:
+            # when that block has no downsample branch, mask + reduce in this epilogue
+            prev = self._blocks[bi - 1] if bi > 0 else None
+            if prev is not None and not prev[1]:
+                kp = prev[0] + ".bn2"
+                _, _, mup, isp = self._coef(ws, kp)
+                sgpf, sgxpf = self._bstat(ws, kp, full=True)
+                dx = ops.conv_dgrad_relu(dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, x,
+                                         blocks[bi - 1]["y2"], mup, isp, sgpf, sgxpf, addend=addend,
+                                         stat_rep=STAT_REP)
+                dout_masked = True
+            else:
+                dx = ops.conv_dgrad(dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, addend=addend)
+                dout_masked = False
             self._wgrad(ws, c1, dy1, x, dyT=tA)
             dout = dx
         # stem: maxpool -> relu -> bn1 -> conv1
         y0, idx = saved["y0"], saved["idx"]
         sc0, sh0, mu0, is0 = self._coef(ws, "bn1")
         sg0f, sgx0f = self._bstat(ws, "bn1", full=True)
-        g0 = torch.empty_like(y0)
-        ops.maxpool_bwd(dout, idx, y0, sc0, sh0, mu0, is0, g0, sg0f, sgx0f, stat_rep=STAT_REP)
+        ops.maxpool_bwd(dout, idx, y0, sc0, sh0, mu0, is0, sg0f, sgx0f, stat_rep=STAT_REP)
         ops.stat_reduce(STAT_REP, 64, sg0f, sgx0f)
         sg0, sgx0 = sg0f[:64], sgx0f[:64]
         ops.bn_param_grad(sg0, sgx0, self.arena.gview("bn1.weight"), self.arena.gview("bn1.bias"))
         dy0 = torch.empty_like(y0)
-        M0 = y0.numel() // 64
-        t0 = self._tbuf(ws, "tA", 64, M0)
-        ops.bn_bwd_apply(M0, 64, g0, None, 1, None,
-                         (y0, mu0, is0, self.arena.view("bn1.weight"), sg0, sgx0, dy0), None, None, y0,
-                         dyT_a=t0)
+        ops.maxpool_bwd_apply(dout, idx, y0, sc0, sh0, mu0, is0, self.arena.view("bn1.weight"), sg0, sgx0, dy0)
+        t0 = None
         o, n = self._wg_off["conv1"]
         wsb = ws["wgrad"][o:o + n]
         ops.stem_wgrad(dy0, saved["xp"], saved["N"], saved["H"], saved["W"], wsb, dyT=t0)
