@@ -53,6 +53,7 @@ CONV_CASES = [
     (2, 12, 12, 64, 128, 3, 3, 2, 1),
     (2, 12, 12, 64, 128, 1, 1, 2, 0),
     (3, 7, 9, 128, 64, 3, 3, 1, 1),
+    (3, 5, 128, 64, 64, 3, 3, 1, 1),    # layer-1 width: row-streaming kernel (bf16)
 ]
 
 
@@ -126,8 +127,9 @@ def test_conv_dgrad_wgrad(ops, dt, case):
 
 
 @pytest.mark.parametrize("dt", DT)
-def test_conv_dgrad_bn_epilogue(ops, dt):
-    N, H, W, C, Co, KH, KW, S, P = 2, 10, 10, 64, 64, 3, 3, 1, 1
+@pytest.mark.parametrize("H,W", [(10, 10), (4, 128)])
+def test_conv_dgrad_bn_epilogue(ops, dt, H, W):
+    N, C, Co, KH, KW, S, P = 2, 64, 64, 3, 3, 1, 1
     torch.manual_seed(3)
     dy = torch.randn(N, Co, H, W).to(dt).float()
     w = (torch.randn(Co, C, KH, KW) * 0.05).to(dt).float()
@@ -146,6 +148,41 @@ def test_conv_dgrad_bn_epilogue(ops, dt):
     s2 = torch.zeros_like(s1)
     g = ops.conv_dgrad(nhwc(dy).to(dt).cuda(), wt, H, W, C, KH, KW, S, P, y_bn=nhwc(ybn).to(dt).cuda(),
                        bn=(sc.cuda(), sh.cuda(), mu.cuda(), ist.cuda()), stat1=s1, stat2=s2)
+    torch.cuda.synchronize()
+    assert rel(nchw(g.float().cpu()), gref) < tol(dt)
+    assert rel(s1.cpu(), gref.sum((0, 2, 3))) < tol(dt)
+    assert rel(s2.cpu(), (gref * xh).sum((0, 2, 3))) < tol(dt)
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("case", [(2, 10, 10, 64, 64, 1), (2, 4, 128, 64, 64, 1), (2, 12, 12, 64, 128, 2)])
+@pytest.mark.parametrize("with_add", [False, True])
+def test_conv_dgrad_relu_epilogue(ops, dt, case, with_add):
+    """g = (dgrad + addend) * (relu_out > 0) and the next block's bn2 sums
+    (vlp_conv_dgrad_relu, the fused replacement of the bn_bwd_reduce pass)."""
+    N, H, W, C, Co, S = case
+    torch.manual_seed(5)
+    Ho, Wo = (H - 1) // S + 1, (W - 1) // S + 1
+    dy = torch.randn(N, Co, Ho, Wo).to(dt).float()
+    w = (torch.randn(Co, C, 3, 3) * 0.05).to(dt).float()
+    relu_out = torch.relu(torch.randn(N, C, H, W)).to(dt).float()
+    y2 = torch.randn(N, C, H, W).to(dt).float()
+    add = torch.randn(N, C, H, W).to(dt).float() if with_add else None
+    mu, ist = torch.randn(C) * 0.1, torch.rand(C) + 0.5
+    dxr = torch.nn.grad.conv2d_input((N, C, H, W), w, dy, stride=S, padding=1)
+    if add is not None:
+        dxr = dxr + add
+    if dt == torch.bfloat16:
+        dxr = dxr.to(dt).float()
+    gref = dxr * (relu_out > 0)
+    xh = (y2 - mu.view(1, -1, 1, 1)) * ist.view(1, -1, 1, 1)
+    wt = torch.empty(C, 3, 3, Co, dtype=dt, device="cuda")
+    ops.pack_conv(w.cuda(), None, wt)
+    s1 = torch.zeros(C, dtype=torch.float64, device="cuda")
+    s2 = torch.zeros_like(s1)
+    g = ops.conv_dgrad_relu(nhwc(dy).to(dt).cuda(), wt, H, W, C, 3, 3, S, 1, nhwc(relu_out).to(dt).cuda(),
+                            nhwc(y2).to(dt).cuda(), mu.cuda(), ist.cuda(), s1, s2,
+                            addend=None if add is None else nhwc(add).to(dt).cuda())
     torch.cuda.synchronize()
     assert rel(nchw(g.float().cpu()), gref) < tol(dt)
     assert rel(s1.cpu(), gref.sum((0, 2, 3))) < tol(dt)

@@ -115,42 +115,64 @@ layernorm_bwd_kernel(int M, int D, const T* __restrict__ dy, float p_out, uint64
                      const float* __restrict__ rstd, const float* __restrict__ gamma,
                      T* __restrict__ dx, T* __restrict__ dxd, float p_in, uint64_t seed_in,
                      float* dgamma, float* dbeta) {
-  extern __shared__ float sh_acc[];  // [2][D]
-  for (int c = threadIdx.x; c < 2 * D; c += blockDim.x) sh_acc[c] = 0.f;
-  __syncthreads();
-  const int l = threadIdx.x & 63;
-  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < M; row += gridDim.x * 4) {
+  // one wave per row; lane l owns columns l + 64j (j < kLnCols, D <= 512),
+  // so the gamma/beta gradient partials live in registers across the wave's
+  // rows and meet once per block (LDS) before one atomic per column
+  constexpr int NJ = 8;
+  __shared__ float part[4][2][NJ * 64];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float pg[NJ], pb[NJ], gm[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    pg[j] = pb[j] = 0.f;
+    const int c = l + 64 * j;
+    gm[j] = c < D ? gamma[c] : 0.f;
+  }
+  for (int row = blockIdx.x * 4 + w; row < M; row += gridDim.x * 4) {
     const T* xr = x + (size_t)row * D;
     const T* dyr = dy + (size_t)row * D;
-    float mu = mean[row], rs = rstd[row];
+    const float mu = mean[row], rs = rstd[row];
+    float g[NJ], xh[NJ];
     float a = 0.f, b = 0.f;
-    for (int c = l; c < D; c += 64) {
-      float g = to_f(dyr[c]);
-      if (p_out > 0.f) g *= drop_scale(seed_out, (uint64_t)row * D + c, p_out);
-      float xh = (to_f(xr[c]) - mu) * rs;
-      float gg = g * gamma[c];
-      a += gg; b += gg * xh;
-      atomicAdd(&sh_acc[c], g * xh);
-      atomicAdd(&sh_acc[D + c], g);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = l + 64 * j;
+      g[j] = 0.f; xh[j] = 0.f;
+      if (c < D) {
+        g[j] = to_f(dyr[c]);
+        if (p_out > 0.f) g[j] *= drop_scale(seed_out, (uint64_t)row * D + c, p_out);
+        xh[j] = (to_f(xr[c]) - mu) * rs;
+      }
+      const float gg = g[j] * gm[j];
+      a += gg;
+      b += gg * xh[j];
+      pg[j] += g[j] * xh[j];
+      pb[j] += g[j];
     }
     a = warp_sum(a) / D;
     b = warp_sum(b) / D;
-    for (int c = l; c < D; c += 64) {
-      float g = to_f(dyr[c]);
-      if (p_out > 0.f) g *= drop_scale(seed_out, (uint64_t)row * D + c, p_out);
-      float xh = (to_f(xr[c]) - mu) * rs;
-      float d = rs * (g * gamma[c] - a - xh * b);
-      dx[(size_t)row * D + c] = from_f<T>(d);
-      if (dxd) {
-        float dd = p_in > 0.f ? d * drop_scale(seed_in, (uint64_t)row * D + c, p_in) : d;
-        dxd[(size_t)row * D + c] = from_f<T>(dd);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = l + 64 * j;
+      if (c < D) {
+        const float d = rs * (g[j] * gm[j] - a - xh[j] * b);
+        dx[(size_t)row * D + c] = from_f<T>(d);
+        if (dxd) {
+          const float dd = p_in > 0.f ? d * drop_scale(seed_in, (uint64_t)row * D + c, p_in) : d;
+          dxd[(size_t)row * D + c] = from_f<T>(dd);
+        }
       }
     }
   }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    part[w][0][l + 64 * j] = pg[j];
+    part[w][1][l + 64 * j] = pb[j];
+  }
   __syncthreads();
   for (int c = threadIdx.x; c < D; c += blockDim.x) {
-    atomicAdd(dgamma + c, sh_acc[c]);
-    atomicAdd(dbeta + c, sh_acc[D + c]);
+    atomicAdd(dgamma + c, part[0][0][c] + part[1][0][c] + part[2][0][c] + part[3][0][c]);
+    atomicAdd(dbeta + c, part[0][1][c] + part[1][1][c] + part[2][1][c] + part[3][1][c]);
   }
 }
 
@@ -288,19 +310,45 @@ __global__ void embed_fwd_kernel(int M, int Tn, int D, const int64_t* __restrict
     e_out[(size_t)row * D + c] = from_f<T>(s);
   }
 }
+// word-embedding rows: scatter-add (ids are mostly distinct, low contention)
 template <typename T>
 __global__ void embed_bwd_kernel(int M, int Tn, int D, const int64_t* __restrict__ ids,
-                                 const int64_t* __restrict__ tt, const T* __restrict__ de,
-                                 float* dwemb, float* dpemb, float* dtemb) {
-  int row = blockIdx.x;
-  int t = row % Tn;
-  int64_t id = ids[row];
-  int64_t ty = tt ? tt[row] : 0;
-  for (int c = threadIdx.x; c < D; c += blockDim.x) {
-    float g = to_f(de[(size_t)row * D + c]);
-    atomicAdd(dwemb + (size_t)id * D + c, g);
-    atomicAdd(dpemb + (size_t)t * D + c, g);
-    atomicAdd(dtemb + (size_t)ty * D + c, g);
+                                 const T* __restrict__ de, float* dwemb) {
+  const int row = blockIdx.x;
+  const int64_t id = ids[row];
+  for (int c = threadIdx.x; c < D; c += blockDim.x)
+    atomicAdd(dwemb + (size_t)id * D + c, to_f(de[(size_t)row * D + c]));
+}
+// position rows (sum over the batch of each position) and token-type rows
+// (sum over all rows of each type): reductions, not 10^4-way atomic
+// contention on the same few addresses.  Block = (position t, 64 columns).
+template <typename T>
+__global__ void __launch_bounds__(256)
+embed_pt_bwd_kernel(int B, int Tn, int D, const int64_t* __restrict__ tt, const T* __restrict__ de,
+                    float* dpemb, float* dtemb) {
+  __shared__ float part[4][3][64];
+  const int t = blockIdx.x, l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + l;
+  float sp = 0.f, s0 = 0.f, s1 = 0.f;
+  if (c < D) {
+    for (int b = w; b < B; b += 4) {
+      const size_t row = (size_t)b * Tn + t;
+      const float g = to_f(de[row * D + c]);
+      sp += g;
+      const int64_t ty = tt ? tt[row] : 0;
+      s0 += ty == 0 ? g : 0.f;
+      s1 += ty == 1 ? g : 0.f;
+    }
+  }
+  part[w][0][l] = sp; part[w][1][l] = s0; part[w][2][l] = s1;
+  __syncthreads();
+  if (w == 0 && c < D) {
+    float a = 0.f, b0 = 0.f, b1 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { a += part[q][0][l]; b0 += part[q][1][l]; b1 += part[q][2][l]; }
+    atomicAdd(dpemb + (size_t)t * D + c, a);
+    atomicAdd(dtemb + c, b0);
+    if (b1 != 0.f) atomicAdd(dtemb + D + c, b1);
   }
 }
 
@@ -403,9 +451,10 @@ VLP_EXPORT int vlp_layernorm_bwd(int dtype, int M, int D, const void* dy, float 
                                  float p_in, unsigned long long seed_in, float* dgamma, float* dbeta,
                                  void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  int blocks = (M + 63) / 64;
-  if (blocks > 512) blocks = 512;
-  size_t lds = 2 * D * sizeof(float);
+  if (D > 512) return (int)hipErrorInvalidValue;
+  int blocks = (M + 15) / 16;   // 4 rows per wave
+  if (blocks > 1024) blocks = 1024;
+  size_t lds = 0;
   if (dtype == VLP_BF16)
     hipLaunchKernelGGL(layernorm_bwd_kernel<bf16>, dim3(blocks), dim3(256), lds, st, M, D,
                        (const bf16*)dy, p_out, seed_out, (const bf16*)x, mean, rstd, gamma, (bf16*)dx,
@@ -462,12 +511,19 @@ VLP_EXPORT int vlp_embed_bwd(int dtype, int M, int Tn, int D, const long long* i
                              const long long* tt, const void* de, float* dwemb, float* dpemb,
                              float* dtemb, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == VLP_BF16)
+  if (M % Tn) return (int)hipErrorInvalidValue;
+  const dim3 gpt(Tn, (D + 63) / 64);
+  if (dtype == VLP_BF16) {
     hipLaunchKernelGGL(embed_bwd_kernel<bf16>, dim3(M), dim3(128), 0, st, M, Tn, D,
-                       (const int64_t*)ids, (const int64_t*)tt, (const bf16*)de, dwemb, dpemb, dtemb);
-  else
+                       (const int64_t*)ids, (const bf16*)de, dwemb);
+    hipLaunchKernelGGL(embed_pt_bwd_kernel<bf16>, gpt, dim3(256), 0, st, M / Tn, Tn, D,
+                       (const int64_t*)tt, (const bf16*)de, dpemb, dtemb);
+  } else {
     hipLaunchKernelGGL(embed_bwd_kernel<float>, dim3(M), dim3(128), 0, st, M, Tn, D,
-                       (const int64_t*)ids, (const int64_t*)tt, (const float*)de, dwemb, dpemb, dtemb);
+                       (const int64_t*)ids, (const float*)de, dwemb);
+    hipLaunchKernelGGL(embed_pt_bwd_kernel<float>, gpt, dim3(256), 0, st, M / Tn, Tn, D,
+                       (const int64_t*)tt, (const float*)de, dpemb, dtemb);
+  }
   return (int)hipGetLastError();
 }
 

@@ -887,6 +887,178 @@ static int gemm_wgrad(int M, int N, int K, const LA& la, const LB& lb, const EP&
   return gemm_wide<T>(M, N, K, ksplit, la, lb, ep, st);
 }
 
+// ---------------- row-streaming 3x3 conv, 64 -> 64 channels (layer1) ----------------
+// The implicit GEMM re-fetches every input pixel once per filter tap (9x) and
+// its 9 K-steps per 256-row tile leave the prologue and epilogue exposed; at
+// 64 output channels that made the layer-1 convolutions the slowest GEMMs.
+// Here a workgroup owns whole images: all 9 taps of the weights are loaded
+// once (LDS, then registers) and the input streams through a 5-row ring (130 pixels x 128 B per
+// row, zero halo columns); output row i reads input rows i-1..i+1 as shifted
+// windows of the ring, so each input byte is fetched once and a row's 9 taps
+// run without barriers.  Input row i+3 is fetched while row i is computed.
+//   waves: 8, each 32 output pixels x 32 channels (MFMA 16x16x32, B = weights)
+// Requirements: C = Co = 64, 3x3, stride 1, pad 1, W = 128, bf16.
+constexpr int kRcW = 128;                        // image width handled
+constexpr int kRcSlot = (kRcW + 2) * 128;        // one ring row (bytes)
+constexpr int kRcWeights = 9 * 64 * 128;         // 73728
+constexpr int kRcRing = 5;
+constexpr int kRcLds = kRcWeights + kRcRing * kRcSlot + 2048;
+
+template <class EP>
+__global__ void __launch_bounds__(512)
+conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __restrict__ w, int flip,
+                        EP ep, int M) {
+  // 8 waves: wave w computes pixels 32*(w&3) .. +31 and channels 32*(w>>2) .. +31
+  // of each output row; its 9 taps x 2 k-substeps x 2 column blocks of filter
+  // fragments (144 VGPRs) stay in registers, so the row loop reads only the
+  // input ring (4 ds_read_b128 per tap) and two waves share each SIMD.
+  constexpr int S = 4;                             // global stores per lane per output row
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* wlds = smem;
+  char* ring = smem + kRcWeights;
+  float* red = reinterpret_cast<float*>(smem + kRcWeights + kRcRing * kRcSlot);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
+  const int pq = wv & 3, ch = wv >> 2;
+  const rsrc_t rx = buf_rsrc(x, (unsigned)((size_t)N * H * kRcW * 64 * 2));
+  const rsrc_t rw = buf_rsrc(w, 64 * 576 * 2);
+  const rsrc_t rz = null_rsrc(zero_page());
+
+  // weights: tap block t (or 8 - t: the flipped filter of a data gradient),
+  // [64 rows][8 chunks] XOR-swizzled like a K-contig GEMM image
+  for (int j = wv; j < 72; j += 8) {
+    const int b = j >> 3, q = (j & 7) * 64 + lane;
+    const int r = q >> 3, c = (q & 7) ^ ((r >> 1) & 7);
+    const int tb = flip ? 8 - b : b;
+    dma16(rw, (unsigned)((r * 576 + tb * 64 + c * 8) * 2), wlds + j * 1024);
+  }
+  // zero halo columns (ring rows 0 and 129 of every slot)
+  for (int q = tid; q < kRcRing * 2 * 8; q += 512) {
+    const int sl = q >> 4, side = (q >> 3) & 1, c = q & 7;
+    *reinterpret_cast<uint4*>(ring + sl * kRcSlot + (side ? (kRcW + 1) * 128 : 0) + c * 16) = zero4();
+  }
+  // input row i of image n -> ring slot (i + 1) % 5, pixels at ring rows 1..128
+  auto fetch = [&](int n, int i) {
+    char* slot = ring + ((i + 1) % kRcRing) * kRcSlot + 128;
+    const bool live = (unsigned)i < (unsigned)H;
+    const rsrc_t r = live ? rx : rz;
+    const unsigned base = live ? (unsigned)(((size_t)n * H + i) * kRcW * 128) : 0u;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = wv * 2 + jj;
+      const int q = j * 64 + lane;
+      const int px = q >> 3, c = (q & 7) ^ (((px + 1) >> 1) & 7);
+      dma16(r, base + (unsigned)(px * 128 + c * 16), slot + j * 1024);
+    }
+  };
+  v4f s1[2], s2[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) s1[b] = s2[b] = v4f{0.f, 0.f, 0.f, 0.f};
+  const int li = lane & 15, lg = lane >> 4;
+  wait_vmcnt<0>();
+  __syncthreads();
+  v8bf wf[9][2][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) wf[t][s][b] = frag_bf16<true, 128, true>(wlds + t * 8192, ch * 32 + b * 16, s);
+
+  for (int n = blockIdx.x; n < N; n += gridDim.x) {
+    wait_vmcnt<0>();
+    __syncthreads();
+    fetch(n, -1); fetch(n, 0); fetch(n, 1); fetch(n, 2);
+    for (int i = 0; i < H; ++i) {
+      if (i == 0) wait_vmcnt<2>();              // rows -1..1 landed (row 2 in flight)
+      else if (i == 1) wait_vmcnt<2 + S>();     // row 2 (row 3, row-0 stores in flight)
+      else wait_vmcnt<2 + 2 * S>();             // row i+1 (rows i+2, stores of i-2, i-1)
+      raw_barrier();                            // all waves: ring rows landed, row i-1 done
+      fetch(n, i + 3);
+      v4f acc[2][2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const char* sl = ring + ((i + kh) % kRcRing) * kRcSlot;   // input row i - 1 + kh
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          v8bf fa[2][2];
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int a = 0; a < 2; ++a) fa[s][a] = frag_bf16<true, 128, true>(sl, pq * 32 + a * 16 + kw, s);
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+              for (int b = 0; b < 2; ++b)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kh * 3 + kw][s][b], fa[s][a], acc[a][b], 0, 0, 0);
+        }
+      }
+      // epilogue: lane (li, lg) owns pixel 32pq + 16a + li, channels 32ch + 16b + 4lg .. +3
+      const int rowbase = (n * H + i) * kRcW + pq * 32;
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          v4f c1 = v4f{0.f, 0.f, 0.f, 0.f}, c2 = c1;
+          ep(rowbase + a * 16 + li, ch * 32 + b * 16 + 4 * lg, acc[a][b], c1, c2);
+          if constexpr (EP::kStats) { s1[b] += c1; s2[b] += c2; }
+        }
+    }
+  }
+  if constexpr (EP::kStats) {
+    // per-column sums: rows of each 16-lane group, then the 4 pixel-quarter
+    // waves, then one fp64 atomic per column into replica blockIdx % stat_rep
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float xs = row16_sum(s1[b][j]), ys = row16_sum(s2[b][j]);
+        if (li == 15) {
+          const int co = ch * 32 + b * 16 + 4 * lg + j;
+          red[(pq * 64 + co) * 2 + 0] = xs;
+          red[(pq * 64 + co) * 2 + 1] = ys;
+        }
+      }
+    __syncthreads();
+    if (tid < 64) {
+      float xs = 0.f, ys = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { xs += red[(q * 64 + tid) * 2]; ys += red[(q * 64 + tid) * 2 + 1]; }
+      const int rep = ep.stat_rep > 1 ? (int)(blockIdx.x % ep.stat_rep) : 0;
+      atomicAdd(ep.stat1 + (size_t)rep * 64 + tid, (double)xs);
+      atomicAdd(ep.stat2 + (size_t)rep * 64 + tid, (double)ys);
+    }
+  }
+  (void)M;
+}
+
+static bool rows_c64_ok(const ConvGeom& g) {
+  static const int off = getenv("VLP_NO_ROWCONV") ? atoi(getenv("VLP_NO_ROWCONV")) : 0;
+  return !off && g.C == 64 && g.Co == 64 && g.KH == 3 && g.KW == 3 && g.S == 1 && g.P == 1 && g.W == kRcW &&
+         g.H >= 3 && (size_t)g.N * g.H * kRcW * 128 < (1ull << 31);
+}
+template <class EP>
+static int launch_rows_c64(const ConvGeom& g, const void* x, const void* w, int flip, const EP& ep,
+                           hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)&conv3x3_c64_rows_kernel<EP>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, kRcLds);
+    attr = true;
+  }
+  int grid = device_cus();
+  if (grid > g.N) grid = g.N;
+  hipLaunchKernelGGL((conv3x3_c64_rows_kernel<EP>), dim3(grid), dim3(512), kRcLds, st, g.N, g.H,
+                     (const bf16*)x, (const bf16*)w, flip, ep, g.N * g.H * g.W);
+  return (int)hipGetLastError();
+}
+
 template <typename T>
 static int conv_fwd_t(const void* x, const void* wp, void* y, ConvGeom g, const float* sc,
                       const float* sh, double* s1, double* s2, int rep, hipStream_t st) {
@@ -897,6 +1069,9 @@ static int conv_fwd_t(const void* x, const void* wp, void* y, ConvGeom g, const 
   if (sc) {
     ConvFwdA<T, true> la{g, (const T*)x, sc, sh};
     return gemm_auto<T>(g.M, g.Co, g.K, 1, la, lb, ep, st);
+  }
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (rows_c64_ok(g)) return launch_rows_c64(g, x, wp, 0, ep, st);
   }
   ConvFwdA<T, false> la{g, (const T*)x, nullptr, nullptr};
   return gemm_auto<T>(g.M, g.Co, g.K, 1, la, lb, ep, st);
@@ -933,11 +1108,19 @@ static int conv_dgrad_t(const void* dy, const void* wt, void* dx, ConvGeom g, co
   }
   ConvDgradA<T> la{g, (const T*)dy};
   KMat<T> lb{(const T*)wt, g.K, g.C, g.K};
+  // stride-1 dgrad = forward conv of dy with the flipped, transposed filter
+  const bool rows = std::is_same<T, bf16>::value && rows_c64_ok(g);
   if (ybn) {
     EpiDgradBN<T> ep{s1, s2, rep, (T*)dx, g.C, (const T*)ybn, sc, sh, mean, invstd};
+    if constexpr (std::is_same<T, bf16>::value) {
+      if (rows) return launch_rows_c64(g, dy, wt, 1, ep, st);
+    }
     return gemm_auto<T>(g.M, g.C, g.K, 1, la, lb, ep, st);
   }
   EpiDgradAdd<T> ep{nullptr, nullptr, (T*)dx, (const T*)addend, g.C};
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (rows) return launch_rows_c64(g, dy, wt, 1, ep, st);
+  }
   return gemm_auto<T>(g.M, g.C, g.K, 1, la, lb, ep, st);
 }
 
@@ -963,6 +1146,9 @@ static int conv_dgrad_relu_t(const void* dy, const void* wt, void* gout, ConvGeo
         if (r) return r;
       }
     return 0;
+  }
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (rows_c64_ok(g)) return launch_rows_c64(g, dy, wt, 1, in, st);
   }
   ConvDgradA<T> la{g, (const T*)dy};
   KMat<T> lb{(const T*)wt, g.K, g.C, g.K};

@@ -1372,6 +1372,7 @@ template <typename T, class LA, class LB, class EP>
 inline int gemm_narrow(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
                        hipStream_t st) {
   if constexpr (use_bk<T, LA, LB>()) {
+    if (gemm_variant() >= 6 && M >= 512) return launch_gemm_big<512, 64, 8, 1>(M, N, K, ksplit, la, lb, ep, st);
     if (gemm_variant() >= 4) return launch_gemm_bk<256, 64, 4, 1>(M, N, K, ksplit, la, lb, ep, st);
   }
   if constexpr (use_ms<T, LA, LB>()) {
