@@ -54,6 +54,7 @@ CONV_CASES = [
     (2, 12, 12, 64, 128, 1, 1, 2, 0),
     (3, 7, 9, 128, 64, 3, 3, 1, 1),
     (3, 5, 128, 64, 64, 3, 3, 1, 1),    # layer-1 width: row-streaming kernel (bf16)
+    (2, 12, 12, 256, 256, 3, 3, 1, 1),  # M, N >= 256: 256x256 large-tile kernel (bf16)
 ]
 
 

@@ -340,8 +340,10 @@ struct EpiS2Remap {
   __device__ v4f value(int row, int col, v4f v, v4f& s1, v4f& s2) const {
     return inner.value(grow(row), col, v, s1, s2);
   }
-  __device__ void row8(int row, int col, const float (&v)[8], float (&s1)[8], float (&s2)[8]) const {
-    inner.row8(grow(row), col, v, s1, s2);
+  __device__ void pre8(int row, int col, RowPre& p) const { inner.pre8(grow(row), col, p); }
+  __device__ void row8(int row, int col, const float (&v)[8], const RowPre& p, float (&s1)[8],
+                       float (&s2)[8]) const {
+    inner.row8(grow(row), col, v, p, s1, s2);
   }
   __device__ void store8(int row, int col, const uint4& u) const { inner.store8(grow(row), col, u); }
 };
@@ -699,6 +701,17 @@ static PixStep make_stem_pixstep(const StemGeom& g, int BK) {
   return p;
 }
 
+typedef const __attribute__((address_space(3))) float* lds_fp;
+template <class E, class = void> struct CoefTrait { static constexpr int value = 0; };
+template <class E> struct CoefTrait<E, std::void_t<decltype(E::kCoefs)>> { static constexpr int value = E::kCoefs; };
+
+// 8 consecutive per-channel coefficients as two 16-B loads
+__device__ __forceinline__ void ld8f(const float* p, float (&o)[8]) {
+  const v4f a = *reinterpret_cast<const v4f*>(p), b = *reinterpret_cast<const v4f*>(p + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { o[j] = a[j]; o[4 + j] = b[j]; }
+}
+
 // ---------------- epilogues ----------------
 // raw conv output + BN batch statistics (sum, sum of squares)
 template <typename T>
@@ -742,15 +755,39 @@ struct EpiDgradBN {
     s2 = g * ((yv - mu) * is);
   }
   static constexpr bool kRow = true;
-  __device__ void row8(int row, int col, const float (&v)[8], float (&s1)[8], float (&s2)[8]) const {
+  __device__ void pre8(int row, int col, RowPre& p) const { p.u[0] = ldg16(y + (size_t)row * C + col); }
+  // per-channel coefficient arrays (a caller may stage them in LDS: row8 with lds_fp)
+  static constexpr int kCoefs = 4;
+  __device__ const float* coef(int k) const { return k == 0 ? sc : k == 1 ? sh : k == 2 ? mean : invstd; }
+  __device__ void row8(int row, int col, const float (&v)[8], const RowPre& p, float (&s1)[8],
+                       float (&s2)[8]) const {
+    row8c(row, col, v, p, s1, s2, sc, sh, mean, invstd);
+  }
+  __device__ void row8(int row, int col, const float (&v)[8], const RowPre& p, float (&s1)[8],
+                       float (&s2)[8], lds_fp cf) const {
+    row8c(row, col, v, p, s1, s2, cf, cf + 64, cf + 128, cf + 192);
+  }
+  template <class FP>
+  __device__ void row8c(int row, int col, const float (&v)[8], const RowPre& p, float (&s1)[8],
+                        float (&s2)[8], FP csc, FP csh, FP cmu, FP cis) const {
     const size_t o = (size_t)row * C + col;
     float yv[8], g[8];
-    Chunk<bf16>::unpack(ldg16(y + o), yv);
+    Chunk<bf16>::unpack(p.u[0], yv);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      g[j] = fmaf(yv[j], sc[col + j], sh[col + j]) > 0.f ? v[j] : 0.f;
-      s1[j] += g[j];
-      s2[j] += g[j] * ((yv[j] - mean[col + j]) * invstd[col + j]);
+    for (int h = 0; h < 2; ++h) {   // 4 channels at a time: 16 coefficient registers live, not 32
+      v4f a, b, mu, is;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        a[jj] = csc[col + 4 * h + jj]; b[jj] = csh[col + 4 * h + jj];
+        mu[jj] = cmu[col + 4 * h + jj]; is[jj] = cis[col + 4 * h + jj];
+      }
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        const int j = 4 * h + jj;
+        g[j] = fmaf(yv[j], a[jj], b[jj]) > 0.f ? v[j] : 0.f;
+        s1[j] += g[j];
+        s2[j] += g[j] * ((yv[j] - mu[jj]) * is[jj]);
+      }
     }
     stg16(g_out + o, Chunk<bf16>::pack(g));
   }
@@ -782,14 +819,17 @@ struct EpiDgradAdd {
     store4(dx + o, v);
   }
   static constexpr bool kRow = true;
-  __device__ void row8(int row, int col, const float (&v)[8], float (&)[8], float (&)[8]) const {
+  __device__ void pre8(int row, int col, RowPre& p) const {
+    if (addend) p.u[0] = ldg16(addend + (size_t)row * C + col);
+  }
+  __device__ void row8(int row, int col, const float (&v)[8], const RowPre& p, float (&)[8], float (&)[8]) const {
     const size_t o = (size_t)row * C + col;
     float d[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) d[j] = v[j];
     if (addend) {
       float a[8];
-      Chunk<bf16>::unpack(ldg16(addend + o), a);
+      Chunk<bf16>::unpack(p.u[0], a);
 #pragma unroll
       for (int j = 0; j < 8; ++j) d[j] += a[j];
     }
@@ -832,21 +872,37 @@ struct EpiDgradRelu {
     store4(g_out + (size_t)row * C + col, grad(row, col, v, s1, s2));
   }
   static constexpr bool kRow = true;
-  __device__ void row8(int row, int col, const float (&v)[8], float (&s1)[8], float (&s2)[8]) const {
+  __device__ void pre8(int row, int col, RowPre& p) const {
     const size_t o = (size_t)row * C + col;
-    float a[8], r[8], yv[8], g[8];
-    if (addend) Chunk<bf16>::unpack(ldg16(addend + o), a);
-    else {
+    p.u[0] = addend ? ldg16(addend + o) : zero4();
+    p.u[1] = ldg16(relu_out + o);
+    p.u[2] = ldg16(y + o);
+  }
+  static constexpr int kCoefs = 2;
+  __device__ const float* coef(int k) const { return k == 0 ? mean : invstd; }
+  __device__ void row8(int row, int col, const float (&v)[8], const RowPre& p, float (&s1)[8],
+                       float (&s2)[8]) const {
+    row8c(row, col, v, p, s1, s2, mean, invstd);
+  }
+  __device__ void row8(int row, int col, const float (&v)[8], const RowPre& p, float (&s1)[8],
+                       float (&s2)[8], lds_fp cf) const {
+    row8c(row, col, v, p, s1, s2, cf, cf + 64);
+  }
+  template <class FP>
+  __device__ void row8c(int row, int col, const float (&v)[8], const RowPre& p, float (&s1)[8],
+                        float (&s2)[8], FP cmu, FP cis) const {
+    const size_t o = (size_t)row * C + col;
+    float a[8], r[8], yv[8], g[8], mu[8], is[8];
+    Chunk<bf16>::unpack(p.u[0], a);
+    Chunk<bf16>::unpack(p.u[1], r);
+    Chunk<bf16>::unpack(p.u[2], yv);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) a[j] = 0.f;
-    }
-    Chunk<bf16>::unpack(ldg16(relu_out + o), r);
-    Chunk<bf16>::unpack(ldg16(y + o), yv);
+    for (int j = 0; j < 8; ++j) { mu[j] = cmu[col + j]; is[j] = cis[col + j]; }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       g[j] = r[j] > 0.f ? v[j] + a[j] : 0.f;
       s1[j] += g[j];
-      s2[j] += g[j] * ((yv[j] - mean[col + j]) * invstd[col + j]);
+      s2[j] += g[j] * ((yv[j] - mu[j]) * is[j]);
     }
     stg16(g_out + o, Chunk<bf16>::pack(g));
   }
@@ -912,11 +968,13 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
   // of each output row; its 9 taps x 2 k-substeps x 2 column blocks of filter
   // fragments (144 VGPRs) stay in registers, so the row loop reads only the
   // input ring (4 ds_read_b128 per tap) and two waves share each SIMD.
-  constexpr int S = 4;                             // global stores per lane per output row
+  constexpr int S = RowTrait<EP>::value ? 2 : 4;  // global stores per lane per output row
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* wlds = smem;
   char* ring = smem + kRcWeights;
-  float* red = reinterpret_cast<float*>(smem + kRcWeights + kRcRing * kRcSlot);
+  // stats scratch: 2 KB after the ring (direct mode) or the filter area past
+  // the 16 KB staging tile (row-chunk mode, 32 KB, used after the last row)
+  float* red = reinterpret_cast<float*>(RowTrait<EP>::value ? smem + 16384 : smem + kRcWeights + kRcRing * kRcSlot);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
   const int pq = wv & 3, ch = wv >> 2;
@@ -964,6 +1022,19 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int b = 0; b < 2; ++b) wf[t][s][b] = frag_bf16<true, 128, true>(wlds + t * 8192, ch * 32 + b * 16, s);
+  if constexpr (RowTrait<EP>::value && EP::kStats) {
+    __syncthreads();   // every wave holds its filter fragments before the area is reused
+    v4f* rp = reinterpret_cast<v4f*>(red + tid * 16);
+    rp[0] = rp[1] = rp[2] = rp[3] = v4f{0.f, 0.f, 0.f, 0.f};
+  }
+  // the epilogue's per-channel coefficients (64 floats each) staged in LDS: read
+  // per row with ds_read instead of held in (or reloaded into) VGPRs
+  constexpr int NCF = CoefTrait<EP>::value;
+  float* cfl = reinterpret_cast<float*>(smem + kRcWeights + kRcRing * kRcSlot);
+  if constexpr (NCF > 0) {
+    for (int q = tid; q < NCF * 64; q += 512) cfl[q] = ep.coef(q >> 6)[q & 63];
+    __syncthreads();
+  }
 
   for (int n = blockIdx.x; n < N; n += gridDim.x) {
     wait_vmcnt<0>();
@@ -975,6 +1046,12 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
       else wait_vmcnt<2 + 2 * S>();             // row i+1 (rows i+2, stores of i-2, i-1)
       raw_barrier();                            // all waves: ring rows landed, row i-1 done
       fetch(n, i + 3);
+      // epilogue operands of this row: issued now, consumed after the MFMAs
+      RowPre pre[2];
+      if constexpr (RowTrait<EP>::value) {
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) ep.pre8((n * H + i) * kRcW + (tid >> 3) + 64 * h2, (tid & 7) * 8, pre[h2]);
+      }
       v4f acc[2][2];
 #pragma unroll
       for (int a = 0; a < 2; ++a)
@@ -999,19 +1076,68 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
                 acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[kh * 3 + kw][s][b], fa[s][a], acc[a][b], 0, 0, 0);
         }
       }
-      // epilogue: lane (li, lg) owns pixel 32pq + 16a + li, channels 32ch + 16b + 4lg .. +3
-      const int rowbase = (n * H + i) * kRcW + pq * 32;
+      if constexpr (RowTrait<EP>::value) {
+        // row-chunk epilogue through the (now free) filter staging area: the
+        // output row is staged as bf16, then thread t handles pixels t/8 and
+        // t/8 + 64 at the FIXED 8-channel group t%8, so its operand loads and
+        // stores are row-contiguous 16-B chunks
+        bf16* stg = reinterpret_cast<bf16*>(wlds);
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < 2; ++b)
 #pragma unroll
-        for (int a = 0; a < 2; ++a) {
-          v4f c1 = v4f{0.f, 0.f, 0.f, 0.f}, c2 = c1;
-          ep(rowbase + a * 16 + li, ch * 32 + b * 16 + 4 * lg, acc[a][b], c1, c2);
-          if constexpr (EP::kStats) { s1[b] += c1; s2[b] += c2; }
+          for (int a = 0; a < 2; ++a) {
+            const int px = pq * 32 + a * 16 + li, co = ch * 32 + b * 16 + 4 * lg;
+            v4bf ob;
+            ob[0] = (bf16)acc[a][b][0]; ob[1] = (bf16)acc[a][b][1];
+            ob[2] = (bf16)acc[a][b][2]; ob[3] = (bf16)acc[a][b][3];
+            *reinterpret_cast<v4bf*>(stg + px * 64 + (((co >> 3) ^ (px & 7)) << 3) + (co & 4)) = ob;
+          }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        raw_barrier();
+        const int rowbase = (n * H + i) * kRcW;
+        float r1[8], r2[8];   // this row's sums of the thread's 8 channels
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r1[j] = r2[j] = 0.f;
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const int px = (tid >> 3) + 64 * h2, c = tid & 7;
+          float v[8];
+          Chunk<bf16>::unpack(*reinterpret_cast<const uint4*>(stg + px * 64 + ((c ^ (px & 7)) << 3)), v);
+          if constexpr (NCF > 0) ep.row8(rowbase + px, c * 8, v, pre[h2], r1, r2, (lds_fp)cfl);
+          else ep.row8(rowbase + px, c * 8, v, pre[h2], r1, r2);
         }
+        if constexpr (EP::kStats) {   // running sums live in LDS (thread-private slots), not VGPRs
+          v4f* rp = reinterpret_cast<v4f*>(red + tid * 16);
+          v4f q0 = rp[0], q1 = rp[1], q2 = rp[2], q3 = rp[3];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { q0[j] += r1[j]; q1[j] += r1[4 + j]; q2[j] += r2[j]; q3[j] += r2[4 + j]; }
+          rp[0] = q0; rp[1] = q1; rp[2] = q2; rp[3] = q3;
+        }
+      } else {
+        // direct epilogue: lane (li, lg) owns pixel 32pq + 16a + li, channels 32ch + 16b + 4lg .. +3
+        const int rowbase = (n * H + i) * kRcW + pq * 32;
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int a = 0; a < 2; ++a) {
+            v4f c1 = v4f{0.f, 0.f, 0.f, 0.f}, c2 = c1;
+            ep(rowbase + a * 16 + li, ch * 32 + b * 16 + 4 * lg, acc[a][b], c1, c2);
+            if constexpr (EP::kStats) { s1[b] += c1; s2[b] += c2; }
+          }
+      }
     }
   }
-  if constexpr (EP::kStats) {
+  if constexpr (EP::kStats && RowTrait<EP>::value) {
+    // per-column sums: thread t holds columns 8*(t%8) .. +7 -> 64 threads per group
+    __syncthreads();
+    if (tid < 128) {
+      const int co = tid >> 1, stt = tid & 1;
+      float xs = 0.f;
+      for (int k = co >> 3; k < 512; k += 8) xs += red[k * 16 + stt * 8 + (co & 7)];
+      const int rep = ep.stat_rep > 1 ? (int)(blockIdx.x % ep.stat_rep) : 0;
+      atomicAdd((stt ? ep.stat2 : ep.stat1) + (size_t)rep * 64 + co, (double)xs);
+    }
+  } else if constexpr (EP::kStats) {
     // per-column sums: rows of each 16-lane group, then the 4 pixel-quarter
     // waves, then one fp64 atomic per column into replica blockIdx % stat_rep
 #pragma unroll

@@ -164,6 +164,8 @@ template <class E, class = void> struct StageTrait { static constexpr bool value
 template <class E> struct StageTrait<E, std::void_t<decltype(E::kStage)>> {
   static constexpr bool value = E::kStage;
 };
+// operands a row-chunk epilogue fetches ahead of its row8() call (16-B chunks)
+struct RowPre { uint4 u[3]; };
 template <class E, class = void> struct RowTrait { static constexpr bool value = false; };
 template <class E> struct RowTrait<E, std::void_t<decltype(E::kRow)>> {
   static constexpr bool value = E::kRow;
@@ -585,7 +587,9 @@ __device__ __forceinline__ void ms_epilogue(const GemmShape& sh, const EP& ep, v
       if (row < sh.M && col < sh.N) {
         float v[8];
         Chunk<bf16>::unpack(*reinterpret_cast<const uint4*>(stg + r * BN + ((c ^ (r & (CPR - 1))) << 3)), v);
-        ep.row8(row, col, v, s1, s2);
+        RowPre pre;
+        ep.pre8(row, col, pre);
+        ep.row8(row, col, v, pre, s1, s2);
       }
     }
     if constexpr (EP::kStats) {
