@@ -151,6 +151,10 @@ int vlp_linear_dgrad(int dtype, int M, int Kin, int Nout, const void* dy, int ld
 /* dw[Nout][Kin] += dy^T x (fp32 atomics; zero first) */
 int vlp_linear_wgrad(int dtype, int M, int Nout, int Kin, const void* dy, int lddy, const void* x,
                      int ldx, float* dw, void* stream);
+/* the same through a split-K workspace ws[ks][Nout][Kin] fp32 (bf16 only, Kin % 4 == 0):
+ * split partials are plain stores, then one pass folds them into dw (no atomics) */
+int vlp_linear_wgrad_ws(int dtype, int M, int Nout, int Kin, const void* dy, int lddy, const void* x,
+                        int ldx, float* dw, float* ws, long long ws_elems, void* stream);
 /* out[n] += sum_m x[m][n] (bias gradients; fp32 atomics) */
 int vlp_colsum(int dtype, int M, int N, const void* x, int ld, float* out, void* stream);
 int vlp_layernorm_fwd(int dtype, int M, int D, const void* x, const float* gamma,

@@ -267,3 +267,19 @@ def test_bn_bwd_apply_transposed(ops, has_b, bcast, C):
     assert torch.equal(ta, a1.t())
     if has_b:
         assert torch.equal(b0, b1) and torch.equal(tb, b1.t())
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("shape", [(640, 936, 312), (300, 312, 1200), (1100, 312, 312)])
+def test_linear_wgrad(ops, dt, shape):
+    """dW += dy^T x (TinyBERT weight gradients): fp32 atomic split-K and the bf16
+    split-K workspace path (vlp_linear_wgrad_ws) against fp32 math."""
+    M, Nout, Kin = shape
+    torch.manual_seed(6)
+    dy = torch.randn(M, Nout).to(dt).float()
+    x = torch.randn(M, Kin).to(dt).float()
+    ref = dy.t() @ x + 0.5
+    dw = torch.full((Nout, Kin), 0.5, device="cuda")
+    ops.linear_wgrad(dy.to(dt).cuda(), x.to(dt).cuda(), dw, M, Nout, Kin)
+    torch.cuda.synchronize()
+    assert rel(dw, ref) < tol(dt) / 4

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--layers", default="l1,l2,l3,l4")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--gemm", action="store_true")
+    ap.add_argument("--text", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
@@ -93,6 +94,25 @@ def main():
             us = e0.elapsed_time(e1) * 1e3 / args.iters
             res[name] = {"us": round(us, 1), "tflops": round(flop / us / 1e6, 1)}
             print(f"{name:9s}: {us:9.1f} us  {flop / us / 1e6:7.1f} TF/s", flush=True)
+    if args.text:
+        # TinyBERT weight gradients: dW[Nout][Kin] = dy^T x over M = B*T tokens
+        for (M, Nout, Kin) in [(10240, 936, 312), (10240, 1200, 312), (10240, 312, 1200), (10240, 312, 312)]:
+            dyb = (torch.randn(M, Nout, device=dev) * 0.1).to(torch.bfloat16)
+            xb = (torch.randn(M, Kin, device=dev) * 0.1).to(torch.bfloat16)
+            dw = torch.zeros(Nout, Kin, device=dev)
+            fn = lambda: ops.linear_wgrad(dyb, xb, dw, M, Nout, Kin)  # noqa: E731
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.iters):
+                fn()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / args.iters
+            flop = 2.0 * M * Nout * Kin
+            print(f"linw {Nout}x{Kin}: {us:9.1f} us  {flop / us / 1e6:7.1f} TF/s", flush=True)
     print(json.dumps(res))
 
 

@@ -69,6 +69,34 @@ struct EpiLinearBwd {
   }
 };
 
+// split-K partial of a weight gradient: split s writes slab s of ws[ks][Nout][Kin]
+// with plain stores (the fp32 atomics of 10+ splits onto the same small dW
+// were the bound: ~50 G atomics/s); linw_reduce_kernel folds the slabs
+struct EpiSplitStore {
+  static constexpr bool kStats = false;
+  static constexpr bool kSplitOut = true;
+  double* stat1 = nullptr; double* stat2 = nullptr;
+  float* out; int ldo; size_t slab;
+  __device__ EpiSplitStore at_split(int s) const {
+    EpiSplitStore e = *this;
+    e.out += (size_t)s * slab;
+    return e;
+  }
+  __device__ void operator()(int row, int col, v4f v, v4f&, v4f&) const {
+    *reinterpret_cast<v4f*>(out + (size_t)row * ldo + col) = v;
+  }
+};
+__global__ void linw_reduce_kernel(size_t n4, int ks, const float4* __restrict__ ws, float4* __restrict__ dw) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    float4 a = dw[i];
+    for (int s = 0; s < ks; ++s) {
+      const float4 b = ws[(size_t)s * n4 + i];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    dw[i] = a;
+  }
+}
+
 template <typename T, class LA, class LB, class EP>
 static int gemm_lin(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
                     hipStream_t st) {
@@ -404,9 +432,10 @@ VLP_EXPORT int vlp_linear_wgrad(int dtype, int M, int Nout, int Kin, const void*
                                 const void* x, int ldx, float* dw, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   // each split reduces >= 1024 token rows (short splits were prologue/atomic bound)
+  static const int rows_per_split = getenv("VLP_LINW_ROWS") ? atoi(getenv("VLP_LINW_ROWS")) : 1024;
   int tiles = ((Nout + 127) / 128) * ((Kin + 127) / 128);
   int ksplit = (512 + tiles - 1) / tiles;
-  int maxsplit = (M + 1023) / 1024;
+  int maxsplit = (M + rows_per_split - 1) / rows_per_split;
   if (ksplit > maxsplit) ksplit = maxsplit;
   EpiAtomic ep{nullptr, nullptr, dw, Kin, 1.0f};
   if (dtype == VLP_BF16) {
@@ -417,6 +446,33 @@ VLP_EXPORT int vlp_linear_wgrad(int dtype, int M, int Nout, int Kin, const void*
   MNMat<float> la{(const float*)dy, lddy, Nout, M};
   MNMat<float> lb{(const float*)x, ldx, Kin, M};
   return launch_gemm<float, 128, 128, 2>(Nout, Kin, M, ksplit, la, lb, ep, st);
+}
+
+// dW[Nout][Kin] += sum_m dy[m][n] x[m][k] through a split-K workspace
+// ws[ks][Nout][Kin] fp32 (ws_elems >= ks * Nout * Kin; Kin % 4 == 0)
+VLP_EXPORT int vlp_linear_wgrad_ws(int dtype, int M, int Nout, int Kin, const void* dy, int lddy,
+                                   const void* x, int ldx, float* dw, float* ws, long long ws_elems,
+                                   void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype != VLP_BF16 || Kin % 4 || !ws) return (int)hipErrorInvalidValue;
+  const int tiles = ((Nout + 127) / 128) * ((Kin + 127) / 128);
+  int ks = (512 + tiles - 1) / tiles;
+  const int maxsplit = (M + 255) / 256;
+  if (ks > maxsplit) ks = maxsplit;
+  while (ks > 1 && (long long)ks * Nout * Kin > ws_elems) --ks;
+  int kc = (M + ks - 1) / ks;
+  kc = (kc + 63) / 64 * 64;
+  ks = (M + kc - 1) / kc;
+  MNMat<bf16> la{(const bf16*)dy, lddy, Nout, M};
+  MNMat<bf16> lb{(const bf16*)x, ldx, Kin, M};
+  EpiSplitStore ep{nullptr, nullptr, ws, Kin, (size_t)Nout * Kin};
+  int r = launch_gemm_bk<128, 128, 2, 2>(Nout, Kin, M, ks, la, lb, ep, st);
+  if (r) return r;
+  const size_t n4 = (size_t)Nout * Kin / 4;
+  int blocks = (int)((n4 + 255) / 256);
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(linw_reduce_kernel, dim3(blocks), dim3(256), 0, st, n4, ks, (const float4*)ws, (float4*)dw);
+  return (int)hipGetLastError();
 }
 
 VLP_EXPORT int vlp_colsum(int dtype, int M, int N, const void* x, int ld, float* out, void* stream) {

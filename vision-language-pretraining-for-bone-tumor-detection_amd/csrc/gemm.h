@@ -166,6 +166,12 @@ template <class E> struct StageTrait<E, std::void_t<decltype(E::kStage)>> {
 };
 // operands a row-chunk epilogue fetches ahead of its row8() call (16-B chunks)
 struct RowPre { uint4 u[3]; };
+// split-K epilogues that write their own partial slab (no atomics): the kernel
+// hands the epilogue its split index via at_split(split)
+template <class E, class = void> struct SplitTrait { static constexpr bool value = false; };
+template <class E> struct SplitTrait<E, std::void_t<decltype(E::kSplitOut)>> {
+  static constexpr bool value = E::kSplitOut;
+};
 template <class E, class = void> struct RowTrait { static constexpr bool value = false; };
 template <class E> struct RowTrait<E, std::void_t<decltype(E::kRow)>> {
   static constexpr bool value = E::kRow;
@@ -582,15 +588,21 @@ __device__ __forceinline__ void ms_epilogue(const GemmShape& sh, const EP& ep, v
     float s1[8], s2[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
-    for (int r = threadIdx.x / CPR; r < BM; r += NT / CPR) {
+    // operands of the next row chunk are fetched while this one is finished
+    constexpr int RS = NT / CPR;
+    int r = threadIdx.x / CPR;
+    RowPre cur;
+    if (row0 + r < sh.M && col < sh.N) ep.pre8(row0 + r, col, cur);
+    for (; r < BM; r += RS) {
       const int row = row0 + r;
+      RowPre nxt;
+      if (r + RS < BM && row + RS < sh.M && col < sh.N) ep.pre8(row + RS, col, nxt);
       if (row < sh.M && col < sh.N) {
         float v[8];
         Chunk<bf16>::unpack(*reinterpret_cast<const uint4*>(stg + r * BN + ((c ^ (r & (CPR - 1))) << 3)), v);
-        RowPre pre;
-        ep.pre8(row, col, pre);
-        ep.row8(row, col, v, pre, s1, s2);
+        ep.row8(row, col, v, cur, s1, s2);
       }
+      cur = nxt;
     }
     if constexpr (EP::kStats) {
       __syncthreads();
@@ -985,7 +997,11 @@ gemm_bk_kernel(GemmShape sh, LA la, LB lb, EP ep) {
     body(std::integral_constant<int, 1>{}, t + 1);
   }
   __syncthreads();   // ring drained (incl. the null-resource tail fetch) before LDS is reused
-  ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep, acc, row0, col0, wid, wm, wn, smem);
+  if constexpr (SplitTrait<EP>::value) {
+    ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep.at_split(split), acc, row0, col0, wid, wm, wn, smem);
+  } else {
+    ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep, acc, row0, col0, wid, wm, wn, smem);
+  }
 }
 
 // ---------------- 8-wave large-tile kernel (bf16) ----------------

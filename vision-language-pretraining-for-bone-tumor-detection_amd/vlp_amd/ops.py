@@ -218,10 +218,28 @@ def linear_dgrad(dy, w, dx, M, Kin, Nout, lddy=None, lddx=None, mode=0, aux=None
     ktimer.end(tk)
 
 
+_LINW_WS = {}
+
+
+def _linw_ws(device, elems):
+    buf = _LINW_WS.get(device)
+    if buf is None or buf.numel() < elems:
+        buf = torch.empty(elems, dtype=torch.float32, device=device)
+        _LINW_WS[device] = buf
+    return buf
+
+
 def linear_wgrad(dy, x, dw, M, Nout, Kin, lddy=None, ldx=None):
+    """dw[Nout][Kin] += dy^T x.  bf16: split-K partial slabs in a cached fp32
+    workspace folded by one reduction pass; fp32: atomic split-K."""
     tk = ktimer.begin("linear_wgrad/wide", 2.0 * M * Nout * Kin)
-    lib().vlp_linear_wgrad(dcode(dy), M, Nout, Kin, ptr(dy), lddy or Nout, ptr(x), ldx or Kin,
-                           ptr(dw), _s())
+    if dy.dtype == torch.bfloat16 and Kin % 4 == 0:
+        ws = _linw_ws(dy.device, 16 * Nout * Kin)
+        lib().vlp_linear_wgrad_ws(dcode(dy), M, Nout, Kin, ptr(dy), lddy or Nout, ptr(x), ldx or Kin,
+                                  ptr(dw), ptr(ws), ws.numel(), _s())
+    else:
+        lib().vlp_linear_wgrad(dcode(dy), M, Nout, Kin, ptr(dy), lddy or Nout, ptr(x), ldx or Kin,
+                               ptr(dw), _s())
     ktimer.end(tk)
 
 
