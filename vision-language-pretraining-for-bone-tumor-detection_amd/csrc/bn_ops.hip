@@ -425,39 +425,56 @@ __device__ __forceinline__ MpCand mp_cand(int h, int Ho) {
   return c;
 }
 
+// The gathers of one pixel (4 candidate pooled outputs + argmax taps + y),
+// issued as one batch; the kernel keeps the NEXT pixel's batch in flight
+// while it finishes the current one.  (vmcnt retires loads and stores in
+// issue order: without the prefetch every pixel's loads would also wait for
+// the previous pixel's store.)
 template <typename T>
-__device__ __forceinline__ void mp_route(const T* __restrict__ dp, const uint8_t* __restrict__ idx, int n,
-                                         const MpCand& ch, int w, int c0, int C, int Ho, int Wo, float* g) {
-  constexpr int E = Chunk<T>::N;
-  const MpCand cw = mp_cand(w, Wo);
+struct MpLoads {
   uint4 v[4];
   uint2 ib[4];
-  int tap[4];
-  bool ok[4];
+  uint4 y;
+  unsigned tap4;   // 4 x 8-bit tap of each candidate, 0xff = invalid
+};
+template <typename T>
+__device__ __forceinline__ void mp_fetch(const T* __restrict__ dp, const uint8_t* __restrict__ idx,
+                                         const T* __restrict__ y, int n, int h, const MpCand& ch, int w,
+                                         int c0, int C, int H, int W, int Ho, int Wo, MpLoads<T>& L) {
+  constexpr int E = Chunk<T>::N;
+  const MpCand cw = mp_cand(w, Wo);
+  L.tap4 = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int ho = (q >> 1) ? ch.b : ch.a, wo = (q & 1) ? cw.b : cw.a;
-    tap[q] = ((q >> 1) ? ch.tb : ch.ta) * 3 + ((q & 1) ? cw.tb : cw.ta);
-    ok[q] = ((q >> 1) ? ch.vb : ch.va) && ((q & 1) ? cw.vb : cw.va);
+    const int tp = ((q >> 1) ? ch.tb : ch.ta) * 3 + ((q & 1) ? cw.tb : cw.ta);
+    const bool ok = ((q >> 1) ? ch.vb : ch.va) && ((q & 1) ? cw.vb : cw.va);
+    L.tap4 |= (unsigned)(ok ? tp : 255) << (8 * q);
     const size_t po = (((size_t)n * Ho + ho) * Wo + wo) * C + c0;
-    v[q] = ldg16(dp + po);
+    L.v[q] = ldg16(dp + po);
     if constexpr (E == 8) {
-      ib[q] = *reinterpret_cast<const uint2*>(idx + po);
+      L.ib[q] = *reinterpret_cast<const uint2*>(idx + po);
     } else {
-      ib[q].x = *reinterpret_cast<const unsigned*>(idx + po);
-      ib[q].y = 0;
+      L.ib[q].x = *reinterpret_cast<const unsigned*>(idx + po);
+      L.ib[q].y = 0;
     }
   }
+  L.y = ldg16(y + (((size_t)n * H + h) * W + w) * C + c0);
+}
+template <typename T>
+__device__ __forceinline__ void mp_route(const MpLoads<T>& L, float* g) {
+  constexpr int E = Chunk<T>::N;
 #pragma unroll
   for (int j = 0; j < E; ++j) g[j] = 0.f;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     float f[E];
-    Chunk<T>::unpack(v[q], f);
+    Chunk<T>::unpack(L.v[q], f);
+    const unsigned tq = (L.tap4 >> (8 * q)) & 255u;
 #pragma unroll
     for (int j = 0; j < E; ++j) {
-      const unsigned b = (((j >> 2) ? ib[q].y : ib[q].x) >> (8 * (j & 3))) & 255u;
-      g[j] += (ok[q] && b == (unsigned)tap[q]) ? f[j] : 0.f;
+      const unsigned b = (((j >> 2) ? L.ib[q].y : L.ib[q].x) >> (8 * (j & 3))) & 255u;
+      g[j] += (b == tq) ? f[j] : 0.f;
     }
   }
 }
@@ -494,24 +511,24 @@ maxpool_bwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const T* __restri
       ka[j] = k; ba[j] = -k * is[j] * mgx; ca[j] = -k * mg + k * is[j] * mgx * mu[j];
     }
   }
-  for (int r = 0; r < kMpRows; ++r) {
-    const int h = rb * kMpRows + r;
-    if (h >= H) break;
-    const MpCand ch = mp_cand(h, Ho);
-    for (int w = t / cpr; w < W; w += wstep) {
-      float g[E], yv[E];
-      mp_route<T>(dp, idx, n, ch, w, c0, C, Ho, Wo, g);
-      const size_t o = (((size_t)n * H + h) * W + w) * C + c0;
-      Chunk<T>::unpack(ldg16(y + o), yv);
-      if constexpr (APPLY) {
-        float d[E];
-#pragma unroll
-        for (int j = 0; j < E; ++j) {
-          const float gg = fmaf(yv[j], a[j], b[j]) > 0.f ? g[j] : 0.f;
-          d[j] = fmaf(ka[j], gg, fmaf(ba[j], yv[j], ca[j]));
-        }
-        stg16(dy + o, Chunk<T>::pack(d));
-      } else {
+  const int w0 = t / cpr;
+  const int nw = w0 < W ? (W - w0 + wstep - 1) / wstep : 0;
+  int rows = H - rb * kMpRows;
+  if (rows > kMpRows) rows = kMpRows;
+  const int total = rows * nw;
+  if constexpr (!APPLY) {
+    // stats pass: no stores, so plain nested walk (loads of consecutive
+    // pixels are free to overlap)
+    for (int r = 0; r < rows; ++r) {
+      const int h = rb * kMpRows + r;
+      const MpCand ch = mp_cand(h, Ho);
+#pragma unroll 2
+      for (int w = w0; w < W; w += wstep) {
+        MpLoads<T> L;
+        mp_fetch<T>(dp, idx, y, n, h, ch, w, c0, C, H, W, Ho, Wo, L);
+        float g[E], yv[E];
+        mp_route<T>(L, g);
+        Chunk<T>::unpack(L.y, yv);
 #pragma unroll
         for (int j = 0; j < E; ++j) {
           const float gg = fmaf(yv[j], a[j], b[j]) > 0.f ? g[j] : 0.f;
@@ -520,8 +537,6 @@ maxpool_bwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const T* __restri
         }
       }
     }
-  }
-  if constexpr (!APPLY) {
     __shared__ float red[2][256][E];
 #pragma unroll
     for (int j = 0; j < E; ++j) { red[0][t][j] = ag[j]; red[1][t][j] = ax[j]; }
@@ -537,6 +552,32 @@ maxpool_bwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const T* __restri
         atomicAdd(sum_gx + ro + j, (double)ax[j]);
       }
     }
+    return;
+  }
+  // apply pass: flattened (row, pixel) walk, one pixel's gathers ahead
+  MpLoads<T> cur, nxt;
+  if (total > 0) {
+    const int h = rb * kMpRows;
+    mp_fetch<T>(dp, idx, y, n, h, mp_cand(h, Ho), w0, c0, C, H, W, Ho, Wo, cur);
+  }
+  for (int it = 0; it < total; ++it) {
+    const int r = it / nw, jw = it - r * nw;
+    const int h = rb * kMpRows + r, w = w0 + jw * wstep;
+    if (it + 1 < total) {
+      const int r1 = (it + 1) / nw, j1 = it + 1 - r1 * nw;
+      const int h1 = rb * kMpRows + r1;
+      mp_fetch<T>(dp, idx, y, n, h1, mp_cand(h1, Ho), w0 + j1 * wstep, c0, C, H, W, Ho, Wo, nxt);
+    }
+    float g[E], yv[E], d[E];
+    mp_route<T>(cur, g);
+    Chunk<T>::unpack(cur.y, yv);
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      const float gg = fmaf(yv[j], a[j], b[j]) > 0.f ? g[j] : 0.f;
+      d[j] = fmaf(ka[j], gg, fmaf(ba[j], yv[j], ca[j]));
+    }
+    stg16(dy + (((size_t)n * H + h) * W + w) * C + c0, Chunk<T>::pack(d));
+    cur = nxt;
   }
 }
 
