@@ -63,6 +63,17 @@ int vlp_conv_dgrad_relu(int dtype, const void* dy, const void* wt, void* g, int 
                         const void* relu_out, const void* y, const float* mean,
                         const float* invstd, double* stat1, double* stat2, int stat_rep,
                         void* stream);
+/* Weight gradient as split-K fp32 slabs: split s of the pixel reduction writes
+ * split_ws[s][Co][KH][KW][C] (plain stores, no atomics); *nsplit receives the
+ * split count (<= ws_floats / (Co*KH*KW*C)).  vlp_conv_wgrad_fold then sums the
+ * slabs into grad[Co][C][KH][KW], the layout of the reference's conv weight
+ * gradient (timm resnet34 convs, VisionLanguageModule.py:34-35), overwriting it.
+ * Replaces vlp_conv_wgrad + vlp_unpack_conv_grad on the training path. */
+int vlp_conv_wgrad_ws(int dtype, const void* dy, const void* x, float* split_ws, long long ws_floats,
+                      int* nsplit, int N, int H, int W, int C, int Co, int KH, int KW, int S, int P,
+                      void* stream);
+int vlp_conv_wgrad_fold(int Co, int C, int KH, int KW, int nsplit, const float* split_ws, float* grad,
+                        void* stream);
 /* dw_ws[Co][KH][KW][C] += sum over pixels dy x_patch (fp32 atomics; zero first).
  * Optional BN+ReLU-on-load of x as in vlp_conv_fwd.  dyT (optional, bf16): the
  * same gradient transposed to [Co][N*Ho*Wo] (vlp_bn_bwd_apply writes it); when

@@ -114,6 +114,12 @@ def test_conv_dgrad_wgrad(ops, dt, case):
     torch.cuda.synchronize()
     assert rel(nchw(dx.float().cpu()), x.grad + add) < tol(dt)
     assert rel(g.cpu(), w.grad) < tol(dt) / 2
+    # split-K slabs + fold straight into the parameter layout (training path)
+    g3 = torch.full((Co, C, KH, KW), float("nan"), device="cuda")
+    ops.conv_wgrad_into(nhwc(dy).to(dt).cuda(), nhwc(x.detach()).to(dt).cuda(), KH, KW, S, P, g3)
+    torch.cuda.synchronize()
+    assert rel(g3.cpu(), w.grad) < tol(dt) / 2
+    assert rel(g3.cpu(), g.cpu()) < 1e-5
     Mp = dy.shape[0] * dy.shape[2] * dy.shape[3]
     if dt == torch.bfloat16 and Mp % 8 == 0:
         # pixel-contiguous A operand (dy^T [Co][pixels], as vlp_bn_bwd_apply writes it)
@@ -125,6 +131,41 @@ def test_conv_dgrad_wgrad(ops, dt, case):
         torch.cuda.synchronize()
         assert rel(g2.cpu(), w.grad) < tol(dt) / 2
         assert rel(g2.cpu(), g.cpu()) < 1e-5
+
+
+@pytest.mark.parametrize("case", [(4, 64, 64, 64, 64, 3, 3, 1, 1), (8, 32, 32, 128, 128, 3, 3, 1, 1),
+                                  (32, 32, 32, 64, 128, 1, 1, 2, 0), (32, 16, 16, 256, 256, 3, 3, 1, 1)])
+@pytest.mark.parametrize("ws_floats", [None, "tight"])
+def test_conv_wgrad_split_slabs(ops, case, ws_floats):
+    """Deep pixel reductions (many K-splits, each its own fp32 slab) against
+    torch's fp32 weight gradient; "tight" gives the workspace room for only 3
+    slabs, so the split count must shrink to fit."""
+    import ctypes
+    from vlp_amd._lib import lib
+    N, H, W, C, Co, KH, KW, S, P = case
+    dt = torch.bfloat16
+    torch.manual_seed(5)
+    x = torch.randn(N, C, H, W).to(dt).float().requires_grad_()
+    w = (torch.randn(Co, C, KH, KW) * (C * KH * KW) ** -0.5).requires_grad_()
+    y = F.conv2d(x, w, stride=S, padding=P)
+    dy = torch.randn_like(y).to(dt).float()
+    y.backward(dy)
+    slab = Co * C * KH * KW
+    nws = 3 * slab if ws_floats == "tight" else 64 * slab
+    ws = torch.full((nws + 64,), float("nan"), device="cuda")
+    g = torch.full((Co, C, KH, KW), float("nan"), device="cuda")
+    ns = ctypes.c_int(0)
+    dyd, xd = nhwc(dy).to(dt).cuda(), nhwc(x.detach()).to(dt).cuda()
+    lib().vlp_conv_wgrad_ws(1, dyd.data_ptr(), xd.data_ptr(), ws.data_ptr(), nws, ctypes.addressof(ns),
+                            N, H, W, C, Co, KH, KW, S, P, torch.cuda.current_stream().cuda_stream)
+    assert 1 <= ns.value <= nws // slab
+    if ws_floats is None:
+        assert ns.value > 1, "deep reduction expected to split"
+    lib().vlp_conv_wgrad_fold(Co, C, KH, KW, ns.value, ws.data_ptr(), g.data_ptr(),
+                              torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.isnan(ws[nws:]).all().item(), "slab writes past the workspace"
+    assert rel(g.cpu(), w.grad) < 2e-3
 
 
 @pytest.mark.parametrize("dt", DT)

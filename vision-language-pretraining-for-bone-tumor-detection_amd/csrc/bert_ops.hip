@@ -69,23 +69,8 @@ struct EpiLinearBwd {
   }
 };
 
-// split-K partial of a weight gradient: split s writes slab s of ws[ks][Nout][Kin]
-// with plain stores (the fp32 atomics of 10+ splits onto the same small dW
-// were the bound: ~50 G atomics/s); linw_reduce_kernel folds the slabs
-struct EpiSplitStore {
-  static constexpr bool kStats = false;
-  static constexpr bool kSplitOut = true;
-  double* stat1 = nullptr; double* stat2 = nullptr;
-  float* out; int ldo; size_t slab;
-  __device__ EpiSplitStore at_split(int s) const {
-    EpiSplitStore e = *this;
-    e.out += (size_t)s * slab;
-    return e;
-  }
-  __device__ void operator()(int row, int col, v4f v, v4f&, v4f&) const {
-    *reinterpret_cast<v4f*>(out + (size_t)row * ldo + col) = v;
-  }
-};
+// split-K weight gradients: EpiSplitStore (gemm.h) writes slab s of
+// ws[ks][Nout][Kin] with plain stores; linw_reduce_kernel folds the slabs
 __global__ void linw_reduce_kernel(size_t n4, int ks, const float4* __restrict__ ws, float4* __restrict__ dw) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
     float4 a = dw[i];

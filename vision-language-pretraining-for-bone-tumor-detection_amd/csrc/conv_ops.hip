@@ -1304,6 +1304,71 @@ static int conv_wgrad_t(const void* dy, const void* x, float* dw, ConvGeom g, co
   return gemm_wgrad<T>(g.Co, g.K, g.M, la, lb, ep, st);
 }
 
+// Weight gradient straight into the parameter's [Co][C][KH][KW] layout: the
+// GEMM's K-splits write fp32 slabs ws[s][Co][KH*KW*C] (EpiSplitStore) and one
+// fold pass sums them and transposes.  Thread per slab element: reads are
+// coalesced over c with 4 independent slab streams in flight per thread; the
+// transposing writes (stride KH*KW) merge in L2.
+__global__ void wgrad_fold_kernel(int Co, int C, int T, int ks, size_t slab, const float* __restrict__ ws,
+                                  float* __restrict__ g) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= slab) return;
+  const float* p = ws + i;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int s = 0;
+  for (; s + 4 <= ks; s += 4) {
+    a0 += p[(size_t)s * slab];
+    a1 += p[(size_t)(s + 1) * slab];
+    a2 += p[(size_t)(s + 2) * slab];
+    a3 += p[(size_t)(s + 3) * slab];
+  }
+  for (; s < ks; ++s) a0 += p[(size_t)s * slab];
+  const int c = (int)(i % C);
+  const size_t r = i / C;
+  const int t = (int)(r % T), co = (int)(r / T);
+  g[((size_t)co * C + c) * T + t] = (a0 + a1) + (a2 + a3);
+}
+
+template <typename T>
+static int conv_wgrad_ws_t(const void* dy, const void* x, float* ws, long long ws_floats, int* ks_out, ConvGeom g,
+                           hipStream_t st) {
+  g.M = g.N * g.Ho * g.Wo;
+  g.K = g.KH * g.KW * g.C;
+  const size_t slab = (size_t)g.Co * g.K;
+  const long long fit = ws_floats > 0 ? ws_floats / (long long)slab : 0;
+  const int max_ks = (int)(fit < 4096 ? fit : 4096);
+  if (max_ks < 1) return (int)hipErrorInvalidValue;
+  int ks = 1;
+  bool split_store = false;
+  if constexpr (std::is_same<T, bf16>::value) {
+    // tile engines whose epilogue honours per-split output slabs
+    if (gemm_variant() >= 5 && g.K % 4 == 0) {
+      static const int mink5 = getenv("VLP_WGRAD_MINK") ? atoi(getenv("VLP_WGRAD_MINK")) : 2048;
+      int mink = g.Co <= 64 ? 2048 : mink5;
+      const int need = (g.M + max_ks - 1) / max_ks;
+      if (mink < need) mink = need;
+      static_assert(use_bk<bf16, MNMat<bf16>, ConvWgradB<bf16, false>>(),
+                    "split slabs need the bk / big engines");
+      MNMat<bf16> la{(const bf16*)dy, g.Co, g.Co, g.M};
+      ConvWgradB<bf16, false> lb{g, (const bf16*)x, nullptr, nullptr, g.K, make_pixstep(g, Elem<bf16>::BK)};
+      EpiSplitStore ep{nullptr, nullptr, ws, g.K, slab};
+      const int r = g.Co <= 64 ? gemm_short<bf16>(g.Co, g.K, g.M, -mink, la, lb, ep, st)
+                               : gemm_conv_wide<bf16>(g.Co, g.K, g.M, -mink, la, lb, ep, st);
+      if (r) return r;
+      ks = last_ksplit();
+      if (ks > max_ks) return (int)hipErrorInvalidValue;   // would have overrun the workspace
+      split_store = true;
+    }
+  }
+  if (!split_store) {   // other engines: atomics into slab 0
+    if (hipMemsetAsync(ws, 0, slab * sizeof(float), st) != hipSuccess) return (int)hipGetLastError();
+    const int r = conv_wgrad_t<T>(dy, x, ws, g, nullptr, nullptr, st);
+    if (r) return r;
+  }
+  *ks_out = ks;
+  return 0;
+}
+
 static StemGeom make_stem(int N, int H, int W) {
   StemGeom g;
   g.N = N;
@@ -1407,6 +1472,25 @@ VLP_EXPORT int vlp_conv_wgrad(int dtype, const void* dy, const void* x, float* d
   if ((long long)N * H * W * C >= (1ll << 31)) return (int)hipErrorInvalidValue;   // 32-bit pixel walk
   if (dtype == VLP_BF16) return conv_wgrad_t<bf16>(dy, x, dw_ws, g, in_scale, in_shift, st, dyT);
   return conv_wgrad_t<float>(dy, x, dw_ws, g, in_scale, in_shift, st);
+}
+
+VLP_EXPORT int vlp_conv_wgrad_ws(int dtype, const void* dy, const void* x, float* split_ws, long long ws_floats,
+                                 int* nsplit, int N, int H, int W, int C, int Co, int KH, int KW, int S, int P,
+                                 void* stream) {
+  ConvGeom g = make_geom(N, H, W, C, Co, KH, KW, S, P);
+  hipStream_t st = (hipStream_t)stream;
+  if (!nsplit || (long long)N * H * W * C >= (1ll << 31)) return (int)hipErrorInvalidValue;
+  if (dtype == VLP_BF16) return conv_wgrad_ws_t<bf16>(dy, x, split_ws, ws_floats, nsplit, g, st);
+  return conv_wgrad_ws_t<float>(dy, x, split_ws, ws_floats, nsplit, g, st);
+}
+
+VLP_EXPORT int vlp_conv_wgrad_fold(int Co, int C, int KH, int KW, int nsplit, const float* split_ws, float* grad,
+                                   void* stream) {
+  if (nsplit < 1) return (int)hipErrorInvalidValue;
+  const size_t n = (size_t)Co * KH * KW * C;
+  hipLaunchKernelGGL(wgrad_fold_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, Co,
+                     C, KH * KW, nsplit, n, split_ws, grad);
+  return (int)hipGetLastError();
 }
 
 VLP_EXPORT int vlp_stem_prep(int dtype, const float* x, void* xp, int N, int H, int W, void* stream) {

@@ -1116,7 +1116,20 @@ gemm_big_kernel(GemmShape sh, LA la, LB lb, EP ep) {
     body(std::integral_constant<int, 1>{}, t + 1);
   }
   __syncthreads();   // ring drained (incl. the null-resource tail fetches) before LDS is reused
-  ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep, acc, row0, col0, wid, wm, wn, smem);
+  if (sh.dbg & 1) {   // diagnostics: no epilogue (acc kept live)
+    float z = 0.f;
+#pragma unroll
+    for (int a = 0; a < MB; ++a)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) z += acc[a][b][0] + acc[a][b][3];
+    if (z == 1234.5f) ep(row0, col0, acc[0][0], acc[0][0], acc[0][0]);
+    return;
+  }
+  if constexpr (SplitTrait<EP>::value) {
+    ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep.at_split(split), acc, row0, col0, wid, wm, wn, smem);
+  } else {
+    ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep, acc, row0, col0, wid, wm, wn, smem);
+  }
 }
 
 template <int BM, int BN, class EP>
@@ -1131,6 +1144,12 @@ constexpr int big_lds_bytes() {
 // launch all cost about the same, so the launch takes ceil(WG / slots)
 // rounds: pick the split (1..4 rounds' worth) with the best slot fill, each
 // split still >= min_k deep (epilogue atomics amortised).
+// split count of the last launch_gemm_bk / launch_gemm_big call on this host
+// thread (callers of split-store epilogues size their fold pass with it)
+inline int& last_ksplit() {
+  static thread_local int v = 1;
+  return v;
+}
 inline int balanced_ksplit(int tiles, int K, int slots, int min_k) {
   if (tiles >= slots) return 1;
   int best = 1;
@@ -1250,6 +1269,7 @@ inline int launch_gemm_bk(int M, int N, int K, int ksplit, const LA& la, const L
   sh.kchunk = kc;
   sh.xsplit = 0;
   sh.nsplit = ksplit;
+  last_ksplit() = ksplit;
   static const int dbg = getenv("VLP_GEMM_DBG") ? atoi(getenv("VLP_GEMM_DBG")) : 0;
   sh.dbg = dbg;
   dim3 grid(sh.tiles_m * sh.tiles_n * ksplit, 1, 1);
@@ -1304,6 +1324,7 @@ inline int launch_gemm_big(int M, int N, int K, int ksplit, const LA& la, const 
   sh.kchunk = kc;
   sh.xsplit = 0;
   sh.nsplit = ksplit;
+  last_ksplit() = ksplit;
   static const int dbg = getenv("VLP_GEMM_DBG") ? atoi(getenv("VLP_GEMM_DBG")) : 0;
   sh.dbg = dbg;
   dim3 grid(sh.tiles_m * sh.tiles_n * ksplit, 1, 1);
@@ -1547,6 +1568,24 @@ struct EpiStore {
     v = v * alpha;
     if (bias) v += *reinterpret_cast<const v4f*>(bias + col);
     store4(out + (size_t)row * ldo + col, v);
+  }
+};
+// split-K partial of a weight gradient: split s writes slab s of
+// out[ks][rows][ldo] with plain stores, folded by a separate pass (fp32
+// atomics of many splits onto the same small dW were the bound:
+// ~50 G atomics/s, 80-170 us per conv weight gradient)
+struct EpiSplitStore {
+  static constexpr bool kStats = false;
+  static constexpr bool kSplitOut = true;
+  double* stat1 = nullptr; double* stat2 = nullptr;
+  float* out; int ldo; size_t slab;
+  __device__ EpiSplitStore at_split(int s) const {
+    EpiSplitStore e = *this;
+    e.out += (size_t)s * slab;
+    return e;
+  }
+  __device__ void operator()(int row, int col, v4f v, v4f&, v4f&) const {
+    *reinterpret_cast<v4f*>(out + (size_t)row * ldo + col) = v;
   }
 };
 // fp32 atomic accumulation (split-K / weight gradients)

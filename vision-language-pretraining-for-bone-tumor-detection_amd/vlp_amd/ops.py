@@ -101,6 +101,30 @@ def conv_wgrad(dy, x, KH, KW, S, P, dw_ws, in_scale=None, in_shift=None, dyT=Non
     return dw_ws
 
 
+_WGRAD_WS = {}
+WGRAD_WS_FLOATS = 32 << 20   # 128 MB of split-K slabs (the largest conv needs ~17M floats at bs=256)
+
+
+def conv_wgrad_into(dy, x, KH, KW, S, P, grad):
+    """grad[Co][C][KH][KW] = sum over pixels dy x_patch, overwriting grad (the
+    parameter's own gradient layout).  The GEMM's K-splits write fp32 slabs of
+    a cached workspace; one fold pass sums and transposes them."""
+    import ctypes
+    N, H, W, C = x.shape
+    Co, Ho, Wo = dy.shape[-1], dy.shape[1], dy.shape[2]
+    ws = _WGRAD_WS.get(dy.device)
+    if ws is None:
+        ws = torch.empty(WGRAD_WS_FLOATS, dtype=torch.float32, device=dy.device)
+        _WGRAD_WS[dy.device] = ws
+    ns = ctypes.c_int(0)
+    tk = ktimer.begin(f"conv_wgrad[raw]{_tile_wgrad(Co)}", 2.0 * N * Ho * Wo * Co * C * KH * KW)
+    lib().vlp_conv_wgrad_ws(dcode(dy), ptr(dy), ptr(x), ptr(ws), ws.numel(), ctypes.addressof(ns), N, H, W, C,
+                            Co, KH, KW, S, P, _s())
+    ktimer.end(tk)
+    lib().vlp_conv_wgrad_fold(Co, C, KH, KW, ns.value, ptr(ws), ptr(grad), _s())
+    return grad
+
+
 def stem_geom(H, W):
     import ctypes
     a, b, c, d = (ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int())

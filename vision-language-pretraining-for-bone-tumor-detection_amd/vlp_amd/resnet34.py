@@ -315,7 +315,8 @@ class ResNet34Tower(ArenaModule):
         T = self.tdtype
         dev = self.arena.data.device
         ws["bstat"].zero_()
-        ws["wgrad"].zero_()
+        o0, n0 = self._wg_off["conv1"]
+        ws["wgrad"][o0:o0 + n0].zero_()   # stem's atomic accumulator (the 3x3 convs overwrite their grads)
         dfeat = dfeat.float().contiguous()
         blocks = saved["blocks"]
         dout = None
@@ -425,8 +426,12 @@ class ResNet34Tower(ArenaModule):
         return buf[:C * M].view(C, M)
 
     def _wgrad(self, ws, c, dy, x, sc=None, sh=None, dyT=None):
+        if sc is None and dyT is None:
+            ops.conv_wgrad_into(dy, x, c.KH, c.KW, c.S, c.P, self.arena.gview(c.key + ".weight"))
+            return
         o, n = self._wg_off[c.key]
         buf = ws["wgrad"][o:o + n]
+        buf.zero_()
         ops.conv_wgrad(dy, x, c.KH, c.KW, c.S, c.P, buf, sc, sh, dyT=dyT)
         ops.unpack_conv_grad(buf, self.arena.gview(c.key + ".weight"))
 
