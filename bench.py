@@ -115,7 +115,8 @@ def _traffic(family):
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    return round(d["traffic_bytes_per_launch"]) if d.get("family") == family else None
+    e = d.get("families", {}).get(family)
+    return round(e["traffic_bytes_per_launch"]) if e else None
 
 
 def main():

@@ -3,7 +3,7 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 TAG=${TAG:-r1}
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/${TAG}_tests.log 2>&1 || { echo TESTS FAILED; tail -30 gpurun_out/${TAG}_tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1 || { echo TESTS FAILED; tail -30 gpurun_out/${TAG}_tests.log; exit 1; }
 tail -1 gpurun_out/${TAG}_tests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || { echo SMOKE FAILED; tail -20 gpurun_out/${TAG}_smoke.log; exit 1; }
 tail -1 gpurun_out/${TAG}_smoke.log

@@ -6,7 +6,8 @@ correction: FETCH_SIZE tallies 128-B requests at 64 B, so wide coalesced reads
 are reported at exactly half their bytes -> x2.  WRITE_SIZE is exact for
 16-B-per-lane stores and float atomics.
 
-  python tools/pmc_traffic.py FETCH.csv WRITE.csv REGEX [--calib adamw_kernel] [--out f.json]
+  python tools/pmc_traffic.py FETCH.csv WRITE.csv REGEX --family NAME [--out f.json]
+  (--out merges the family's entry into the file's "families" map)
 """
 import argparse
 import csv
@@ -53,8 +54,17 @@ def main():
                                     "write_bytes_mean": 1024.0 * sum(wr.get(cal[0], [0])) / max(len(wr.get(cal[0], [])), 1)}
     print(json.dumps(res, indent=1))
     if args.out:
+        # one file, one entry per kernel family (bench.py looks its roofline family up)
+        try:
+            with open(args.out) as f:
+                doc = json.load(f)
+        except (OSError, ValueError):
+            doc = {}
+        if "families" not in doc:
+            doc = {"families": {}}
+        doc["families"][args.family or args.regex] = res
         with open(args.out, "w") as f:
-            json.dump(res, f, indent=1)
+            json.dump(doc, f, indent=1)
 
 
 if __name__ == "__main__":
