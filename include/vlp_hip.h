@@ -109,6 +109,17 @@ int vlp_bn_finalize(int C, double count, const double* sum, const double* sumsq,
                     const float* gamma, const float* beta, float eps, float momentum,
                     float* running_mean, float* running_var, float* scale, float* shift,
                     float* mean, float* invstd, void* stream);
+/* vlp_stat_reduce + vlp_bn_finalize in one launch (sum / sumsq: [rep][C]
+ * replicas, folded into copy 0 as a side effect) */
+int vlp_bn_finalize_rep(int rep, int C, double count, double* sum, double* sumsq,
+                        const float* gamma, const float* beta, float eps, float momentum,
+                        float* running_mean, float* running_var, float* scale, float* shift,
+                        float* mean, float* invstd, void* stream);
+/* vlp_stat_reduce + vlp_bn_param_grad in one launch: dgamma = sum g*xhat,
+ * dbeta = sum g; sum_gxd / dgamma_d / dbeta_d (all or none): the downsample BN
+ * that shares g (BasicBlock bn2 + downsample.1).  Sums folded into copy 0. */
+int vlp_bn_grad_rep(int rep, int C, double* sum_g, double* sum_gx, double* sum_gxd, float* dgamma,
+                    float* dbeta, float* dgamma_d, float* dbeta_d, void* stream);
 int vlp_bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* running_mean,
                        const float* running_var, float eps, float* scale, float* shift,
                        void* stream);

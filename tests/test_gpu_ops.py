@@ -324,3 +324,18 @@ def test_linear_wgrad(ops, dt, shape):
     ops.linear_wgrad(dy.to(dt).cuda(), x.to(dt).cuda(), dw, M, Nout, Kin)
     torch.cuda.synchronize()
     assert rel(dw, ref) < tol(dt) / 4
+
+
+@pytest.mark.parametrize("M,N,ld,off", [(10240, 312, 312, 0), (10240, 1200, 1200, 0), (777, 936, 944, 8),
+                                        (300, 312, 320, 4), (5, 64, 64, 0)])
+def test_colsum(ops, M, N, ld, off):
+    """Bias-gradient column sums (fp32 atomics onto a pre-filled output):
+    16-B vector path for aligned bf16 rows, scalar path otherwise (off=4)."""
+    torch.manual_seed(9)
+    buf = torch.randn(M * ld + off + 8).to(torch.bfloat16).cuda()
+    x = buf[off:off + M * ld].view(M, ld)
+    out = torch.full((N,), 0.5, device="cuda")
+    ops.colsum(x, out, M, N, ld)
+    torch.cuda.synchronize()
+    ref = x[:, :N].float().sum(0) + 0.5
+    assert (out - ref).abs().max().item() < 1e-3 * (1 + ref.abs().max().item())

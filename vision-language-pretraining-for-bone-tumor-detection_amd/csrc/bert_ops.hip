@@ -200,6 +200,50 @@ __global__ void colsum_kernel(int M, int N, const T* __restrict__ x, int ld, flo
   atomicAdd(out + n, s);
 }
 
+// 16-B column chunks: 32 chunks (256 bf16 columns) x 8 row partitions per
+// block, 4 independent row loads in flight per thread
+__global__ void __launch_bounds__(256)
+colsum_vec_kernel(int M, int N, const bf16* __restrict__ x, int ld, float* __restrict__ out) {
+  const int cg = threadIdx.x & 31, part = threadIdx.x >> 5;
+  const int n0 = blockIdx.x * 256 + cg * 8;
+  __shared__ float red[8][256 + 8];
+  float s[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = 0.f;
+  if (n0 < N) {
+    const int step = gridDim.y * 8;
+    int m = blockIdx.y * 8 + part;
+    for (; m + 3 * step < M; m += 4 * step) {
+      uint4 u[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) u[q] = ldg16(x + (size_t)(m + q * step) * ld + n0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float f[8];
+        Chunk<bf16>::unpack(u[q], f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += f[j];
+      }
+    }
+    for (; m < M; m += step) {
+      float f[8];
+      Chunk<bf16>::unpack(ldg16(x + (size_t)m * ld + n0), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += f[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[part][cg * 8 + j] = s[j];
+  __syncthreads();
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t += red[q][threadIdx.x];
+    atomicAdd(out + n, t);
+  }
+}
+
 // ---------------- attention ----------------
 // One workgroup per (sequence b, head h).  qkv: [B*T][3*Dm] rows (q | k | v),
 // head slice [h*dh, (h+1)*dh).  Saves softmax probabilities P[b][h][T][T] (fp32).
@@ -462,6 +506,14 @@ VLP_EXPORT int vlp_linear_wgrad_ws(int dtype, int M, int Nout, int Kin, const vo
 
 VLP_EXPORT int vlp_colsum(int dtype, int M, int N, const void* x, int ld, float* out, void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  if (dtype == VLP_BF16 && N % 8 == 0 && ld % 8 == 0 && ((uintptr_t)x & 15) == 0) {
+    const int gx = (N + 255) / 256;
+    int gy = 512 / gx;
+    if (gy > (M + 63) / 64) gy = (M + 63) / 64;
+    if (gy < 1) gy = 1;
+    hipLaunchKernelGGL(colsum_vec_kernel, dim3(gx, gy), dim3(256), 0, st, M, N, (const bf16*)x, ld, out);
+    return (int)hipGetLastError();
+  }
   int gy = (M + 255) / 256;
   if (gy > 64) gy = 64;
   dim3 grid((N + 63) / 64, gy);

@@ -78,6 +78,89 @@ stat_reduce_kernel(int rep, int C, double* a, double* b, double* c) {
   if (w == 0 && ch < C) p[ch] = part[0][lane] + part[1][lane] + part[2][lane] + part[3][lane];
 }
 
+// replica fold of up to 3 arrays for one 64-channel group: 8 waves split the
+// replicas and every lane keeps all its loads in flight (latency-bound
+// otherwise); returns the totals in tot[k][lane] and stores them into replica 0
+constexpr int kFoldWaves = 8;
+__device__ __forceinline__ void fold_replicas(int rep, int C, double* const* arr, int n, double (*tot)[64]) {
+  __shared__ double part[3][kFoldWaves][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ch = blockIdx.x * 64 + lane;
+  double s[3] = {0, 0, 0};
+  if (ch < C) {
+    int r = w;
+    for (; r + 3 * kFoldWaves < rep; r += 4 * kFoldWaves) {
+      double v[3][4];
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          v[k][j] = (k < n && arr[k]) ? arr[k][(size_t)(r + j * kFoldWaves) * C + ch] : 0.0;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) s[k] += (v[k][0] + v[k][1]) + (v[k][2] + v[k][3]);
+    }
+    for (; r < rep; r += kFoldWaves)
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        if (k < n && arr[k]) s[k] += arr[k][(size_t)r * C + ch];
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) part[k][w][lane] = s[k];
+  __syncthreads();
+  if (w == 0 && ch < C)
+    for (int k = 0; k < n; ++k) {
+      double t = 0;
+#pragma unroll
+      for (int q = 0; q < kFoldWaves; ++q) t += part[k][q][lane];
+      tot[k][lane] = t;
+      if (arr[k]) arr[k][ch] = t;
+    }
+}
+
+// stat_reduce + bn_finalize in one launch (forward BN after a replicated-sum producer)
+__global__ void __launch_bounds__(64 * kFoldWaves)
+bn_finalize_rep_kernel(int rep, int C, double count, double* sum, double* sumsq, const float* __restrict__ gamma,
+                       const float* __restrict__ beta, float eps, float momentum, float* running_mean,
+                       float* running_var, float* scale, float* shift, float* mean_out, float* invstd_out) {
+  __shared__ double tot[2][64];
+  double* arr[2] = {sum, sumsq};
+  fold_replicas(rep, C, arr, 2, tot);
+  const int lane = threadIdx.x & 63, c = blockIdx.x * 64 + lane;
+  if (threadIdx.x >= 64 || c >= C) return;
+  double mean = tot[0][lane] / count;
+  double var = tot[1][lane] / count - mean * mean;
+  if (var < 0) var = 0;
+  float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  float sc = gamma[c] * invstd;
+  scale[c] = sc;
+  shift[c] = beta[c] - (float)mean * sc;
+  mean_out[c] = (float)mean;
+  invstd_out[c] = invstd;
+  if (running_mean) {
+    float unbiased = (float)(count > 1 ? var * count / (count - 1) : var);
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
+  }
+}
+
+// stat_reduce + bn_param_grad: dgamma = sum g*xhat, dbeta = sum g for a BN and
+// (optionally) the downsample BN that shares g
+__global__ void __launch_bounds__(64 * kFoldWaves)
+bn_grad_rep_kernel(int rep, int C, double* sum_g, double* sum_gx, double* sum_gxd, float* dgamma, float* dbeta,
+                   float* dgamma_d, float* dbeta_d) {
+  __shared__ double tot[3][64];
+  double* arr[3] = {sum_g, sum_gx, sum_gxd};
+  fold_replicas(rep, C, arr, 3, tot);
+  const int lane = threadIdx.x & 63, c = blockIdx.x * 64 + lane;
+  if (threadIdx.x >= 64 || c >= C) return;
+  dgamma[c] = (float)tot[1][lane];
+  dbeta[c] = (float)tot[0][lane];
+  if (dgamma_d) {
+    dgamma_d[c] = (float)tot[2][lane];
+    dbeta_d[c] = (float)tot[0][lane];
+  }
+}
+
 // ---- out = relu(sc*y + sh + identity), identity = idt or (scd*idt + shd) ----
 template <typename T, bool HAS_IDT>
 __global__ void __launch_bounds__(256)
@@ -614,6 +697,25 @@ VLP_EXPORT int vlp_bn_eval_coeffs(int C, const float* gamma, const float* beta, 
                                   void* stream) {
   hipLaunchKernelGGL(bn_eval_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, C,
                      gamma, beta, rm, rv, eps, scale, shift);
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_bn_finalize_rep(int rep, int C, double count, double* sum, double* sumsq,
+                                   const float* gamma, const float* beta, float eps, float momentum,
+                                   float* running_mean, float* running_var, float* scale, float* shift,
+                                   float* mean, float* invstd, void* stream) {
+  if (rep < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_finalize_rep_kernel, dim3((C + 63) / 64), dim3(64 * kFoldWaves), 0, (hipStream_t)stream, rep, C,
+                     count, sum, sumsq, gamma, beta, eps, momentum, running_mean, running_var, scale, shift, mean,
+                     invstd);
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_bn_grad_rep(int rep, int C, double* sum_g, double* sum_gx, double* sum_gxd, float* dgamma,
+                               float* dbeta, float* dgamma_d, float* dbeta_d, void* stream) {
+  if (rep < 1 || (sum_gxd == nullptr) != (dgamma_d == nullptr)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_grad_rep_kernel, dim3((C + 63) / 64), dim3(64 * kFoldWaves), 0, (hipStream_t)stream, rep, C, sum_g,
+                     sum_gx, sum_gxd, dgamma, dbeta, dgamma_d, dbeta_d);
   return (int)hipGetLastError();
 }
 

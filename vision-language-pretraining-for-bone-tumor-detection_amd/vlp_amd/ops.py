@@ -161,6 +161,19 @@ def stat_reduce(rep, C, a, b=None, c=None):
     lib().vlp_stat_reduce(int(rep), int(C), ptr(a), ptr(b), ptr(c), _s())
 
 
+def bn_finalize_rep(rep, count, s, ss, gamma, beta, eps, momentum, running_mean, running_var, scale, shift,
+                    mean, invstd):
+    """Fold the [rep][C] replicated sums and finalize in one launch."""
+    lib().vlp_bn_finalize_rep(int(rep), gamma.numel(), float(count), ptr(s), ptr(ss), ptr(gamma), ptr(beta),
+                              float(eps), float(momentum), ptr(running_mean), ptr(running_var),
+                              ptr(scale), ptr(shift), ptr(mean), ptr(invstd), _s())
+
+
+def bn_grad_rep(rep, C, sum_g, sum_gx, dgamma, dbeta, sum_gxd=None, dgamma_d=None, dbeta_d=None):
+    lib().vlp_bn_grad_rep(int(rep), int(C), ptr(sum_g), ptr(sum_gx), ptr(sum_gxd), ptr(dgamma), ptr(dbeta),
+                          ptr(dgamma_d), ptr(dbeta_d), _s())
+
+
 def bn_finalize(count, s, ss, gamma, beta, eps, momentum, running_mean, running_var, scale, shift,
                 mean, invstd):
     lib().vlp_bn_finalize(gamma.numel(), float(count), ptr(s), ptr(ss), ptr(gamma), ptr(beta),

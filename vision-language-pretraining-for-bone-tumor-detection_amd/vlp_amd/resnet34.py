@@ -235,10 +235,8 @@ class ResNet34Tower(ArenaModule):
         h = bn.holder
         if training:
             s, ss = self._fstat(ws, key, full=True)
-            ops.stat_reduce(STAT_REP, bn.C, s, ss)
-            s, ss = s[:bn.C], ss[:bn.C]
-            ops.bn_finalize(count, s, ss, gamma, beta, BN_EPS, BN_MOMENTUM, h.running_mean,
-                            h.running_var, sc, sh, mu, ist)
+            ops.bn_finalize_rep(STAT_REP, count, s, ss, gamma, beta, BN_EPS, BN_MOMENTUM, h.running_mean,
+                                h.running_var, sc, sh, mu, ist)
             h.num_batches_tracked.add_(1)
         else:
             ops.bn_eval_coeffs(gamma, beta, h.running_mean, h.running_var, BN_EPS, sc, sh)
@@ -343,17 +341,19 @@ class ResNet34Tower(ArenaModule):
             if not dout_masked:
                 ops.bn_bwd_reduce(M, C, dout, dbc, HW, out, y2, mu2, is2, yd, mud, isd, sg2f, sgx2f, sgxdf,
                                   out, stat_rep=STAT_REP)
-            ops.stat_reduce(STAT_REP, C, sg2f, sgx2f, sgxdf)
+            kd = pre + ".downsample.1"
+            ops.bn_grad_rep(STAT_REP, C, sg2f, sgx2f, self.arena.gview(k2 + ".weight"),
+                            self.arena.gview(k2 + ".bias"), sgxdf,
+                            self.arena.gview(kd + ".weight") if has_ds else None,
+                            self.arena.gview(kd + ".bias") if has_ds else None)
             sg2, sgx2 = sg2f[:C], sgx2f[:C]
             sgxd = sgxdf[:C] if has_ds else None
-            ops.bn_param_grad(sg2, sgx2, self.arena.gview(k2 + ".weight"), self.arena.gview(k2 + ".bias"))
             dy2 = torch.empty_like(y2)
             A = (y2, mu2, is2, self.arena.view(k2 + ".weight"), sg2, sgx2, dy2)
             Bside, g_id = None, None
             if has_ds:
                 dyd = torch.empty_like(yd)
                 Bside = (yd, mud, isd, self.arena.view(kd + ".weight"), sg2, sgxd, dyd)
-                ops.bn_param_grad(sg2, sgxd, self.arena.gview(kd + ".weight"), self.arena.gview(kd + ".bias"))
             elif dout_masked:
                 g_id = dout          # the identity branch's gradient is g itself
             else:
@@ -367,10 +367,10 @@ class ResNet34Tower(ArenaModule):
             sg1f, sgx1f = self._bstat(ws, k1, full=True)
             g1 = ops.conv_dgrad(dy2, ws[c2.key + ".wt"], Hh, Ww, C, 3, 3, 1, 1, y_bn=y1,
                                 bn=(sc1, sh1, mu1, is1), stat1=sg1f, stat2=sgx1f, stat_rep=STAT_REP)
-            ops.stat_reduce(STAT_REP, C, sg1f, sgx1f)
+            ops.bn_grad_rep(STAT_REP, C, sg1f, sgx1f, self.arena.gview(k1 + ".weight"),
+                            self.arena.gview(k1 + ".bias"))
             sg1, sgx1 = sg1f[:C], sgx1f[:C]
             self._wgrad(ws, c2, dy2, B["a1"], dyT=tA)
-            ops.bn_param_grad(sg1, sgx1, self.arena.gview(k1 + ".weight"), self.arena.gview(k1 + ".bias"))
             dy1 = torch.empty_like(y1)
             ops.bn_bwd_apply(M, C, g1, None, 1, None,
                              (y1, mu1, is1, self.arena.view(k1 + ".weight"), sg1, sgx1, dy1), None, None, y1,
@@ -402,9 +402,8 @@ class ResNet34Tower(ArenaModule):
         sc0, sh0, mu0, is0 = self._coef(ws, "bn1")
         sg0f, sgx0f = self._bstat(ws, "bn1", full=True)
         ops.maxpool_bwd(dout, idx, y0, sc0, sh0, mu0, is0, sg0f, sgx0f, stat_rep=STAT_REP)
-        ops.stat_reduce(STAT_REP, 64, sg0f, sgx0f)
+        ops.bn_grad_rep(STAT_REP, 64, sg0f, sgx0f, self.arena.gview("bn1.weight"), self.arena.gview("bn1.bias"))
         sg0, sgx0 = sg0f[:64], sgx0f[:64]
-        ops.bn_param_grad(sg0, sgx0, self.arena.gview("bn1.weight"), self.arena.gview("bn1.bias"))
         dy0 = torch.empty_like(y0)
         ops.maxpool_bwd_apply(dout, idx, y0, sc0, sh0, mu0, is0, self.arena.view("bn1.weight"), sg0, sgx0, dy0)
         t0 = None
