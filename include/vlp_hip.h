@@ -235,6 +235,10 @@ int vlp_adamw(long long n, float* p, const float* g, float* m, float* v, float l
               float beta2, float eps, float wd, float step_size, float bc2_sqrt, void* stream);
 int vlp_pack_conv(int dtype, int Co, int C, int KH, int KW, const float* w, void* wp, void* wt,
                   void* stream);
+/* vlp_pack_conv for n <= 48 convolutions in one launch: desc holds n rows of
+ * 6 values {w, wp, wt (device pointers; wp / wt may be 0), Co, C, KH*KW}
+ * (host memory, read during the call) */
+int vlp_pack_conv_batch(int dtype, int n, const long long* desc, void* stream);
 int vlp_pack_stem(int dtype, const float* w, void* wp, void* stream);
 int vlp_unpack_conv_grad(int Co, int C, int KH, int KW, const float* ws, float* g, void* stream);
 int vlp_unpack_stem_grad(const float* ws, float* g, void* stream);

@@ -339,3 +339,26 @@ def test_colsum(ops, M, N, ld, off):
     torch.cuda.synchronize()
     ref = x[:, :N].float().sum(0) + 0.5
     assert (out - ref).abs().max().item() < 1e-3 * (1 + ref.abs().max().item())
+
+
+@pytest.mark.parametrize("dt", DT)
+def test_pack_conv_batch(ops, dt):
+    """One-launch packing of many convs == per-conv vlp_pack_conv (bit-exact)."""
+    torch.manual_seed(10)
+    shapes = [(64, 64, 3, 3), (128, 64, 1, 1), (256, 128, 3, 3), (512, 512, 3, 3), (128, 64, 3, 3)]
+    entries, refs = [], []
+    for Co, C, KH, KW in shapes:
+        w = torch.randn(Co, C, KH, KW, device="cuda")
+        wp = torch.empty(Co, KH, KW, C, dtype=dt, device="cuda")
+        wt = torch.empty(C, KH, KW, Co, dtype=dt, device="cuda")
+        rp, rt = torch.empty_like(wp), torch.empty_like(wt)
+        ops.pack_conv(w, rp, rt)
+        entries.append((w, wp, wt))
+        refs.append((rp, rt))
+    entries[1] = (entries[1][0], entries[1][1], None)   # wt optional
+    ops.pack_conv_batch_run(ops.pack_conv_batch(entries[0][1], entries))
+    torch.cuda.synchronize()
+    for i, ((w, wp, wt), (rp, rt)) in enumerate(zip(entries, refs)):
+        assert torch.equal(wp, rp), i
+        if wt is not None:
+            assert torch.equal(wt, rt), i

@@ -44,6 +44,41 @@ __global__ void pack_conv_kernel(int Co, int C, int KH, int KW, const float* __r
   }
 }
 
+// All convolutions of the tower packed in one launch (blockIdx.y = conv).
+// wp: thread per (co, c) -> 16-bit stores coalesced over c for each tap;
+// wt: thread per (c, co) -> stores coalesced over co (the strided fp32 reads
+// hit the lines the other taps of the same (co, c) just pulled in).
+constexpr int kPackMax = 48;
+struct PackDesc {
+  const float* w;
+  void* wp;
+  void* wt;
+  int Co, C, T;
+};
+struct PackBatch {
+  PackDesc d[kPackMax];
+};
+template <typename T>
+__global__ void __launch_bounds__(256) pack_conv_batch_kernel(PackBatch b) {
+  const PackDesc& d = b.d[blockIdx.y];
+  const int n = d.Co * d.C;
+  T* wp = (T*)d.wp;
+  T* wt = (T*)d.wt;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < 2 * n; i += gridDim.x * 256) {
+    if (i < n) {
+      if (!wp) continue;
+      const int co = i / d.C, c = i - co * d.C;
+      const float* src = d.w + (size_t)i * d.T;
+      for (int t = 0; t < d.T; ++t) wp[((size_t)co * d.T + t) * d.C + c] = from_f<T>(src[t]);
+    } else {
+      if (!wt) continue;
+      const int j = i - n, c = j / d.Co, co = j - c * d.Co;
+      const float* src = d.w + ((size_t)co * d.C + c) * d.T;
+      for (int t = 0; t < d.T; ++t) wt[((size_t)c * d.T + t) * d.Co + co] = from_f<T>(src[t]);
+    }
+  }
+}
+
 // stem [64][3][7][7] -> Wp[64][kh:8][kw:8][c:4] (zeros outside)
 template <typename T>
 __global__ void pack_stem_kernel(const float* __restrict__ w, T* __restrict__ wp) {
@@ -96,6 +131,25 @@ VLP_EXPORT int vlp_adamw(long long n, float* p, const float* g, float* m, float*
   if (n <= 0) return 0;
   hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (size_t)n, p, g,
                      m, v, lr, beta1, beta2, eps, wd, step_size, bc2_sqrt);
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_pack_conv_batch(int dtype, int n, const long long* desc, void* stream) {
+  if (n < 1 || n > kPackMax) return (int)hipErrorInvalidValue;
+  PackBatch b;
+  int maxn = 0;
+  for (int i = 0; i < n; ++i) {
+    const long long* e = desc + 6 * i;
+    b.d[i] = PackDesc{(const float*)e[0], (void*)e[1], (void*)e[2], (int)e[3], (int)e[4], (int)e[5]};
+    if (e[3] * e[4] > maxn) maxn = (int)(e[3] * e[4]);
+  }
+  int gx = (2 * maxn + 255) / 256;
+  if (gx > 2048) gx = 2048;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == VLP_BF16)
+    hipLaunchKernelGGL(pack_conv_batch_kernel<bf16>, dim3(gx, n), dim3(256), 0, st, b);
+  else
+    hipLaunchKernelGGL(pack_conv_batch_kernel<float>, dim3(gx, n), dim3(256), 0, st, b);
   return (int)hipGetLastError();
 }
 

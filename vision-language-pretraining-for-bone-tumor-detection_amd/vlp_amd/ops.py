@@ -377,6 +377,25 @@ def pack_conv(w, wp, wt):
     lib().vlp_pack_conv(dcode(ref), Co, C, KH, KW, ptr(w), ptr(wp), ptr(wt), _s())
 
 
+def pack_conv_batch(dtype_ref, entries):
+    """entries: [(w fp32 [Co][C][KH][KW], wp, wt)] packed in one launch.
+    Returns the ctypes descriptor table (reusable with pack_conv_batch_run)."""
+    import ctypes
+    rows = []
+    for w, wp, wt in entries:
+        Co, C, KH, KW = w.shape
+        rows += [w.data_ptr(), wp.data_ptr() if wp is not None else 0, wt.data_ptr() if wt is not None else 0,
+                 Co, C, KH * KW]
+    table = (ctypes.c_longlong * len(rows))(*rows)
+    return (dcode(dtype_ref), len(entries), table)
+
+
+def pack_conv_batch_run(desc):
+    import ctypes
+    code, n, table = desc
+    lib().vlp_pack_conv_batch(code, n, ctypes.addressof(table), _s())
+
+
 def pack_stem(w, wp):
     lib().vlp_pack_stem(dcode(wp), ptr(w), ptr(wp), _s())
 

@@ -219,12 +219,15 @@ class ResNet34Tower(ArenaModule):
     def pack_weights(self):
         """fp32 master (timm layout) -> GEMM operand layouts in the compute dtype."""
         ws = self._workspace()
-        for c in self._convs.values():
-            w = self.arena.view(c.key + ".weight")
-            if c.key == "conv1":
-                ops.pack_stem(w, ws["conv1.wp"])
-            else:
-                ops.pack_conv(w, ws[c.key + ".wp"], ws[c.key + ".wt"])
+        key = ("pack_desc", self.arena.data.data_ptr())
+        desc = ws.get(key)
+        if desc is None:   # one launch for every 3x3 / 1x1 conv (pointers are stable per arena)
+            entries = [(self.arena.view(c.key + ".weight"), ws[c.key + ".wp"], ws[c.key + ".wt"])
+                       for c in self._convs.values() if c.key != "conv1"]
+            desc = ops.pack_conv_batch(entries[0][1], entries)
+            ws[key] = desc
+        ops.pack_conv_batch_run(desc)
+        ops.pack_stem(self.arena.view("conv1.weight"), ws["conv1.wp"])
         return ws
 
     # ---------------- BN helpers ----------------
