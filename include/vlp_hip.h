@@ -143,8 +143,13 @@ int vlp_bn_bwd_apply(int dtype, long long M, int C, const void* dout, const floa
                      void* dy_b, void* g_out, void* dyT_a, void* dyT_b, void* stream);
 int vlp_bn_param_grad(int C, const double* sum_g, const double* sum_gx, float* dgamma,
                       float* dbeta, void* stream);
+/* out = maxpool3x3/2(relu(sc*y + sh)), idx = argmax tap (0..8) per element;
+ * yarg (optional): y at the argmax, so the stem BN's backward sums can be taken
+ * per pooled output (g*[out>0]*xhat(yarg)) by the layer-1 data-gradient
+ * epilogue (vlp_conv_dgrad_relu with relu_out = out, y = yarg) instead of a
+ * pass over the full-resolution y */
 int vlp_maxpool_fwd(int dtype, int N, int H, int W, int C, const void* y, const float* sc,
-                    const float* sh, void* out, uint8_t* idx, void* stream);
+                    const float* sh, void* out, uint8_t* idx, void* yarg, void* stream);
 /* stem backward, pass 1: g = dp routed to each window's recorded argmax, masked by
  * the stem ReLU; accumulates sum g and sum g*xhat(y) (g itself is not stored) */
 int vlp_maxpool_bwd(int dtype, int N, int H, int W, int C, const void* dp, const uint8_t* idx,

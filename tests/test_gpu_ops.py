@@ -362,3 +362,37 @@ def test_pack_conv_batch(ops, dt):
         assert torch.equal(wp, rp), i
         if wt is not None:
             assert torch.equal(wt, rt), i
+
+
+@pytest.mark.parametrize("dt", DT)
+def test_maxpool_fwd_argmax_value(ops, dt):
+    """maxpool 3x3/2 over relu(sc*y+sh): pooled values, argmax taps and the
+    pre-BN y at the argmax (yarg) against torch."""
+    torch.manual_seed(11)
+    N, H, W, C = 2, 15, 16, 64
+    y = torch.randn(N, H, W, C).to(dt)
+    sc, sh = torch.randn(C), torch.randn(C) * 0.5
+    z = torch.relu(y.float() * sc + sh)
+    ref, ridx = F.max_pool2d(nchw(z), 3, 2, 1, return_indices=True)
+    Ho, Wo = ref.shape[2], ref.shape[3]
+    out = torch.empty(N, Ho, Wo, C, dtype=dt, device="cuda")
+    idx = torch.empty(N, Ho, Wo, C, dtype=torch.uint8, device="cuda")
+    yarg = torch.empty_like(out)
+    ops.maxpool_fwd(y.cuda(), sc.cuda(), sh.cuda(), out, idx, yarg)
+    torch.cuda.synchronize()
+    # (the kernel rounds sc*y+sh as one fma: compare within an ulp-scale tolerance)
+    assert torch.allclose(nchw(out.float().cpu()), ref.to(dt).float(), rtol=1e-2 if dt == torch.bfloat16 else 1e-5,
+                          atol=1e-6)
+    # value of y at the recorded tap
+    t = idx.long().cpu()
+    ho = torch.arange(Ho).view(1, Ho, 1, 1) * 2 - 1 + t // 3
+    wo = torch.arange(Wo).view(1, 1, Wo, 1) * 2 - 1 + t % 3
+    n = torch.arange(N).view(N, 1, 1, 1).expand_as(t)
+    c = torch.arange(C).view(1, 1, 1, C).expand_as(t)
+    ok = (ho >= 0) & (ho < H) & (wo >= 0) & (wo < W)
+    g = y[n, ho.clamp(0, H - 1), wo.clamp(0, W - 1), c]
+    assert ok.all()
+    assert torch.equal(yarg.cpu(), g)
+    # the recorded tap holds the window maximum
+    assert torch.allclose(z[n, ho, wo, c].to(dt).float(), out.float().cpu(),
+                          rtol=1e-2 if dt == torch.bfloat16 else 1e-5, atol=1e-6)

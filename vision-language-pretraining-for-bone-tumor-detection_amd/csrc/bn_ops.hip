@@ -433,7 +433,7 @@ template <typename T>
 __global__ void __launch_bounds__(256)
 maxpool_fwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const T* __restrict__ y,
                    const float* __restrict__ sc, const float* __restrict__ sh, T* __restrict__ out,
-                   uint8_t* __restrict__ idx) {
+                   uint8_t* __restrict__ idx, T* __restrict__ yarg) {
   constexpr int E = Chunk<T>::N;
   const int cpr = C / E;
   const unsigned total = (unsigned)N * Ho * Wo * cpr;
@@ -449,10 +449,10 @@ maxpool_fwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const T* __restri
     unsigned t = p / Wo;
     int ho = (int)(t % Ho);
     int n = (int)(t / Ho);
-    float best[E], v[E];
+    float best[E], v[E], ya[E];
     uint8_t bi[E];
 #pragma unroll
-    for (int j = 0; j < E; ++j) { best[j] = -INFINITY; bi[j] = 0; }
+    for (int j = 0; j < E; ++j) { best[j] = -INFINITY; bi[j] = 0; ya[j] = 0.f; }
     for (int kh = 0; kh < 3; ++kh) {
       int h = ho * 2 - 1 + kh;
       if ((unsigned)h >= (unsigned)H) continue;
@@ -463,11 +463,12 @@ maxpool_fwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const T* __restri
 #pragma unroll
         for (int j = 0; j < E; ++j) {
           float q = fmaxf(fmaf(v[j], a[j], b[j]), 0.f);
-          if (q > best[j]) { best[j] = q; bi[j] = (uint8_t)(kh * 3 + kw); }
+          if (q > best[j]) { best[j] = q; bi[j] = (uint8_t)(kh * 3 + kw); ya[j] = v[j]; }
         }
       }
     }
     stg16(out + (size_t)p * C + c0, Chunk<T>::pack(best));
+    if (yarg) stg16(yarg + (size_t)p * C + c0, Chunk<T>::pack(ya));
     if constexpr (E == 8) {
       uint2 packed;
       packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((unsigned)bi[3] << 24);
@@ -830,17 +831,17 @@ VLP_EXPORT int vlp_bn_param_grad(int C, const double* sum_g, const double* sum_g
 }
 
 VLP_EXPORT int vlp_maxpool_fwd(int dtype, int N, int H, int W, int C, const void* y, const float* sc,
-                               const float* sh, void* out, uint8_t* idx, void* stream) {
+                               const float* sh, void* out, uint8_t* idx, void* yarg, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
   int epc = dtype == VLP_BF16 ? 8 : 4;
   size_t n = (size_t)N * Ho * Wo * (C / epc);
   if (dtype == VLP_BF16)
     hipLaunchKernelGGL(maxpool_fwd_kernel<bf16>, dim3(ew_grid(n)), dim3(256), 0, st, N, H, W, C, Ho,
-                       Wo, (const bf16*)y, sc, sh, (bf16*)out, idx);
+                       Wo, (const bf16*)y, sc, sh, (bf16*)out, idx, (bf16*)yarg);
   else
     hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, st, N, H, W, C, Ho,
-                       Wo, (const float*)y, sc, sh, (float*)out, idx);
+                       Wo, (const float*)y, sc, sh, (float*)out, idx, (float*)yarg);
   return (int)hipGetLastError();
 }
 

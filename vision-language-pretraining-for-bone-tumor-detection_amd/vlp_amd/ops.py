@@ -214,9 +214,9 @@ def bn_param_grad(sum_g, sum_gx, dgamma, dbeta):
     lib().vlp_bn_param_grad(dgamma.numel(), ptr(sum_g), ptr(sum_gx), ptr(dgamma), ptr(dbeta), _s())
 
 
-def maxpool_fwd(y, sc, sh, out, idx):
+def maxpool_fwd(y, sc, sh, out, idx, yarg=None):
     N, H, W, C = y.shape
-    lib().vlp_maxpool_fwd(dcode(y), N, H, W, C, ptr(y), ptr(sc), ptr(sh), ptr(out), ptr(idx), _s())
+    lib().vlp_maxpool_fwd(dcode(y), N, H, W, C, ptr(y), ptr(sc), ptr(sh), ptr(out), ptr(idx), ptr(yarg), _s())
 
 
 def maxpool_bwd(dp, idx, y, sc, sh, mean, istd, sum_g, sum_gx, stat_rep=1):

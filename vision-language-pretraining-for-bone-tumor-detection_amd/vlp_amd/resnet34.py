@@ -275,8 +275,9 @@ class ResNet34Tower(ArenaModule):
         Hq, Wq = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
         p = torch.empty(N, Hq, Wq, 64, dtype=T, device=dev)
         idx = torch.empty(N, Hq, Wq, 64, dtype=torch.uint8, device=dev)
-        ops.maxpool_fwd(y0, sc0, sh0, p, idx)
-        saved["y0"], saved["idx"] = y0, idx
+        yarg = torch.empty_like(p) if training else None   # y0 at each window's argmax
+        ops.maxpool_fwd(y0, sc0, sh0, p, idx, yarg)
+        saved["y0"], saved["idx"], saved["yarg"] = y0, idx, yarg
         xcur = p
         blocks = []
         for pre, has_ds in self._blocks:
@@ -387,7 +388,17 @@ class ResNet34Tower(ArenaModule):
             # the gradient reaching block bi-1 passes its output ReLU and feeds its bn2:
             # when that block has no downsample branch, mask + reduce in this epilogue
             prev = self._blocks[bi - 1] if bi > 0 else None
-            if prev is not None and not prev[1]:
+            stem_sums = bi == 0 and saved.get("yarg") is not None
+            if stem_sums:
+                # block 0's input is the maxpool output p = relu(bn1(y0)) at each window's
+                # argmax: its mask and the stem BN's backward sums (xhat of y0 at the
+                # argmax) are taken per pooled output here, replacing a full-resolution pass
+                _, _, mu0, is0 = self._coef(ws, "bn1")
+                sg0f, sgx0f = self._bstat(ws, "bn1", full=True)
+                dx = ops.conv_dgrad_relu(dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, x, saved["yarg"],
+                                         mu0, is0, sg0f, sgx0f, addend=addend, stat_rep=STAT_REP)
+                dout_masked = True
+            elif prev is not None and not prev[1]:
                 kp = prev[0] + ".bn2"
                 _, _, mup, isp = self._coef(ws, kp)
                 sgpf, sgxpf = self._bstat(ws, kp, full=True)
@@ -404,7 +415,8 @@ class ResNet34Tower(ArenaModule):
         y0, idx = saved["y0"], saved["idx"]
         sc0, sh0, mu0, is0 = self._coef(ws, "bn1")
         sg0f, sgx0f = self._bstat(ws, "bn1", full=True)
-        ops.maxpool_bwd(dout, idx, y0, sc0, sh0, mu0, is0, sg0f, sgx0f, stat_rep=STAT_REP)
+        if saved.get("yarg") is None:
+            ops.maxpool_bwd(dout, idx, y0, sc0, sh0, mu0, is0, sg0f, sgx0f, stat_rep=STAT_REP)
         ops.bn_grad_rep(STAT_REP, 64, sg0f, sgx0f, self.arena.gview("bn1.weight"), self.arena.gview("bn1.bias"))
         sg0, sgx0 = sg0f[:64], sgx0f[:64]
         dy0 = torch.empty_like(y0)
