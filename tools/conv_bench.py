@@ -52,7 +52,8 @@ def main():
             elif op == "dgrad":
                 fn = lambda: ops.conv_dgrad(dy, wt, H, W, C, KH, KW, S, P)  # noqa: E731
             else:
-                fn = lambda: ops.conv_wgrad(dy, x, KH, KW, S, P, dws)  # noqa: E731
+                gw = torch.empty(Co, C, KH, KW, device=dev)
+                fn = lambda: ops.conv_wgrad_into(dy, x, KH, KW, S, P, gw)  # noqa: E731
             for _ in range(3):
                 fn()
             torch.cuda.synchronize()

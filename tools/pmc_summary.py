@@ -8,9 +8,9 @@ from collections import defaultdict
 
 
 def short(k):
-    m = re.search(r"gemm_ms_kernelILi(\d+)ELi(\d+)E.*?NS_\d+(\w+?)I", k)
+    m = re.search(r"gemm_(\w+?)_kernelILi(\d+)ELi(\d+)E.*?NS_\d+(\w+?)I", k)
     if m:
-        return f"gemm{m.group(1)}x{m.group(2)}:{m.group(3)}"
+        return f"gemm_{m.group(1)}{m.group(2)}x{m.group(3)}:{m.group(4)}"
     return k[:60]
 
 

@@ -1431,6 +1431,11 @@ template <typename T, class LA, class LB, class EP>
 inline int gemm_short(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
                       hipStream_t st) {
   if constexpr (use_bk<T, LA, LB>()) {
+    // 64 x 192 tiles (3 taps of 64 channels) on the two-K-tiles-in-flight engine:
+    // the 4-wave 64 x 128 ring kept one K-tile in flight and was latency-bound
+    static const int short_big = getenv("VLP_SHORT_BIG") ? atoi(getenv("VLP_SHORT_BIG")) : 1;
+    if (gemm_variant() >= 5 && short_big && N % 192 == 0)
+      return launch_gemm_big<64, 192, 1, 4>(M, N, K, ksplit, la, lb, ep, st);
     if (gemm_variant() >= 4) return launch_gemm_bk<64, 128, 1, 4>(M, N, K, ksplit, la, lb, ep, st);
   }
   if constexpr (use_ms<T, LA, LB>()) {
