@@ -57,12 +57,14 @@ int vlp_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, int N, i
                    void* stream);
 /* dgrad fused with the next block's output ReLU and BN2 backward sums:
  * g = (dgrad + addend) * (relu_out > 0); stat1 += sum g, stat2 += sum g*(y-mean)*invstd
- * (replaces the separate bn_bwd_reduce pass over dx, out, y2) */
+ * (replaces the separate bn_bwd_reduce pass over dx, out, y2).  Exactly one of
+ * relu_out (the activation) and relu_mask (its sign bits as written by
+ * vlp_bn_add_relu / vlp_maxpool_fwd: bit e&7 of byte e>>3 for element e) is given. */
 int vlp_conv_dgrad_relu(int dtype, const void* dy, const void* wt, void* g, int N, int H, int W,
                         int C, int Co, int KH, int KW, int S, int P, const void* addend,
-                        const void* relu_out, const void* y, const float* mean,
-                        const float* invstd, double* stat1, double* stat2, int stat_rep,
-                        void* stream);
+                        const void* relu_out, const uint8_t* relu_mask, const void* y,
+                        const float* mean, const float* invstd, double* stat1, double* stat2,
+                        int stat_rep, void* stream);
 /* Weight gradient as split-K fp32 slabs: split s of the pixel reduction writes
  * split_ws[s][Co][KH][KW][C] (plain stores, no atomics); *nsplit receives the
  * split count (<= ws_floats / (Co*KH*KW*C)).  vlp_conv_wgrad_fold then sums the
@@ -123,9 +125,11 @@ int vlp_bn_grad_rep(int rep, int C, double* sum_g, double* sum_gx, double* sum_g
 int vlp_bn_eval_coeffs(int C, const float* gamma, const float* beta, const float* running_mean,
                        const float* running_var, float eps, float* scale, float* shift,
                        void* stream);
-/* out = relu(sc*y + sh + idt'), idt' = idt (scd == NULL) or scd*idt + shd; idt == NULL: relu(sc*y + sh) */
+/* out = relu(sc*y + sh + idt'), idt' = idt (scd == NULL) or scd*idt + shd; idt == NULL: relu(sc*y + sh).
+ * relu_mask (optional, bf16 only): out's sign bits, byte e>>3 bit e&7 = (out[e] > 0) */
 int vlp_bn_add_relu(int dtype, long long M, int C, const void* y, const float* sc, const float* sh,
-                    const void* idt, const float* scd, const float* shd, void* out, void* stream);
+                    const void* idt, const float* scd, const float* shd, void* out, uint8_t* relu_mask,
+                    void* stream);
 /* g = dout * (mask > 0) (dout may be a broadcast [N][C]/HW gradient `dbc`);
  * sum_g += sum g, sum_ga += sum g*xhat(ya), sum_gb += sum g*xhat(yb) */
 int vlp_bn_bwd_reduce(int dtype, long long M, int C, const void* dout, const float* dbc, int HW,
@@ -149,7 +153,8 @@ int vlp_bn_param_grad(int C, const double* sum_g, const double* sum_gx, float* d
  * epilogue (vlp_conv_dgrad_relu with relu_out = out, y = yarg) instead of a
  * pass over the full-resolution y */
 int vlp_maxpool_fwd(int dtype, int N, int H, int W, int C, const void* y, const float* sc,
-                    const float* sh, void* out, uint8_t* idx, void* yarg, void* stream);
+                    const float* sh, void* out, uint8_t* idx, void* yarg, uint8_t* relu_mask,
+                    void* stream);
 /* stem backward, pass 1: g = dp routed to each window's recorded argmax, masked by
  * the stem ReLU; accumulates sum g and sum g*xhat(y) (g itself is not stored) */
 int vlp_maxpool_bwd(int dtype, int N, int H, int W, int C, const void* dp, const uint8_t* idx,

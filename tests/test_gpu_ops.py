@@ -199,15 +199,31 @@ def test_conv_dgrad_bn_epilogue(ops, dt, H, W):
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("case", [(2, 10, 10, 64, 64, 1), (2, 4, 128, 64, 64, 1), (2, 12, 12, 64, 128, 2)])
 @pytest.mark.parametrize("with_add", [False, True])
-def test_conv_dgrad_relu_epilogue(ops, dt, case, with_add):
+@pytest.mark.parametrize("bits", [False, True])
+def test_conv_dgrad_relu_epilogue(ops, dt, case, with_add, bits):
     """g = (dgrad + addend) * (relu_out > 0) and the next block's bn2 sums
-    (vlp_conv_dgrad_relu, the fused replacement of the bn_bwd_reduce pass)."""
+    (vlp_conv_dgrad_relu, the fused replacement of the bn_bwd_reduce pass);
+    bits: the ReLU sign as the uint8 bit mask vlp_bn_add_relu writes."""
+    if bits and dt != torch.bfloat16:
+        pytest.skip("bit masks are written by the bf16 producers only")
     N, H, W, C, Co, S = case
     torch.manual_seed(5)
     Ho, Wo = (H - 1) // S + 1, (W - 1) // S + 1
     dy = torch.randn(N, Co, Ho, Wo).to(dt).float()
     w = (torch.randn(Co, C, 3, 3) * 0.05).to(dt).float()
     relu_out = torch.relu(torch.randn(N, C, H, W)).to(dt).float()
+    rarg = nhwc(relu_out).to(dt).cuda()
+    if bits:
+        # the producer: relu(1*x + 0) with its sign bits, bit e&7 of byte e>>3
+        pre = nhwc(torch.randn(N, C, H, W)).to(dt).cuda()
+        act = torch.empty_like(pre)
+        rarg = torch.empty(pre.numel() // 8, dtype=torch.uint8, device="cuda")
+        ops.bn_add_relu(pre, torch.ones(C, device="cuda"), torch.zeros(C, device="cuda"), None, None, None, act,
+                        relu_mask=rarg)
+        torch.cuda.synchronize()
+        relu_out = nchw(act.float().cpu())
+        bitref = ((act.view(-1, 8) > 0).to(torch.int32) << torch.arange(8, device="cuda")).sum(1)
+        assert torch.equal(rarg.to(torch.int32), bitref)
     y2 = torch.randn(N, C, H, W).to(dt).float()
     add = torch.randn(N, C, H, W).to(dt).float() if with_add else None
     mu, ist = torch.randn(C) * 0.1, torch.rand(C) + 0.5
@@ -222,7 +238,7 @@ def test_conv_dgrad_relu_epilogue(ops, dt, case, with_add):
     ops.pack_conv(w.cuda(), None, wt)
     s1 = torch.zeros(C, dtype=torch.float64, device="cuda")
     s2 = torch.zeros_like(s1)
-    g = ops.conv_dgrad_relu(nhwc(dy).to(dt).cuda(), wt, H, W, C, 3, 3, S, 1, nhwc(relu_out).to(dt).cuda(),
+    g = ops.conv_dgrad_relu(nhwc(dy).to(dt).cuda(), wt, H, W, C, 3, 3, S, 1, rarg,
                             nhwc(y2).to(dt).cuda(), mu.cuda(), ist.cuda(), s1, s2,
                             addend=None if add is None else nhwc(add).to(dt).cuda())
     torch.cuda.synchronize()

@@ -18,6 +18,20 @@ namespace vlp {
 
 constexpr int kEwThreads = 256;
 
+// bit j = (bf16 element j of the 16-B chunk > 0): the ReLU mask of a stored
+// activation, 1/16 of its bytes (read back by the data-gradient epilogues)
+__device__ __forceinline__ uint8_t relu_bits8(const uint4& u) {
+  const unsigned w[4] = {u.x, u.y, u.z, u.w};
+  unsigned m = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const unsigned lo = w[q] & 0xffffu, hi = w[q] >> 16;
+    m |= (unsigned)((lo & 0x8000u) == 0 && lo != 0) << (2 * q);
+    m |= (unsigned)((hi & 0x8000u) == 0 && hi != 0) << (2 * q + 1);
+  }
+  return (uint8_t)m;
+}
+
 static inline int ew_blocks(size_t work, int per_block = kEwThreads, int cap = 8192) {
   size_t b = (work + per_block - 1) / per_block;
   if (b > (size_t)cap) b = cap;
@@ -166,7 +180,8 @@ template <typename T, bool HAS_IDT>
 __global__ void __launch_bounds__(256)
 bn_add_relu_kernel(unsigned nchunks, int cpr, const T* __restrict__ y, const float* __restrict__ sc,
                    const float* __restrict__ sh, const T* __restrict__ idt,
-                   const float* __restrict__ scd, const float* __restrict__ shd, T* __restrict__ out) {
+                   const float* __restrict__ scd, const float* __restrict__ shd, T* __restrict__ out,
+                   uint8_t* __restrict__ rmask) {
   constexpr int E = Chunk<T>::N;
   const unsigned tid = blockIdx.x * blockDim.x + threadIdx.x;
   const unsigned stride = gridDim.x * blockDim.x;   // multiple of cpr
@@ -190,7 +205,11 @@ bn_add_relu_kernel(unsigned nchunks, int cpr, const T* __restrict__ y, const flo
 #pragma unroll
       for (int j = 0; j < E; ++j) u[j] = fmaxf(fmaf(u[j], a[j], b[j]), 0.f);
     }
-    stg16(out + (size_t)i * E, Chunk<T>::pack(u));
+    const uint4 pk = Chunk<T>::pack(u);
+    stg16(out + (size_t)i * E, pk);
+    if constexpr (E == 8) {
+      if (rmask) rmask[i] = relu_bits8(pk);
+    }
   }
 }
 
@@ -433,7 +452,7 @@ template <typename T>
 __global__ void __launch_bounds__(256)
 maxpool_fwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const T* __restrict__ y,
                    const float* __restrict__ sc, const float* __restrict__ sh, T* __restrict__ out,
-                   uint8_t* __restrict__ idx, T* __restrict__ yarg) {
+                   uint8_t* __restrict__ idx, T* __restrict__ yarg, uint8_t* __restrict__ rmask) {
   constexpr int E = Chunk<T>::N;
   const int cpr = C / E;
   const unsigned total = (unsigned)N * Ho * Wo * cpr;
@@ -467,8 +486,12 @@ maxpool_fwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const T* __restri
         }
       }
     }
-    stg16(out + (size_t)p * C + c0, Chunk<T>::pack(best));
+    const uint4 pk = Chunk<T>::pack(best);
+    stg16(out + (size_t)p * C + c0, pk);
     if (yarg) stg16(yarg + (size_t)p * C + c0, Chunk<T>::pack(ya));
+    if constexpr (E == 8) {
+      if (rmask) rmask[((size_t)p * C + c0) >> 3] = relu_bits8(pk);
+    }
     if constexpr (E == 8) {
       uint2 packed;
       packed.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((unsigned)bi[3] << 24);
@@ -729,9 +752,10 @@ VLP_EXPORT int vlp_stat_reduce(int rep, int C, double* a, double* b, double* c, 
 
 VLP_EXPORT int vlp_bn_add_relu(int dtype, long long M, int C, const void* y, const float* sc,
                                const float* sh, const void* idt, const float* scd, const float* shd,
-                               void* out, void* stream) {
+                               void* out, uint8_t* relu_mask, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   int epc = dtype == VLP_BF16 ? 8 : 4;
+  if (relu_mask && dtype != VLP_BF16) return (int)hipErrorInvalidValue;
   unsigned n = (unsigned)((size_t)M * C / epc);
   int cpr = C / epc;
   if (256 % cpr) return (int)hipErrorInvalidValue;
@@ -739,17 +763,17 @@ VLP_EXPORT int vlp_bn_add_relu(int dtype, long long M, int C, const void* y, con
   if (dtype == VLP_BF16) {
     if (idt)
       hipLaunchKernelGGL((bn_add_relu_kernel<bf16, true>), g, dim3(256), 0, st, n, cpr, (const bf16*)y, sc,
-                         sh, (const bf16*)idt, scd, shd, (bf16*)out);
+                         sh, (const bf16*)idt, scd, shd, (bf16*)out, relu_mask);
     else
       hipLaunchKernelGGL((bn_add_relu_kernel<bf16, false>), g, dim3(256), 0, st, n, cpr, (const bf16*)y,
-                         sc, sh, (const bf16*)idt, scd, shd, (bf16*)out);
+                         sc, sh, (const bf16*)idt, scd, shd, (bf16*)out, relu_mask);
   } else {
     if (idt)
       hipLaunchKernelGGL((bn_add_relu_kernel<float, true>), g, dim3(256), 0, st, n, cpr, (const float*)y,
-                         sc, sh, (const float*)idt, scd, shd, (float*)out);
+                         sc, sh, (const float*)idt, scd, shd, (float*)out, nullptr);
     else
       hipLaunchKernelGGL((bn_add_relu_kernel<float, false>), g, dim3(256), 0, st, n, cpr,
-                         (const float*)y, sc, sh, (const float*)idt, scd, shd, (float*)out);
+                         (const float*)y, sc, sh, (const float*)idt, scd, shd, (float*)out, nullptr);
   }
   return (int)hipGetLastError();
 }
@@ -831,17 +855,19 @@ VLP_EXPORT int vlp_bn_param_grad(int C, const double* sum_g, const double* sum_g
 }
 
 VLP_EXPORT int vlp_maxpool_fwd(int dtype, int N, int H, int W, int C, const void* y, const float* sc,
-                               const float* sh, void* out, uint8_t* idx, void* yarg, void* stream) {
+                               const float* sh, void* out, uint8_t* idx, void* yarg, uint8_t* relu_mask,
+                               void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  if (relu_mask && dtype != VLP_BF16) return (int)hipErrorInvalidValue;
   int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
   int epc = dtype == VLP_BF16 ? 8 : 4;
   size_t n = (size_t)N * Ho * Wo * (C / epc);
   if (dtype == VLP_BF16)
     hipLaunchKernelGGL(maxpool_fwd_kernel<bf16>, dim3(ew_grid(n)), dim3(256), 0, st, N, H, W, C, Ho,
-                       Wo, (const bf16*)y, sc, sh, (bf16*)out, idx, (bf16*)yarg);
+                       Wo, (const bf16*)y, sc, sh, (bf16*)out, idx, (bf16*)yarg, relu_mask);
   else
     hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(ew_grid(n)), dim3(256), 0, st, N, H, W, C, Ho,
-                       Wo, (const float*)y, sc, sh, (float*)out, idx, (float*)yarg);
+                       Wo, (const float*)y, sc, sh, (float*)out, idx, (float*)yarg, nullptr);
   return (int)hipGetLastError();
 }
 

@@ -848,22 +848,34 @@ struct EpiDgradAdd {
 // is g = (conv_dgrad + addend) * (out_{b-1} > 0), and its bn2 needs sum(g),
 // sum(g * xhat(y2_{b-1})).  Fusing this here removes the separate reduction
 // pass over (dx, out, y2) and lets the next BN-backward apply read g directly.
-template <typename T>
+// BITS: the ReLU sign comes from a bit mask (1/16 of the activation's bytes);
+// a separate instantiation, so the activation path's registers are not shared
+template <typename T, bool BITS = false>
 struct EpiDgradRelu {
   static constexpr bool kStats = true;
   double* stat1; double* stat2; int stat_rep;
   T* g_out; const T* addend; int C;
   const T* relu_out; const T* y; const float* mean; const float* invstd;
+  const uint8_t* rmask;   // when set: bit (o & 7) of byte o >> 3 replaces relu_out[o] > 0
   __device__ v4f grad(int row, int col, v4f v, v4f& s1, v4f& s2) const {
     const size_t o = (size_t)row * C + col;
     if (addend) v += load4(addend + o);
-    const v4f r = load4(relu_out + o);
+    bool pos[4];
+    if constexpr (BITS) {
+      const unsigned b = rmask[o >> 3] >> (o & 7);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pos[j] = (b >> j) & 1u;
+    } else {
+      const v4f r = load4(relu_out + o);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pos[j] = r[j] > 0.f;
+    }
     const v4f yv = load4(y + o);
     const v4f mu = *reinterpret_cast<const v4f*>(mean + col);
     const v4f is = *reinterpret_cast<const v4f*>(invstd + col);
     v4f g;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) g[j] = r[j] > 0.f ? v[j] : 0.f;
+    for (int j = 0; j < 4; ++j) g[j] = pos[j] ? v[j] : 0.f;
     s1 = g;
     s2 = g * ((yv - mu) * is);
     return g;
@@ -875,7 +887,11 @@ struct EpiDgradRelu {
   __device__ void pre8(int row, int col, RowPre& p) const {
     const size_t o = (size_t)row * C + col;
     p.u[0] = addend ? ldg16(addend + o) : zero4();
-    p.u[1] = ldg16(relu_out + o);
+    if constexpr (BITS) {
+      p.u[1].x = rmask[o >> 3];
+    } else {
+      p.u[1] = ldg16(relu_out + o);
+    }
     p.u[2] = ldg16(y + o);
   }
   static constexpr int kCoefs = 2;
@@ -892,15 +908,24 @@ struct EpiDgradRelu {
   __device__ void row8c(int row, int col, const float (&v)[8], const RowPre& p, float (&s1)[8],
                         float (&s2)[8], FP cmu, FP cis) const {
     const size_t o = (size_t)row * C + col;
-    float a[8], r[8], yv[8], g[8], mu[8], is[8];
+    float a[8], yv[8], g[8], mu[8], is[8];
+    bool pos[8];
     Chunk<bf16>::unpack(p.u[0], a);
-    Chunk<bf16>::unpack(p.u[1], r);
+    if constexpr (BITS) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pos[j] = (p.u[1].x >> j) & 1u;
+    } else {
+      float r[8];
+      Chunk<bf16>::unpack(p.u[1], r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pos[j] = r[j] > 0.f;
+    }
     Chunk<bf16>::unpack(p.u[2], yv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) { mu[j] = cmu[col + j]; is[j] = cis[col + j]; }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      g[j] = r[j] > 0.f ? v[j] + a[j] : 0.f;
+      g[j] = pos[j] ? v[j] + a[j] : 0.f;
       s1[j] += g[j];
       s2[j] += g[j] * ((yv[j] - mu[j]) * is[j]);
     }
@@ -1251,14 +1276,15 @@ static int conv_dgrad_t(const void* dy, const void* wt, void* dx, ConvGeom g, co
 }
 
 // dgrad whose output is masked by a ReLU output and reduced for a BN backward
-template <typename T>
-static int conv_dgrad_relu_t(const void* dy, const void* wt, void* gout, ConvGeom g0, const void* addend,
-                             const void* relu_out, const void* y, const float* mean, const float* invstd,
-                             double* s1, double* s2, int rep, hipStream_t st) {
+template <typename T, bool BITS>
+static int conv_dgrad_relu_impl(const void* dy, const void* wt, void* gout, ConvGeom g0, const void* addend,
+                                const void* relu_out, const uint8_t* relu_mask, const void* y, const float* mean,
+                                const float* invstd, double* s1, double* s2, int rep, hipStream_t st) {
   ConvGeom g = g0;
   g.M = g.N * g.H * g.W;
   g.K = g.KH * g.KW * g.Co;
-  EpiDgradRelu<T> in{s1, s2, rep, (T*)gout, (const T*)addend, g.C, (const T*)relu_out, (const T*)y, mean, invstd};
+  EpiDgradRelu<T, BITS> in{s1, s2, rep, (T*)gout, (const T*)addend, g.C, (const T*)relu_out, (const T*)y, mean,
+                           invstd, relu_mask};
   if (g.S == 2) {
     for (int ph = 0; ph < 2; ++ph)
       for (int pw = 0; pw < 2; ++pw) {
@@ -1267,7 +1293,7 @@ static int conv_dgrad_relu_t(const void* dy, const void* wt, void* gout, ConvGeo
         if (Mc <= 0) continue;
         ConvDgradS2A<T> la{g, c, (const T*)dy, Mc, Kc};
         WtS2B<T> lb{(const T*)wt, g, c, Kc};
-        EpiS2Remap<EpiDgradRelu<T>> ep{s1, s2, rep, in, c, g.H, g.W};
+        EpiS2Remap<EpiDgradRelu<T, BITS>> ep{s1, s2, rep, in, c, g.H, g.W};
         const int r = gemm_auto<T>(Mc, g.C, Kc, 1, la, lb, ep, st);
         if (r) return r;
       }
@@ -1279,6 +1305,16 @@ static int conv_dgrad_relu_t(const void* dy, const void* wt, void* gout, ConvGeo
   ConvDgradA<T> la{g, (const T*)dy};
   KMat<T> lb{(const T*)wt, g.K, g.C, g.K};
   return gemm_auto<T>(g.M, g.C, g.K, 1, la, lb, in, st);
+}
+template <typename T>
+static int conv_dgrad_relu_t(const void* dy, const void* wt, void* gout, ConvGeom g0, const void* addend,
+                             const void* relu_out, const uint8_t* relu_mask, const void* y, const float* mean,
+                             const float* invstd, double* s1, double* s2, int rep, hipStream_t st) {
+  if (relu_mask)
+    return conv_dgrad_relu_impl<T, true>(dy, wt, gout, g0, addend, relu_out, relu_mask, y, mean, invstd, s1, s2,
+                                         rep, st);
+  return conv_dgrad_relu_impl<T, false>(dy, wt, gout, g0, addend, relu_out, relu_mask, y, mean, invstd, s1, s2,
+                                        rep, st);
 }
 
 template <typename T>
@@ -1453,14 +1489,17 @@ VLP_EXPORT int vlp_conv_dgrad(int dtype, const void* dy, const void* wt, void* d
 
 VLP_EXPORT int vlp_conv_dgrad_relu(int dtype, const void* dy, const void* wt, void* g, int N, int H,
                                    int W, int C, int Co, int KH, int KW, int S, int P,
-                                   const void* addend, const void* relu_out, const void* y,
-                                   const float* mean, const float* invstd, double* stat1,
+                                   const void* addend, const void* relu_out, const uint8_t* relu_mask,
+                                   const void* y, const float* mean, const float* invstd, double* stat1,
                                    double* stat2, int stat_rep, void* stream) {
   ConvGeom geo = make_geom(N, H, W, C, Co, KH, KW, S, P);
   hipStream_t st = (hipStream_t)stream;
+  if ((relu_out == nullptr) == (relu_mask == nullptr) || C % 8) return (int)hipErrorInvalidValue;
   if (dtype == VLP_BF16)
-    return conv_dgrad_relu_t<bf16>(dy, wt, g, geo, addend, relu_out, y, mean, invstd, stat1, stat2, stat_rep, st);
-  return conv_dgrad_relu_t<float>(dy, wt, g, geo, addend, relu_out, y, mean, invstd, stat1, stat2, stat_rep, st);
+    return conv_dgrad_relu_t<bf16>(dy, wt, g, geo, addend, relu_out, relu_mask, y, mean, invstd, stat1, stat2,
+                                   stat_rep, st);
+  return conv_dgrad_relu_t<float>(dy, wt, g, geo, addend, relu_out, relu_mask, y, mean, invstd, stat1, stat2,
+                                  stat_rep, st);
 }
 
 VLP_EXPORT int vlp_conv_wgrad(int dtype, const void* dy, const void* x, float* dw_ws, int N, int H,

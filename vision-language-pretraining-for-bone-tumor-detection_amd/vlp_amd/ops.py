@@ -78,13 +78,15 @@ def conv_dgrad(dy, wt, H, W, C, KH, KW, S, P, addend=None, y_bn=None, bn=None, s
 def conv_dgrad_relu(dy, wt, H, W, C, KH, KW, S, P, relu_out, y, mean, invstd, stat1, stat2,
                     addend=None, stat_rep=1):
     """g = (dgrad(dy) + addend) * (relu_out > 0), plus the BN backward sums of g
-    against y (the next block's bn2 input)."""
+    against y (the next block's bn2 input).  relu_out may be the activation or
+    its uint8 sign-bit mask (bn_add_relu / maxpool_fwd relu_mask)."""
     N, Ho, Wo, Co = dy.shape
     g = torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
+    bits = relu_out.dtype == torch.uint8
     tk = ktimer.begin(f"conv_dgrad[relu]{_tile_auto(C)}", 2.0 * N * Ho * Wo * Co * C * KH * KW)
     lib().vlp_conv_dgrad_relu(dcode(dy), ptr(dy), ptr(wt), ptr(g), N, H, W, C, Co, KH, KW, S, P,
-                              ptr(addend), ptr(relu_out), ptr(y), ptr(mean), ptr(invstd), ptr(stat1),
-                              ptr(stat2), int(stat_rep), _s())
+                              ptr(addend), None if bits else ptr(relu_out), ptr(relu_out) if bits else None,
+                              ptr(y), ptr(mean), ptr(invstd), ptr(stat1), ptr(stat2), int(stat_rep), _s())
     ktimer.end(tk)
     return g
 
@@ -186,11 +188,11 @@ def bn_eval_coeffs(gamma, beta, rm, rv, eps, scale, shift):
                              ptr(scale), ptr(shift), _s())
 
 
-def bn_add_relu(y, sc, sh, idt, scd, shd, out):
+def bn_add_relu(y, sc, sh, idt, scd, shd, out, relu_mask=None):
     C = y.shape[-1]
     M = y.numel() // C
     lib().vlp_bn_add_relu(dcode(y), M, C, ptr(y), ptr(sc), ptr(sh), ptr(idt), ptr(scd), ptr(shd),
-                          ptr(out), _s())
+                          ptr(out), ptr(relu_mask), _s())
 
 
 def bn_bwd_reduce(M, C, dout, dbc, HW, mask, ya, mean_a, istd_a, yb, mean_b, istd_b, sum_g, sum_ga,
@@ -214,9 +216,10 @@ def bn_param_grad(sum_g, sum_gx, dgamma, dbeta):
     lib().vlp_bn_param_grad(dgamma.numel(), ptr(sum_g), ptr(sum_gx), ptr(dgamma), ptr(dbeta), _s())
 
 
-def maxpool_fwd(y, sc, sh, out, idx, yarg=None):
+def maxpool_fwd(y, sc, sh, out, idx, yarg=None, relu_mask=None):
     N, H, W, C = y.shape
-    lib().vlp_maxpool_fwd(dcode(y), N, H, W, C, ptr(y), ptr(sc), ptr(sh), ptr(out), ptr(idx), ptr(yarg), _s())
+    lib().vlp_maxpool_fwd(dcode(y), N, H, W, C, ptr(y), ptr(sc), ptr(sh), ptr(out), ptr(idx), ptr(yarg),
+                          ptr(relu_mask), _s())
 
 
 def maxpool_bwd(dp, idx, y, sc, sh, mean, istd, sum_g, sum_gx, stat_rep=1):

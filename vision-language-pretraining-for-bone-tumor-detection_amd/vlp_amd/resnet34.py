@@ -276,8 +276,11 @@ class ResNet34Tower(ArenaModule):
         p = torch.empty(N, Hq, Wq, 64, dtype=T, device=dev)
         idx = torch.empty(N, Hq, Wq, 64, dtype=torch.uint8, device=dev)
         yarg = torch.empty_like(p) if training else None   # y0 at each window's argmax
-        ops.maxpool_fwd(y0, sc0, sh0, p, idx, yarg)
+        bits = training and T == torch.bfloat16              # ReLU sign bits of each block input
+        pm = torch.empty(p.numel() // 8, dtype=torch.uint8, device=dev) if bits else None
+        ops.maxpool_fwd(y0, sc0, sh0, p, idx, yarg, relu_mask=pm)
         saved["y0"], saved["idx"], saved["yarg"] = y0, idx, yarg
+        xmask = pm
         xcur = p
         blocks = []
         for pre, has_ds in self._blocks:
@@ -301,9 +304,10 @@ class ResNet34Tower(ArenaModule):
                                   stat_sumsq=ss, stat_rep=STAT_REP)
                 scd, shd = self._bn_finalize(ws, pre + ".downsample.1", Mb, training)
             out = torch.empty_like(y2)
-            ops.bn_add_relu(y2, sc2, sh2, yd if has_ds else xcur, scd, shd, out)
-            blocks.append({"x": xcur, "y1": y1, "a1": a1, "y2": y2, "yd": yd, "out": out})
-            xcur = out
+            om = torch.empty(out.numel() // 8, dtype=torch.uint8, device=dev) if bits else None
+            ops.bn_add_relu(y2, sc2, sh2, yd if has_ds else xcur, scd, shd, out, relu_mask=om)
+            blocks.append({"x": xcur, "xmask": xmask, "y1": y1, "a1": a1, "y2": y2, "yd": yd, "out": out})
+            xcur, xmask = out, om
         feat = torch.empty(N, 512, dtype=T, device=dev)
         ops.avgpool_fwd(xcur, feat)
         saved["blocks"] = blocks
@@ -395,14 +399,16 @@ class ResNet34Tower(ArenaModule):
                 # argmax) are taken per pooled output here, replacing a full-resolution pass
                 _, _, mu0, is0 = self._coef(ws, "bn1")
                 sg0f, sgx0f = self._bstat(ws, "bn1", full=True)
-                dx = ops.conv_dgrad_relu(dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, x, saved["yarg"],
+                rmask = B["xmask"] if B.get("xmask") is not None else x
+                dx = ops.conv_dgrad_relu(dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, rmask, saved["yarg"],
                                          mu0, is0, sg0f, sgx0f, addend=addend, stat_rep=STAT_REP)
                 dout_masked = True
             elif prev is not None and not prev[1]:
                 kp = prev[0] + ".bn2"
                 _, _, mup, isp = self._coef(ws, kp)
                 sgpf, sgxpf = self._bstat(ws, kp, full=True)
-                dx = ops.conv_dgrad_relu(dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, x,
+                rmask = B["xmask"] if B.get("xmask") is not None else x
+                dx = ops.conv_dgrad_relu(dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, rmask,
                                          blocks[bi - 1]["y2"], mup, isp, sgpf, sgxpf, addend=addend,
                                          stat_rep=STAT_REP)
                 dout_masked = True
