@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--cpu-sample-steps", type=int, default=3)
     ap.add_argument("--roofline-kernel", default="auto")
     ap.add_argument("--kernel-report", default="")
+    ap.add_argument("--pcie-steps", type=int, default=5,
+                    help="steps timed with the batch copied from pinned host memory (0: skip)")
     return ap.parse_args()
 
 
@@ -103,6 +105,45 @@ def cpu_baseline(args):
             "kind": "port",
             "sample": f"oracle fp32 CPU step (fwd+bwd+AdamW), bs={B}, {H}x{H}, T={T}, "
                       f"median of {len(times)} steps after 1 warm-up ({med:.2f} s/step)"}
+
+
+def pcie_inclusive(args, model, opt, world, dev):
+    """The SURVEY §8(d) step including the batch's H2D copy: the batch starts in
+    pinned host memory each step (as the reference's pin_memory DataLoader
+    hands it over) and goes up with non_blocking copies inside training_step.
+    Two forms: the reference's collated fp32 3-channel images (805 MB at
+    bs=256, 512^2) and the 1-channel uint8 upload (67 MB) that
+    vlp_stem_prep_u8 normalises on the device.  Reported beside `value`."""
+    from tests.golden.synth import synth_batch
+    b = synth_batch(args.batch, args.image_size, args.seq_len, 0, with_u8=True)
+    caps = {k: v.pin_memory() for k, v in b["caption_tokenized"].items()}
+    out = {}
+    for form, key in (("fp32_3ch", "x-ray"), ("u8_1ch", "x-ray-u8")):
+        host = {key: b[key].pin_memory(), "caption_tokenized": caps, "label": b["label"], "caption": b["caption"]}
+
+        def step():
+            opt.zero_grad()
+            loss = model.training_step(host)
+            loss.backward()
+            opt.step()
+        step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.pcie_steps):
+            step()
+        torch.cuda.synchronize()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        el = el.item()
+        out[form] = {"value": round(world * args.batch * args.pcie_steps / el, 2),
+                     "ms_per_step": round(el / args.pcie_steps * 1e3, 3),
+                     "h2d_mb_per_step": round(b[key].numel() * b[key].element_size() / 1e6, 1)}
+    out["unit"] = "image-text pairs/s"
+    out["steps"] = args.pcie_steps
+    return out
 
 
 def _traffic(family):
@@ -174,6 +215,7 @@ def main():
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     el = elapsed.item()
     tot = ktimer.totals().get(tk, (0.0, 0, 0.0))
+    pcie = pcie_inclusive(args, model, opt, world, dev) if args.pcie_steps > 0 else None
     ms_k, nl, flop_k = tot
     if rank == 0:
         pairs = world * args.batch * args.steps
@@ -206,6 +248,8 @@ def main():
                          "traffic": _traffic(tk)},
             "loss": round(loss.item(), 5),
         }
+        if pcie is not None:
+            res["pcie_inclusive"] = pcie
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(res), flush=True)
