@@ -107,6 +107,23 @@ def cpu_baseline(args):
                       f"median of {len(times)} steps after 1 warm-up ({med:.2f} s/step)"}
 
 
+def mfma_peak_measured(dev):
+    """Dense bf16 MFMA ceiling of this card (vlp_mfma_peak_probe), TFLOP/s."""
+    from vlp_amd._lib import lib
+    blocks, iters = 2048, 2000
+    out = torch.empty(blocks * 256, device=dev)
+    st = torch.cuda.current_stream(dev)
+    best = 0.0
+    for _ in range(4):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        lib().vlp_mfma_peak_probe(blocks, iters, out.data_ptr(), st.cuda_stream)
+        e1.record(st)
+        e1.synchronize()
+        best = max(best, blocks * 4 * iters * 8 * 16384 / (e0.elapsed_time(e1) * 1e-3) / 1e12)
+    return round(best, 1)
+
+
 def pcie_inclusive(args, model, opt, world, dev):
     """The SURVEY §8(d) step including the batch's H2D copy: the batch starts in
     pinned host memory each step (as the reference's pin_memory DataLoader
@@ -216,6 +233,7 @@ def main():
     el = elapsed.item()
     tot = ktimer.totals().get(tk, (0.0, 0, 0.0))
     pcie = pcie_inclusive(args, model, opt, world, dev) if args.pcie_steps > 0 else None
+    peak_meas = mfma_peak_measured(dev) if args.dtype == "bf16" else None
     ms_k, nl, flop_k = tot
     if rank == 0:
         pairs = world * args.batch * args.steps
@@ -244,7 +262,9 @@ def main():
             "roofline": {"bound": "mfma", "kernel": tk, "achieved": round(achieved, 2), "peak": peak,
                          "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                          "avg_launch_us": round(ms_k * 1e3 / max(nl, 1), 2), "launches": nl,
-                         "flop_per_launch": round(flop_k / max(nl, 1)), "traffic_unit": "HBM bytes/launch",
+                         "flop_per_launch": round(flop_k / max(nl, 1)), "peak_measured": peak_meas,
+                         "frac_of_measured": round(achieved / peak_meas, 4) if peak_meas else None,
+                         "traffic_unit": "HBM bytes/launch",
                          "traffic": _traffic(tk)},
             "loss": round(loss.item(), 5),
         }

@@ -32,6 +32,11 @@ extern "C" {
 #endif
 
 int vlp_abi_version(void);
+/* Diagnostic: register-only v_mfma_f32_16x16x32_bf16 chains (8 independent
+ * accumulators per wave, 4 waves per block) to measure the card's dense bf16
+ * MFMA ceiling next to the vendor figure.
+ * FLOP = blocks * 4 * iters * 8 * 16384; out: blocks * 256 floats. */
+int vlp_mfma_peak_probe(int blocks, int iters, float* out, void* stream);
 
 /* ---------------- image tower: convolutions ----------------
  * Replace the cuDNN conv fwd/dgrad/wgrad calls made by timm resnet34

@@ -1,0 +1,44 @@
+// Measured MFMA ceiling of the card the bench runs on (report the
+// vendor dense bf16 peak AND a microbenchmark of it).  Register-only
+// v_mfma_f32_16x16x32_bf16 chains, 8 independent accumulators per wave, two
+// waves per SIMD; no memory traffic inside the loop.
+#include "common.h"
+
+namespace vlp {
+
+constexpr int kProbeAcc = 8;
+
+__global__ void __launch_bounds__(256) mfma_peak_kernel(int iters, float* __restrict__ out) {
+  const int l = threadIdx.x;
+  v8bf a, b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a[j] = (__bf16)(0.001f * (float)((l + j) & 7));
+    b[j] = (__bf16)(0.002f * (float)((l * 3 + j) & 7));
+  }
+  v4f acc[kProbeAcc];
+#pragma unroll
+  for (int q = 0; q < kProbeAcc; ++q) acc[q] = v4f{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < iters; i += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < kProbeAcc; ++q)   // in place (dst = srcC in AGPRs): no accumulator copies
+        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[q]) : "v"(a), "v"(b));
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < kProbeAcc; ++q) s += acc[q][0] + acc[q][1] + acc[q][2] + acc[q][3];
+  out[blockIdx.x * 256 + l] = s;
+}
+
+}  // namespace vlp
+
+using namespace vlp;
+
+// FLOP = blocks * 4 waves * iters * kProbeAcc * 16*16*32*2 (iters: a multiple of 4); out: blocks*256 floats
+VLP_EXPORT int vlp_mfma_peak_probe(int blocks, int iters, float* out, void* stream) {
+  if (blocks < 1 || iters < 4 || iters % 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(mfma_peak_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, iters, out);
+  return (int)hipGetLastError();
+}
