@@ -98,12 +98,13 @@ class ClipStepFn(torch.autograd.Function):
         img_t, txt_t, head = model.image_tower, model.text_tower, model.head
         training = model.training
         feat_img, sv_img = img_t.run_forward(x, training, x_u8=x_u8)
-        h_last, sv_txt = txt_t.run_forward(input_ids, attention_mask, token_type_ids, training)
+        # only the CLS token's last hidden state is used (TextEncoder, :57-60)
+        h_last, sv_txt = txt_t.run_forward(input_ids, attention_mask, token_type_ids, training, cls_only=True)
         B, Tn = input_ids.shape
         D, E = txt_t.cfg.hidden, head.embedding_dim
         wT = head.wcopy()
         ie, inorm = _project_normalize(head, wT, feat_img, 512, 512, "image_projection", E)
-        te, tnorm = _project_normalize(head, wT, h_last, Tn * D, D, "text_projection", E)
+        te, tnorm = _project_normalize(head, wT, h_last, D, D, "text_projection", E)
         rank, world = vdist.world()
         ie_all = vdist.all_gather_rows(ie)
         te_all = vdist.all_gather_rows(te)
@@ -138,7 +139,7 @@ class ClipStepFn(torch.autograd.Function):
         ops.scale(small[2:3], gs, head.arena.gview("logit_scale"))
         dfeat_img = _project_backward(head, wT, feat_img, 512, 512, "image_projection", E, ie, inorm,
                                       g_img, gs)
-        dcls = _project_backward(head, wT, h_last, Tn * D, D, "text_projection", E, te, tnorm,
+        dcls = _project_backward(head, wT, h_last, D, D, "text_projection", E, te, tnorm,
                                  g_txt, gs)
         # data parallel: SUM all-reduce of the flat gradient arenas, the head and
         # text tower's launched while the (much longer) image backward runs

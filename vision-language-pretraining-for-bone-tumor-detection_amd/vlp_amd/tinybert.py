@@ -175,7 +175,12 @@ class TinyBertTower(ArenaModule):
         return t if bias else t.view(3 * D, D)
 
     # ---------------- forward ----------------
-    def run_forward(self, input_ids, attention_mask=None, token_type_ids=None, training=True):
+    def run_forward(self, input_ids, attention_mask=None, token_type_ids=None, training=True, cls_only=False):
+        """Returns (h, saved).  h = the last hidden state [B*T, D], or with
+        cls_only the CLS rows only, [B, D]: the last encoder layer then runs its
+        attention-output, LayerNorm and FFN work on the B CLS rows (its keys and
+        values still cover every token), since the caller (VisionLanguageModule
+        TextEncoder, :57-60) reads token 0 only."""
         cfg = self.cfg
         D, Fd, H = cfg.hidden, cfg.ffn, cfg.heads
         dh = D // H
@@ -209,6 +214,10 @@ class TinyBertTower(ArenaModule):
         for i in range(cfg.layers):
             p = f"encoder.layer.{i}."
             s_i = seed + 100 * (i + 1)
+            if cls_only and i == cfg.layers - 1:
+                layers.append(self._last_layer_cls(h, wT, A, am, B, Tn, p, s_i, p_h, p_a, scale))
+                h = layers[-1]["h2"]
+                break
             qkv = torch.empty(M, 3 * D, dtype=T, device=dev)
             ops.linear_fwd(h, self._qkv(wT, i), self._qkv(A, i, bias=True), qkv, M, 3 * D, D)
             ctx = torch.empty(M, D, dtype=T, device=dev)
@@ -243,7 +252,93 @@ class TinyBertTower(ArenaModule):
         sv["layers"] = layers
         sv["wT"] = wT
         sv["h_last"] = h
+        sv["cls_only"] = cls_only
         return h, sv
+
+    def _last_layer_cls(self, h, wT, A, am, B, Tn, p, s_i, p_h, p_a, scale):
+        """Last encoder layer for the CLS rows (row b*Tn of every [B*Tn] tensor,
+        read in place through the GEMMs' leading dimensions)."""
+        cfg = self.cfg
+        D, Fd, H = cfg.hidden, cfg.ffn, cfg.heads
+        dh = D // H
+        M = B * Tn
+        T, dev = self.tdtype, self.arena.data.device
+        i = cfg.layers - 1
+        qkv = torch.empty(M, 3 * D, dtype=T, device=dev)
+        ops.linear_fwd(h, self._qkv(wT, i), self._qkv(A, i, bias=True), qkv, M, 3 * D, D)
+        ctx = torch.empty(M, D, dtype=T, device=dev)
+        P = torch.empty(B, H, Tn, Tn, device=dev)
+        ops.attn_fwd(qkv, am, ctx, P, B, Tn, H, dh, scale, p=p_a, seed=s_i + 1)
+        s1 = torch.empty(B, D, dtype=T, device=dev)
+        ops.linear_fwd(ctx, self._w(wT, p + "attention.output.dense.weight"),
+                       self.arena.view(p + "attention.output.dense.bias"), s1, B, D, D, ldx=Tn * D, mode=2,
+                       res=h, ldr=Tn * D, p=p_h, seed=s_i + 2)
+        h1 = torch.empty(B, D, dtype=T, device=dev)
+        mu1 = torch.empty(B, device=dev)
+        rs1 = torch.empty(B, device=dev)
+        ops.layernorm_fwd(s1, self.arena.view(p + "attention.output.LayerNorm.weight"),
+                          self.arena.view(p + "attention.output.LayerNorm.bias"), cfg.ln_eps, h1, mu1, rs1, B, D)
+        u = torch.empty(B, Fd, dtype=T, device=dev)
+        f = torch.empty(B, Fd, dtype=T, device=dev)
+        ops.linear_fwd(h1, self._w(wT, p + "intermediate.dense.weight"),
+                       self.arena.view(p + "intermediate.dense.bias"), f, B, Fd, D, mode=1, aux=u)
+        s2 = torch.empty(B, D, dtype=T, device=dev)
+        ops.linear_fwd(f, self._w(wT, p + "output.dense.weight"), self.arena.view(p + "output.dense.bias"), s2,
+                       B, D, Fd, mode=2, res=h1, p=p_h, seed=s_i + 3)
+        h2 = torch.empty(B, D, dtype=T, device=dev)
+        mu2 = torch.empty(B, device=dev)
+        rs2 = torch.empty(B, device=dev)
+        ops.layernorm_fwd(s2, self.arena.view(p + "output.LayerNorm.weight"),
+                          self.arena.view(p + "output.LayerNorm.bias"), cfg.ln_eps, h2, mu2, rs2, B, D)
+        return {"h": h, "qkv": qkv, "ctx": ctx, "P": P, "s1": s1, "mu1": mu1, "rs1": rs1, "h1": h1, "u": u,
+                "f": f, "s2": s2, "mu2": mu2, "rs2": rs2, "h2": h2, "seed": s_i, "cls": True}
+
+    def _last_layer_cls_backward(self, Ls, dcls, wT, B, Tn, p_h, p_a, scale):
+        """Backward of _last_layer_cls; returns the gradient of its input [B*Tn, D]."""
+        cfg = self.cfg
+        D, Fd, H = cfg.hidden, cfg.ffn, cfg.heads
+        dh = D // H
+        M = B * Tn
+        T, dev = self.tdtype, self.arena.data.device
+        G = self.arena
+        i = cfg.layers - 1
+        p = f"encoder.layer.{i}."
+        s_i = Ls["seed"]
+        dc = dcls.to(T).contiguous()
+        ds2 = torch.empty(B, D, dtype=T, device=dev)
+        dz = torch.empty(B, D, dtype=T, device=dev)
+        ops.layernorm_bwd(dc, Ls["s2"], Ls["mu2"], Ls["rs2"], self.arena.view(p + "output.LayerNorm.weight"),
+                          ds2, dz, G.gview(p + "output.LayerNorm.weight"), G.gview(p + "output.LayerNorm.bias"),
+                          B, D, p_in=p_h, seed_in=s_i + 3)
+        ops.colsum(dz, G.gview(p + "output.dense.bias"), B, D)
+        ops.linear_wgrad(dz, Ls["f"], G.gview(p + "output.dense.weight"), B, D, Fd)
+        du = torch.empty(B, Fd, dtype=T, device=dev)
+        ops.linear_dgrad(dz, self._w(wT, p + "output.dense.weight"), du, B, Fd, D, mode=1, aux=Ls["u"])
+        ops.colsum(du, G.gview(p + "intermediate.dense.bias"), B, Fd)
+        ops.linear_wgrad(du, Ls["h1"], G.gview(p + "intermediate.dense.weight"), B, Fd, D)
+        dh1 = torch.empty(B, D, dtype=T, device=dev)
+        ops.linear_dgrad(du, self._w(wT, p + "intermediate.dense.weight"), dh1, B, D, Fd, addend=ds2)
+        ds1 = torch.empty(B, D, dtype=T, device=dev)
+        da = torch.empty(B, D, dtype=T, device=dev)
+        ops.layernorm_bwd(dh1, Ls["s1"], Ls["mu1"], Ls["rs1"],
+                          self.arena.view(p + "attention.output.LayerNorm.weight"), ds1, da,
+                          G.gview(p + "attention.output.LayerNorm.weight"),
+                          G.gview(p + "attention.output.LayerNorm.bias"), B, D, p_in=p_h, seed_in=s_i + 2)
+        ops.colsum(da, G.gview(p + "attention.output.dense.bias"), B, D)
+        ops.linear_wgrad(da, Ls["ctx"], G.gview(p + "attention.output.dense.weight"), B, D, D, ldx=Tn * D)
+        # only the CLS queries receive a context gradient; the residual gradient
+        # ds1 reaches the CLS rows of the layer input
+        dctx = torch.zeros(M, D, dtype=T, device=dev)
+        ops.linear_dgrad(da, self._w(wT, p + "attention.output.dense.weight"), dctx, B, D, D, lddx=Tn * D)
+        dqkv = torch.empty(M, 3 * D, dtype=T, device=dev)
+        ops.attn_bwd(Ls["qkv"], Ls["P"], dctx, dqkv, B, Tn, H, dh, scale, p=p_a, seed=s_i + 1)
+        ops.colsum(dqkv, self._qkv(None, i, bias=True, grad=True), M, 3 * D)
+        ops.linear_wgrad(dqkv, Ls["h"], self._qkv(None, i, grad=True), M, 3 * D, D)
+        ds1_full = torch.zeros(M, D, dtype=T, device=dev)
+        ops.scatter_rows(ds1, ds1_full, B, D, D, Tn * D)
+        dh_new = torch.empty(M, D, dtype=T, device=dev)
+        ops.linear_dgrad(dqkv, self._qkv(wT, i), dh_new, M, D, 3 * D, addend=ds1_full)
+        return dh_new
 
     # ---------------- backward ----------------
     def run_backward(self, sv, dcls):
@@ -261,10 +356,15 @@ class TinyBertTower(ArenaModule):
         G.grad.zero_()
         p_h, p_a = sv["p_h"], sv["p_a"]
         scale = 1.0 / math.sqrt(dh)
-        dh_ = torch.zeros(M, D, dtype=T, device=dev)
-        dc = dcls.to(T).contiguous()
-        ops.scatter_rows(dc, dh_, B, D, D, Tn * D)
-        for i in range(cfg.layers - 1, -1, -1):
+        top = cfg.layers - 1
+        if sv.get("cls_only"):
+            dh_ = self._last_layer_cls_backward(sv["layers"][top], dcls, wT, B, Tn, p_h, p_a, scale)
+            top -= 1
+        else:
+            dh_ = torch.zeros(M, D, dtype=T, device=dev)
+            dc = dcls.to(T).contiguous()
+            ops.scatter_rows(dc, dh_, B, D, D, Tn * D)
+        for i in range(top, -1, -1):
             p = f"encoder.layer.{i}."
             Ls = sv["layers"][i]
             s_i = Ls["seed"]
