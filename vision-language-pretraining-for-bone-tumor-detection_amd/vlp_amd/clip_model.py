@@ -17,6 +17,8 @@ from __future__ import annotations
 
 import math
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -90,6 +92,23 @@ def _project_backward(head, wT, feat, ld, dim, proj_name, E, emb, norm, g_emb, g
     return dfeat
 
 
+_TEXT_STREAMS = {}
+_USE_TEXT_STREAM = os.environ.get("VLP_TEXT_STREAM", "1") != "0"
+
+
+def _text_stream(dev):
+    """Second HIP stream for the text tower: its small, latency-bound kernels run
+    beside the image tower's instead of after them (the towers only meet in
+    the head).  None when disabled (VLP_TEXT_STREAM=0) or not on a GPU."""
+    if not _USE_TEXT_STREAM or dev.type != "cuda":
+        return None
+    s = _TEXT_STREAMS.get(dev)
+    if s is None:
+        s = torch.cuda.Stream(device=dev)
+        _TEXT_STREAMS[dev] = s
+    return s
+
+
 class ClipStepFn(torch.autograd.Function):
     """loss, image_loss, text_loss, img_emb, txt_emb = f(batch; all parameters)."""
 
@@ -97,9 +116,20 @@ class ClipStepFn(torch.autograd.Function):
     def forward(ctx, model, x, x_u8, input_ids, attention_mask, token_type_ids, *params):
         img_t, txt_t, head = model.image_tower, model.text_tower, model.head
         training = model.training
-        feat_img, sv_img = img_t.run_forward(x, training, x_u8=x_u8)
-        # only the CLS token's last hidden state is used (TextEncoder, :57-60)
-        h_last, sv_txt = txt_t.run_forward(input_ids, attention_mask, token_type_ids, training, cls_only=True)
+        main = torch.cuda.current_stream(input_ids.device) if input_ids.is_cuda else None
+        s_txt = _text_stream(input_ids.device)
+        if s_txt is not None:
+            # fork: the text tower on its own stream (inputs are ready on main)
+            s_txt.wait_stream(main)
+            with torch.cuda.stream(s_txt):
+                # only the CLS token's last hidden state is used (TextEncoder, :57-60)
+                h_last, sv_txt = txt_t.run_forward(input_ids, attention_mask, token_type_ids, training,
+                                                   cls_only=True)
+            feat_img, sv_img = img_t.run_forward(x, training, x_u8=x_u8)
+            main.wait_stream(s_txt)   # join before the head
+        else:
+            feat_img, sv_img = img_t.run_forward(x, training, x_u8=x_u8)
+            h_last, sv_txt = txt_t.run_forward(input_ids, attention_mask, token_type_ids, training, cls_only=True)
         B, Tn = input_ids.shape
         D, E = txt_t.cfg.hidden, head.embedding_dim
         wT = head.wcopy()
@@ -142,12 +172,27 @@ class ClipStepFn(torch.autograd.Function):
         dcls = _project_backward(head, wT, h_last, D, D, "text_projection", E, te, tnorm,
                                  g_txt, gs)
         # data parallel: SUM all-reduce of the flat gradient arenas, the head and
-        # text tower's launched while the (much longer) image backward runs
+        # text tower's launched while the (much longer) image backward runs.
+        # With the text stream the text backward and its collective also run
+        # beside the image backward; every tensor crossing streams stays
+        # referenced until the join below.
         reducer = vdist.GradReducer()
-        txt_t.run_backward(sv_txt, dcls)
-        reducer.reduce([head.arena, txt_t.arena])
-        img_t.run_backward(sv_img, dfeat_img)
-        reducer.reduce([img_t.arena])
+        s_txt = _text_stream(dcls.device)
+        if s_txt is not None:
+            main = torch.cuda.current_stream(dcls.device)
+            s_txt.wait_stream(main)
+            with torch.cuda.stream(s_txt):
+                txt_t.run_backward(sv_txt, dcls)
+                reducer.reduce([txt_t.arena])
+            reducer.reduce([head.arena])
+            img_t.run_backward(sv_img, dfeat_img)
+            reducer.reduce([img_t.arena])
+            main.wait_stream(s_txt)
+        else:
+            txt_t.run_backward(sv_txt, dcls)
+            reducer.reduce([head.arena, txt_t.arena])
+            img_t.run_backward(sv_img, dfeat_img)
+            reducer.reduce([img_t.arena])
         reducer.wait()
         grads = (head.grads_for_autograd() + img_t.grads_for_autograd() + txt_t.grads_for_autograd())
         return (None, None, None, None, None, None, *grads)
