@@ -38,7 +38,14 @@ LAYERS = (3, 4, 6, 3)
 WIDTHS = (64, 128, 256, 512)
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
-_USE_DYT = os.environ.get("VLP_WGRAD_DYT", "0") != "0"   # measured: the extra transposed write costs more than it saves
+_USE_DYT = os.environ.get("VLP_WGRAD_DYT", "0") != "0"
+# weight gradients on a side stream (VLP_WGRAD_STREAM=1): they are off the
+# data-gradient chain, so the MFMA-bound wgrad GEMMs overlap the HBM-bound BN /
+# elementwise passes.  Measured +0.8 % per step, but every wgrad launch then
+# shares the CUs and its own duration stretches by ~50 %, so it is off by
+# default (the per-kernel roofline is read from those durations)
+_USE_WG_STREAM = os.environ.get("VLP_WGRAD_STREAM", "0") != "0"
+_WG_STREAMS = {}   # measured: the extra transposed write costs more than it saves
 STAT_REP = 64   # replicas of per-channel fp64 sums (see vlp_stat_reduce)
 
 
@@ -320,6 +327,19 @@ class ResNet34Tower(ArenaModule):
         ws = self._workspace()
         T = self.tdtype
         dev = self.arena.data.device
+        self._sw = None
+        if _USE_WG_STREAM and dev.type == "cuda":
+            self._sw = _WG_STREAMS.get(dev)
+            if self._sw is None:
+                self._sw = _WG_STREAMS[dev] = torch.cuda.Stream(device=dev)
+        try:
+            self._run_backward(saved, dfeat, ws, T, dev)
+        finally:
+            if self._sw is not None:   # join: every weight gradient is in the arena
+                torch.cuda.current_stream(dev).wait_stream(self._sw)
+            self._sw = None
+
+    def _run_backward(self, saved, dfeat, ws, T, dev):
         ws["bstat"].zero_()
         o0, n0 = self._wg_off["conv1"]
         ws["wgrad"][o0:o0 + n0].zero_()   # stem's atomic accumulator (the 3x3 convs overwrite their grads)
@@ -447,6 +467,16 @@ class ResNet34Tower(ArenaModule):
 
     def _wgrad(self, ws, c, dy, x, sc=None, sh=None, dyT=None):
         if sc is None and dyT is None:
+            sw = getattr(self, "_sw", None)
+            if sw is not None:
+                # fork onto the weight-gradient stream; the allocator must not
+                # recycle dy / x before that stream has read them
+                sw.wait_stream(torch.cuda.current_stream(dy.device))
+                with torch.cuda.stream(sw):
+                    ops.conv_wgrad_into(dy, x, c.KH, c.KW, c.S, c.P, self.arena.gview(c.key + ".weight"))
+                dy.record_stream(sw)
+                x.record_stream(sw)
+                return
             ops.conv_wgrad_into(dy, x, c.KH, c.KW, c.S, c.P, self.arena.gview(c.key + ".weight"))
             return
         o, n = self._wg_off[c.key]
