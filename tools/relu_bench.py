@@ -11,7 +11,8 @@ from vlp_amd import ops  # noqa: E402
 
 dev = torch.device("cuda", 0)
 for name, (N, H, W, C, Co, S) in {"l1 s1": (256, 128, 128, 64, 64, 1), "l2 s2": (256, 128, 128, 64, 128, 2),
-                                   "l2 s1": (256, 64, 64, 128, 128, 1)}.items():
+                                   "l2 s1": (256, 64, 64, 128, 128, 1), "l3 s1": (256, 32, 32, 256, 256, 1),
+                                   "l4 s1": (256, 16, 16, 512, 512, 1)}.items():
     Ho, Wo = (H - 1) // S + 1, (W - 1) // S + 1
     dy = (torch.randn(N, Ho, Wo, Co, device=dev) * 0.5).to(torch.bfloat16)
     wt = (torch.randn(C, 3, 3, Co, device=dev) * 0.05).to(torch.bfloat16)
