@@ -214,6 +214,15 @@ int vlp_embed_bwd(int dtype, int M, int T, int D, const long long* ids, const lo
 int vlp_scatter_rows(int dtype, int R, int D, const void* in, int ldi, void* out, int ldo,
                      void* stream);
 
+/* ---------------- retrieval metrics ----------------
+ * Replace the topk over the full similarity matrix in
+ * precision_at_k_on_image_embeddings (VisionLanguageModule.py:364-400) and
+ * recall_at_k_on_image_text_retreival (:402-439).  vals/idx[R][K] = the K
+ * largest entries of each row x[r][0..N) in descending order, ties to the
+ * lower column; K <= 16.  The caller builds x one query chunk at a time
+ * (fp32 vlp_linear_fwd of normalised embeddings). */
+int vlp_row_topk(int R, int N, const float* x, long long ldx, int K, float* vals, int* idx, void* stream);
+
 /* ---------------- contrastive head ----------------
  * Replace VisionLanguageModule.forward (VisionLanguageModule.py:441-461: projections,
  * F.normalize, logit_scale.exp().clamp(max=100) * img @ txt.T) and

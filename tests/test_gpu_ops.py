@@ -412,3 +412,48 @@ def test_maxpool_fwd_argmax_value(ops, dt):
     # the recorded tap holds the window maximum
     assert torch.allclose(z[n, ho, wo, c].to(dt).float(), out.float().cpu(),
                           rtol=1e-2 if dt == torch.bfloat16 else 1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("N,K", [(3000, 16), (37, 16), (1000, 1), (5, 16)])
+def test_row_topk_vs_torch(ops, N, K):
+    """vlp_row_topk (via ops.sim_topk's chunked fp32 similarity) against
+    torch.topk of the full similarity matrix: values within fp32 rounding,
+    indices exact (random data has no ties); rows shorter than K pad with -1."""
+    torch.manual_seed(12)
+    q = torch.nn.functional.normalize(torch.randn(257, 128, device="cuda"))
+    k = torch.nn.functional.normalize(torch.randn(N, 128, device="cuda"))
+    vals, idx = ops.sim_topk(q, k, K)
+    kk = min(K, N)
+    ref = (q @ k.T).topk(kk, dim=1)
+    assert torch.equal(idx[:, :kk].cpu(), ref.indices.cpu())
+    assert (vals[:, :kk] - ref.values).abs().max().item() < 1e-5
+    if K > N:
+        assert (idx[:, N:] == -1).all()
+
+
+def test_retrieval_metrics_vs_oracle(ops):
+    """Module precision@k / recall@k on the GPU path against the CPU oracle
+    restatement (:364-439) and the reference-generated known answers."""
+    import os
+    from oracle.clip import precision_at_k, recall_at_k
+    from src.models.pretrain.VisionLanguageModule import VisionLanguageModule
+    ka = torch.load(os.path.join(os.path.dirname(__file__), "golden", "known_answers.pt"), weights_only=True)
+    m = VisionLanguageModule.__new__(VisionLanguageModule)
+    ks = [3, 5, 10, 15]
+    p = VisionLanguageModule.precision_at_k_on_image_embeddings(m, ka["retr_img"].cuda(), ka["retr_lab"].cuda(), ks)
+    r = VisionLanguageModule.recall_at_k_on_image_text_retreival(m, ka["retr_img"].cuda(), ka["retr_txt"].cuda(), ks)
+    assert [p[k] for k in ks] == pytest.approx(ka["prec"].tolist(), abs=1e-7)
+    assert [r[k] for k in ks] == pytest.approx(ka["recall"].tolist(), abs=1e-7)
+    e = torch.tensor([[1, 1], [1, 1.1], [2, 1], [3, 1]], dtype=torch.float32).cuda()   # notebook cell 27
+    assert VisionLanguageModule.precision_at_k_on_image_embeddings(m, e, torch.tensor([0, 0, 1, 1]).cuda(), [1]) == {1: 1.0}
+    assert VisionLanguageModule.recall_at_k_on_image_text_retreival(m, e, e, [1, 2]) == {1: 1.0, 2: 1.0}
+    torch.manual_seed(13)
+    img, txt = torch.randn(4096, 128), torch.randn(4096, 128)
+    txt = img + 3.0 * txt   # recall between 0 and 1
+    lab = torch.randint(0, 7, (4096,))
+    p = VisionLanguageModule.precision_at_k_on_image_embeddings(m, img.cuda(), lab.cuda(), ks)
+    r = VisionLanguageModule.recall_at_k_on_image_text_retreival(m, img.cuda(), txt.cuda(), ks)
+    po, ro = precision_at_k(img, lab, ks), recall_at_k(img, txt, ks)
+    assert [p[k] for k in ks] == pytest.approx([po[k] for k in ks], abs=1e-6)
+    assert [r[k] for k in ks] == pytest.approx([ro[k] for k in ks], abs=1e-6)
+    assert 0.05 < r[3] < 0.95

@@ -413,10 +413,20 @@ class VisionLanguageModule(_Base):
                 torch.cat(cache["label"]))
 
     def precision_at_k_on_image_embeddings(self, image_embeddings, labels, ks: list) -> dict:
+        """:364-400.  On the GPU the top-(k+1) lists come from chunked fp32
+        similarity GEMMs + vlp_row_topk (no N x N matrix); the first entry (the
+        query itself) is dropped as in the reference."""
         assert all(k + 1 <= image_embeddings.shape[0] for k in ks), "k+1 must be less than or equal to the batch size"
         e = torch.nn.functional.normalize(image_embeddings.float())
-        sim = e @ e.T
+        labels = labels.to(e.device)
         out = {}
+        if e.is_cuda and max(ks) + 1 <= 16:
+            _, top_all = ops.sim_topk(e, e, max(ks) + 1)
+            for k in ks:
+                correct = (labels.unsqueeze(1) == labels[top_all[:, 1:k + 1]]).sum(dim=1)
+                out[k] = (correct.float() / k).mean().item()
+            return out
+        sim = e @ e.T
         for k in ks:
             top = sim.topk(k=k + 1, dim=1).indices[:, 1:]
             correct = (labels.unsqueeze(1) == labels[top]).sum(dim=1)
@@ -424,13 +434,19 @@ class VisionLanguageModule(_Base):
         return out
 
     def recall_at_k_on_image_text_retreival(self, image_embeddings, text_embeddings, ks: list) -> dict:
+        """:402-439 (GPU: chunked similarity + vlp_row_topk, as above)."""
         i = torch.nn.functional.normalize(image_embeddings.float())
         t = torch.nn.functional.normalize(text_embeddings.float())
-        sim = i @ t.T
         out = {}
+        tgt = torch.arange(i.shape[0], device=i.device)
+        if i.is_cuda and max(ks) <= 16:
+            _, top_all = ops.sim_topk(i, t, max(ks))
+            for k in ks:
+                out[k] = (top_all[:, :k] == tgt.unsqueeze(1)).any(dim=1).sum().item() / i.shape[0]
+            return out
+        sim = i @ t.T
         for k in ks:
             top = sim.topk(k=k, dim=1).indices
-            tgt = torch.arange(i.shape[0], device=top.device)
             out[k] = (top == tgt.unsqueeze(1)).any(dim=1).sum().item() / i.shape[0]
         return out
 

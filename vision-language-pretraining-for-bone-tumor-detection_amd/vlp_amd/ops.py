@@ -410,3 +410,32 @@ def unpack_conv_grad(ws, g):
 
 def unpack_stem_grad(ws, g):
     lib().vlp_unpack_stem_grad(ptr(ws), ptr(g), _s())
+
+
+# ---------------- retrieval metrics ----------------
+SIM_CHUNK_BYTES = 256 << 20
+
+
+def sim_topk(q, keys, K):
+    """Top-K (values, indices) of q @ keys^T per row, descending (ties to the
+    lower index), without materialising the full similarity matrix: query
+    chunks of <= 256 MB of fp32 similarities, each an fp32 GEMM
+    (vlp_linear_fwd) reduced by vlp_row_topk.  q [Q, E], keys [N, E] fp32."""
+    q = q.float().contiguous()
+    keys = keys.float().contiguous()
+    if q.shape[1] % 4:   # 16-B operand rows: zero columns leave every dot product unchanged
+        pad = 4 - q.shape[1] % 4
+        q = torch.nn.functional.pad(q, (0, pad))
+        keys = torch.nn.functional.pad(keys, (0, pad))
+    Q, E = q.shape
+    N = keys.shape[0]
+    Np = (N + 3) // 4 * 4   # 16-B rows for the GEMM epilogue
+    vals = torch.empty(Q, K, device=q.device)
+    idx = torch.empty(Q, K, dtype=torch.int32, device=q.device)
+    rows = max(1, min(Q, SIM_CHUNK_BYTES // (4 * Np)))
+    tile = torch.empty(rows, Np, device=q.device)
+    for r0 in range(0, Q, rows):
+        r = min(rows, Q - r0)
+        linear_fwd(q[r0:r0 + r], keys, None, tile, r, N, E, ldy=Np)
+        lib().vlp_row_topk(r, N, ptr(tile), Np, K, ptr(vals[r0:r0 + r]), ptr(idx[r0:r0 + r]), _s())
+    return vals, idx.long()
