@@ -102,6 +102,12 @@ int vlp_stem_fwd(int dtype, const void* xp, const void* wp, void* y, int N, int 
                  double* stat_sum, double* stat_sumsq, int stat_rep, void* stream);
 int vlp_stem_wgrad(int dtype, const void* dy, const void* xp, float* dw_ws, int N, int H, int W,
                    const void* dyT, void* stream);
+/* the same through per-split fp32 slabs split_ws[s][64][256] (plain stores, no
+ * atomics; *nsplit receives the split count), then vlp_stem_wgrad_fold sums
+ * them into grad[64][3][7][7] (timm conv1.weight layout), overwriting it */
+int vlp_stem_wgrad_ws(int dtype, const void* dy, const void* xp, float* split_ws, long long ws_floats,
+                      int* nsplit, int N, int H, int W, void* stream);
+int vlp_stem_wgrad_fold(int nsplit, const float* split_ws, float* grad, void* stream);
 
 /* ---------------- image tower: BatchNorm / residual / pooling ----------------
  * Replace timm resnet34's BatchNorm2d (train-mode batch statistics), ReLU,

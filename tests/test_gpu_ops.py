@@ -273,6 +273,10 @@ def test_stem_fwd_wgrad(ops, dt):
     torch.cuda.synchronize()
     assert rel(nchw(yd.float().cpu()), y.detach()) < tol(dt)
     assert rel(g.cpu(), w.grad) < tol(dt) / 2
+    g3 = torch.full((64, 3, 7, 7), float("nan"), device="cuda")   # split slabs + fold (training path)
+    ops.stem_wgrad_into(nhwc(dy).to(dt).cuda(), xp, N, H, W, g3)
+    torch.cuda.synchronize()
+    assert rel(g3.cpu(), w.grad) < tol(dt) / 2
     if dt == torch.bfloat16:
         Mp = N * Ho * Wo
         dyT = nhwc(dy).to(dt).reshape(Mp, 64).t().contiguous().cuda()
@@ -457,3 +461,22 @@ def test_retrieval_metrics_vs_oracle(ops):
     assert [p[k] for k in ks] == pytest.approx([po[k] for k in ks], abs=1e-6)
     assert [r[k] for k in ks] == pytest.approx([ro[k] for k in ks], abs=1e-6)
     assert 0.05 < r[3] < 0.95
+
+
+def test_stem_wgrad_many_splits(ops):
+    """Stem weight gradient over 32768 output pixels (16 K-splits of slabs)
+    against torch's fp32 weight gradient."""
+    N, H, W = 8, 128, 128
+    torch.manual_seed(14)
+    x = torch.randn(N, 3, H, W).to(torch.bfloat16).float()
+    w = (torch.randn(64, 3, 7, 7) * 0.1).requires_grad_()
+    y = F.conv2d(x, w, stride=2, padding=3)
+    dy = torch.randn_like(y).to(torch.bfloat16).float()
+    y.backward(dy)
+    Ho, Wo, Hp, Wp = ops.stem_geom(H, W)
+    xp = torch.zeros(N, Hp, Wp, 4, dtype=torch.bfloat16, device="cuda")
+    ops.stem_prep(x.cuda(), xp)
+    g = torch.full((64, 3, 7, 7), float("nan"), device="cuda")
+    ops.stem_wgrad_into(nhwc(dy).to(torch.bfloat16).cuda(), xp, N, H, W, g)
+    torch.cuda.synchronize()
+    assert rel(g.cpu(), w.grad) < 2e-3

@@ -1582,6 +1582,66 @@ VLP_EXPORT int vlp_stem_fwd(int dtype, const void* xp, const void* wp, void* y, 
 }
 
 // dW_ws[64][256] (kh:8, kw:8, c:4 layout), fp32, accumulated atomically.
+VLP_EXPORT int vlp_stem_wgrad(int dtype, const void* dy, const void* xp, float* dw_ws, int N, int H, int W,
+                              const void* dyT, void* stream);
+// stem weight gradient through per-split fp32 slabs [ks][64][256] (no atomics),
+// folded straight into the parameter's [64][3][7][7] gradient:
+// 64 slab elements x 4 slab groups per block: every wave reads 256 contiguous
+// bytes of one slab per step; the 4 group partials meet in LDS (deterministic)
+__global__ void __launch_bounds__(256) stem_wgrad_fold_kernel(int ks, const float* __restrict__ ws,
+                                                              float* __restrict__ g) {
+  __shared__ float part[4][64];
+  const int e = blockIdx.x * 64 + (threadIdx.x & 63), grp = threadIdx.x >> 6;   // e < 64 * 256
+  const float* p = ws + e;
+  float a0 = 0.f, a1 = 0.f;
+  int s = grp;
+  for (; s + 4 < ks; s += 8) { a0 += p[(size_t)s * 64 * 256]; a1 += p[(size_t)(s + 4) * 64 * 256]; }
+  if (s < ks) a0 += p[(size_t)s * 64 * 256];
+  part[grp][threadIdx.x & 63] = a0 + a1;
+  __syncthreads();
+  if (grp == 0) {
+    const int co = e >> 8, k = e & 255, kh = k >> 5, kw = (k >> 2) & 7, c = k & 3;
+    if (kh < 7 && kw < 7 && c < 3) {
+      const int l = threadIdx.x & 63;
+      g[((co * 3 + c) * 7 + kh) * 7 + kw] = (part[0][l] + part[1][l]) + (part[2][l] + part[3][l]);
+    }
+  }
+}
+
+VLP_EXPORT int vlp_stem_wgrad_ws(int dtype, const void* dy, const void* xp, float* split_ws, long long ws_floats,
+                                 int* nsplit, int N, int H, int W, void* stream) {
+  StemGeom g = make_stem(N, H, W);
+  hipStream_t st = (hipStream_t)stream;
+  if (!nsplit || (long long)N * g.Hp * g.Wp * 4 >= (1ll << 31)) return (int)hipErrorInvalidValue;
+  const long long slab = 64 * 256;
+  const long long fit = ws_floats / slab;
+  const int max_ks = (int)(fit < 4096 ? fit : 4096);
+  if (max_ks < 1) return (int)hipErrorInvalidValue;
+  if (dtype != VLP_BF16 || gemm_variant() < 4) {   // other engines: atomics into slab 0
+    if (hipMemsetAsync(split_ws, 0, slab * sizeof(float), st) != hipSuccess) return (int)hipGetLastError();
+    *nsplit = 1;
+    return vlp_stem_wgrad(dtype, dy, xp, split_ws, N, H, W, nullptr, stream);
+  }
+  // <= 512 splits: the fold then reads <= 32 MB of slabs
+  int mink = 2048;
+  const int need = (g.M + (max_ks < 512 ? max_ks : 512) - 1) / (max_ks < 512 ? max_ks : 512);
+  if (mink < need) mink = need;
+  StemWgradB<bf16> lb{g, (const bf16*)xp, make_stem_pixstep(g, Elem<bf16>::BK)};
+  MNMat<bf16> la{(const bf16*)dy, 64, 64, g.M};
+  EpiSplitStore ep{nullptr, nullptr, split_ws, 256, (size_t)slab};
+  const int r = launch_gemm_bk<64, 128, 1, 4>(64, 224, g.M, -mink, la, lb, ep, st);
+  if (r) return r;
+  *nsplit = last_ksplit();
+  return *nsplit > max_ks ? (int)hipErrorInvalidValue : 0;
+}
+
+VLP_EXPORT int vlp_stem_wgrad_fold(int nsplit, const float* split_ws, float* grad, void* stream) {
+  if (nsplit < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(stem_wgrad_fold_kernel, dim3(64 * 256 / 64), dim3(256), 0, (hipStream_t)stream, nsplit, split_ws,
+                     grad);
+  return (int)hipGetLastError();
+}
+
 VLP_EXPORT int vlp_stem_wgrad(int dtype, const void* dy, const void* xp, float* dw_ws, int N, int H,
                               int W, const void* dyT, void* stream) {
   StemGeom g = make_stem(N, H, W);

@@ -127,6 +127,22 @@ def conv_wgrad_into(dy, x, KH, KW, S, P, grad):
     return grad
 
 
+def stem_wgrad_into(dy, xp, N, H, W, grad):
+    """grad[64][3][7][7] = stem weight gradient (overwrites), via per-split
+    fp32 slabs of the shared weight-gradient workspace and one fold pass."""
+    import ctypes
+    ws = _WGRAD_WS.get(dy.device)
+    if ws is None:
+        ws = torch.empty(WGRAD_WS_FLOATS, dtype=torch.float32, device=dy.device)
+        _WGRAD_WS[dy.device] = ws
+    ns = ctypes.c_int(0)
+    tk = ktimer.begin("stem_wgrad", 2.0 * dy.numel() * 147)
+    lib().vlp_stem_wgrad_ws(dcode(dy), ptr(dy), ptr(xp), ptr(ws), ws.numel(), ctypes.addressof(ns), N, H, W, _s())
+    ktimer.end(tk)
+    lib().vlp_stem_wgrad_fold(ns.value, ptr(ws), ptr(grad), _s())
+    return grad
+
+
 def stem_geom(H, W):
     import ctypes
     a, b, c, d = (ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int())

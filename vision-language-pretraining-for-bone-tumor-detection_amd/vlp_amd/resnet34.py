@@ -341,8 +341,6 @@ class ResNet34Tower(ArenaModule):
 
     def _run_backward(self, saved, dfeat, ws, T, dev):
         ws["bstat"].zero_()
-        o0, n0 = self._wg_off["conv1"]
-        ws["wgrad"][o0:o0 + n0].zero_()   # stem's atomic accumulator (the 3x3 convs overwrite their grads)
         dfeat = dfeat.float().contiguous()
         blocks = saved["blocks"]
         dout = None
@@ -447,11 +445,7 @@ class ResNet34Tower(ArenaModule):
         sg0, sgx0 = sg0f[:64], sgx0f[:64]
         dy0 = torch.empty_like(y0)
         ops.maxpool_bwd_apply(dout, idx, y0, sc0, sh0, mu0, is0, self.arena.view("bn1.weight"), sg0, sgx0, dy0)
-        t0 = None
-        o, n = self._wg_off["conv1"]
-        wsb = ws["wgrad"][o:o + n]
-        ops.stem_wgrad(dy0, saved["xp"], saved["N"], saved["H"], saved["W"], wsb, dyT=t0)
-        ops.unpack_stem_grad(wsb, self.arena.gview("conv1.weight"))
+        ops.stem_wgrad_into(dy0, saved["xp"], saved["N"], saved["H"], saved["W"], self.arena.gview("conv1.weight"))
 
     def _tbuf(self, ws, name, C, M):
         """[C][M] bf16 scratch for a transposed output gradient (the weight-gradient
