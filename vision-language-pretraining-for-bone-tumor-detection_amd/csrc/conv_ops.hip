@@ -943,6 +943,17 @@ static int gemm_auto(int M, int N, int K, int ksplit, const LA& la, const LB& lb
   if (N <= 64) return gemm_narrow<T>(M, N, K, ksplit, la, lb, ep, st);
   return gemm_conv_wide<T>(M, N, K, ksplit, la, lb, ep, st);
 }
+// stride-2 data-gradient parity classes (short K: 1..4 taps of Co channels)
+template <typename T, class LA, class LB, class EP>
+static int gemm_s2(int M, int N, int K, const LA& la, const LB& lb, const EP& ep, hipStream_t st) {
+  if constexpr (use_bk<T, LA, LB>()) {
+    // 256x64 on the two-tiles-in-flight engine: +3 % over the one-tile ring
+    static const int s2v = getenv("VLP_S2_BIG") ? atoi(getenv("VLP_S2_BIG")) : 1;
+    if (N <= 64 && s2v == 1) return launch_gemm_big<256, 64, 4, 1>(M, N, K, 1, la, lb, ep, st);
+    if (N <= 64 && s2v == 2) return launch_gemm_big<128, 64, 2, 1>(M, N, K, 1, la, lb, ep, st);
+  }
+  return gemm_auto<T>(M, N, K, 1, la, lb, ep, st);
+}
 // weight-gradient GEMMs: rows = Co, cols = KH*KW*C, reduction = pixels.
 //  Co = 64 (stem, layer1): 64 x 128 tiles, split-K chosen by the launcher to
 //    fill whole rounds of resident workgroups (ksplit = -2048: >= 2048 pixels)
@@ -1247,11 +1258,11 @@ static int conv_dgrad_t(const void* dy, const void* wt, void* dx, ConvGeom g, co
         if (ybn) {
           EpiDgradBN<T> in{s1, s2, rep, (T*)dx, g.C, (const T*)ybn, sc, sh, mean, invstd};
           EpiS2Remap<EpiDgradBN<T>> ep{s1, s2, rep, in, c, g.H, g.W};
-          r = gemm_auto<T>(Mc, g.C, Kc, 1, la, lb, ep, st);
+          r = gemm_s2<T>(Mc, g.C, Kc, la, lb, ep, st);
         } else {
           EpiDgradAdd<T> in{nullptr, nullptr, (T*)dx, (const T*)addend, g.C};
           EpiS2Remap<EpiDgradAdd<T>> ep{nullptr, nullptr, 1, in, c, g.H, g.W};
-          r = gemm_auto<T>(Mc, g.C, Kc, 1, la, lb, ep, st);
+          r = gemm_s2<T>(Mc, g.C, Kc, la, lb, ep, st);
         }
         if (r) return r;
       }
@@ -1294,7 +1305,7 @@ static int conv_dgrad_relu_impl(const void* dy, const void* wt, void* gout, Conv
         ConvDgradS2A<T> la{g, c, (const T*)dy, Mc, Kc};
         WtS2B<T> lb{(const T*)wt, g, c, Kc};
         EpiS2Remap<EpiDgradRelu<T, BITS>> ep{s1, s2, rep, in, c, g.H, g.W};
-        const int r = gemm_auto<T>(Mc, g.C, Kc, 1, la, lb, ep, st);
+        const int r = gemm_s2<T>(Mc, g.C, Kc, la, lb, ep, st);
         if (r) return r;
       }
     return 0;
