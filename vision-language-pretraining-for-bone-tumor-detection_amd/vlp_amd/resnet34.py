@@ -425,7 +425,9 @@ class ResNet34Tower(ArenaModule):
                 kp = prev[0] + ".bn2"
                 _, _, mup, isp = self._coef(ws, kp)
                 sgpf, sgxpf = self._bstat(ws, kp, full=True)
-                rmask = B["xmask"] if B.get("xmask") is not None else x
+                # sign bits for stride 1; the stride-2 parity-class epilogue reads the
+                # activation faster than single mask bytes (measured 840 vs 884 us)
+                rmask = B["xmask"] if (B.get("xmask") is not None and c1.S == 1) else x
                 dx = ops.conv_dgrad_relu(dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, rmask,
                                          blocks[bi - 1]["y2"], mup, isp, sgpf, sgxpf, addend=addend,
                                          stat_rep=STAT_REP)
