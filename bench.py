@@ -158,6 +158,29 @@ def pcie_inclusive(args, model, opt, world, dev):
         out[form] = {"value": round(world * args.batch * args.pcie_steps / el, 2),
                      "ms_per_step": round(el / args.pcie_steps * 1e3, 3),
                      "h2d_mb_per_step": round(b[key].numel() * b[key].element_size() / 1e6, 1)}
+        # same upload through src/data's DevicePrefetcher: batch i+1 is copied on a
+        # side stream while step i runs (the training loop's data path)
+        from src.data.PretrainDataModule import DevicePrefetcher
+
+        def steps_overlapped(n):
+            for dbatch in DevicePrefetcher((host for _ in range(n)), dev):
+                opt.zero_grad()
+                loss = model.training_step(dbatch)
+                loss.backward()
+                opt.step()
+        steps_overlapped(2)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        steps_overlapped(args.pcie_steps)
+        torch.cuda.synchronize()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        el = el.item()
+        out[form + "_prefetched"] = {"value": round(world * args.batch * args.pcie_steps / el, 2),
+                                     "ms_per_step": round(el / args.pcie_steps * 1e3, 3)}
     out["unit"] = "image-text pairs/s"
     out["steps"] = args.pcie_steps
     return out

@@ -1,0 +1,132 @@
+"""src/train.py / Hydra-config / src/data collation boundary (SURVEY §8(a) collation
+row, §8(b) config boundary and loop semantics).  CPU tests: config composition,
+instantiation, the synthetic data module's batch schema and normalisation
+(checked against the oracle-side synth.normalize_u8 formula, PretrainDataModule.py:165-171),
+and the Trainer's step order with a plain-torch stand-in module."""
+import functools
+
+import pytest
+import torch
+
+from src.data.PretrainDataModule import (DevicePrefetcher, PairCollator, PretrainDataModule,
+                                         SyntheticRadiographCaptions, normalize_u8)
+from src.utils.config import compose, instantiate
+from src.utils.trainer import Trainer
+from tests.golden import synth
+
+
+def test_compose_experiment_and_overrides():
+    c = compose("train", ["experiment=pretrain/pretrain_resnet34_tinybert", "data.batch_size=4",
+                          "scheduler=cosine", "trainer.max_epochs=7"])
+    assert c["data"]["_target_"] == "src.data.PretrainDataModule.PretrainDataModule"
+    assert c["data"]["batch_size"] == 4 and c["data"]["tokenizer"] == "tinybert"
+    assert c["model"]["text_encoder_model"] == "tinybert"
+    assert c["model"]["embedding_dim"] == 128 and c["model"]["text_embedding_dim"] == 312
+    assert c["model"]["optimizer"]["lr"] == 5e-5                  # experiment optimizer.lr
+    assert c["model"]["scheduler"]["T_max"] == 7                   # ${trainer.max_epochs} after the CLI
+    opt = instantiate(c["model"]["optimizer"])
+    assert isinstance(opt, functools.partial) and opt.func is torch.optim.AdamW and opt.keywords["lr"] == 5e-5
+    assert isinstance(instantiate(c["trainer"]), Trainer)            # lightning Trainer target, absent here
+
+
+def test_compose_defaults_and_errors():
+    c = compose("train", [])
+    assert c["seed"] == 42 and c["scheduler"] == {} and c["model"]["scheduler"] == {}
+    with pytest.raises(FileNotFoundError):
+        compose("train", ["experiment=pretrain/does_not_exist"])
+    with pytest.raises(ValueError):
+        compose("train", ["no_equals_sign"])
+    c = compose("train", ["experiment=pretrain/pretrain_resnet34_tinybert_mi355x"])
+    assert (c["data"]["batch_size"], c["data"]["image_size"], c["model"]["compute_dtype"]) == (256, 512, "bf16")
+
+
+def test_datamodule_schema_and_normalisation():
+    with pytest.raises(ValueError):
+        PretrainDataModule(num_channels=2)
+    with pytest.raises(NotImplementedError):
+        PretrainDataModule(synthetic=False)
+    dm = PretrainDataModule(batch_size=4, num_workers=0, image_size=32, n_samples=10, tokenizer="tinybert")
+    (fold, lw), = list(dm.get_cv_splits())
+    assert fold is dm and lw == (1.0, 1.0)
+    batches = list(dm.train_dataloader())
+    assert len(batches) == 2                                             # drop_last on train
+    b = batches[0]
+    assert b["x-ray-u8"].shape == (4, 1, 32, 32) and b["x-ray-u8"].dtype == torch.uint8
+    ct = b["caption_tokenized"]
+    assert set(ct) == {"input_ids", "token_type_ids", "attention_mask"}
+    assert ct["input_ids"].shape == (4, 40) and ct["input_ids"].dtype == torch.long
+    assert (ct["input_ids"][:, 0] == 101).all()
+    L = ct["attention_mask"].sum(1)
+    assert ((L >= 10) & (L <= 22)).all()
+    assert (ct["input_ids"].gather(1, (L - 1)[:, None]) == 102).all()
+    assert (ct["input_ids"] * (1 - ct["attention_mask"]) == 0).all()
+    assert all(len(b[k]) == 4 for k in ("caption", "dataset", "anatomy_site", "image_path"))
+    val = dm.val_dataloader()
+    assert len(val) == 2 and all(len(list(v)) == 16 for v in val)         # 64 val pairs, no drop_last
+    # fp32 upload == the reference's normalised 3-channel tensor on the same bytes
+    ds = SyntheticRadiographCaptions(3, 16, seed=5)
+    samples = [ds[i] for i in range(3)]
+    f32 = PairCollator("fp32")(samples)["x-ray"]
+    u8 = PairCollator("u8")(samples)["x-ray-u8"]
+    assert f32.shape == (3, 3, 16, 16) and f32.dtype == torch.float32
+    assert torch.equal(f32, synth.normalize_u8(u8))
+    assert torch.equal(normalize_u8(u8, 1), ((u8.float() - 127.5) / 73.9))
+    # determinism and per-index independence
+    assert torch.equal(ds[1]["x-ray-u8"], SyntheticRadiographCaptions(3, 16, seed=5)[1]["x-ray-u8"])
+    assert not torch.equal(ds[0]["x-ray-u8"], ds[1]["x-ray-u8"])
+    with pytest.raises(IndexError):
+        ds[3]
+    with pytest.raises(ValueError):
+        PairCollator("u8")([])
+    assert PretrainDataModule(num_channels=1, num_workers=0).upload == "fp32"
+    assert len(PretrainDataModule(try_with_only_n_samples=5, num_workers=0).train_dataset) == 5
+
+
+def test_prefetcher_cpu_passthrough():
+    items = [{"a": torch.arange(3)}, {"a": torch.arange(4)}]
+    out = list(DevicePrefetcher(items, "cpu"))
+    assert out == items
+
+
+class _Toy(torch.nn.Module):
+    """Plain-torch stand-in with the hooks the Trainer drives."""
+
+    def __init__(self):
+        super().__init__()
+        self.w = torch.nn.Parameter(torch.ones(3))
+        self.calls = []
+
+    @property
+    def device(self):
+        return self.w.device
+
+    def configure_optimizers(self):
+        return {"optimizer": torch.optim.SGD(self.parameters(), lr=0.1)}
+
+    def on_train_epoch_start(self):
+        self.calls.append("epoch_start")
+
+    def on_train_epoch_end(self):
+        self.calls.append("epoch_end")
+
+    def training_step(self, batch, i):
+        assert self.training
+        self.calls.append(("step", i))
+        return ((self.w * batch["x"]).sum() - 1.0) ** 2
+
+
+def test_trainer_loop_semantics():
+    m = _Toy()
+    data = [{"x": torch.full((3,), float(i + 1))} for i in range(5)]
+    t = Trainer(max_epochs=3, log_every_n_steps=2, max_steps=7)
+    t.fit(m, train_dataloaders=data)
+    assert t.global_step == 7 and t.current_epoch == 1
+    assert [s for s, _ in t.history] == [2, 4, 6]
+    assert m.calls[0] == "epoch_start" and m.calls.count("epoch_end") == 2
+    # the step really optimises: w moved away from ones by SGD
+    assert not torch.allclose(m.w.detach(), torch.ones(3))
+    m2 = _Toy()
+    Trainer(max_epochs=1, limit_train_batches=2).fit(m2, train_dataloaders=data)
+    assert [c for c in m2.calls if isinstance(c, tuple)] == [("step", 0), ("step", 1)]
+    with pytest.raises(ValueError):
+        Trainer(min_epochs=3, max_epochs=2)

@@ -346,7 +346,8 @@ class VisionLanguageModule(_Base):
     # ---------------- forward / loss ----------------
     def forward(self, batch):
         """:441-461 — returns (logits, image_embeddings, text_embeddings)."""
-        image_features = self.image_encoder(batch["x-ray"].to(self.device, non_blocking=True))
+        x = batch["x-ray"] if "x-ray" in batch else batch["x-ray-u8"]   # u8: on-device normalise
+        image_features = self.image_encoder(x.to(self.device, non_blocking=True))
         text_features = self.text_encoder(**{k: v.to(self.device, non_blocking=True)
                                              for k, v in batch["caption_tokenized"].items()})
         ie = _EmbedFn.apply(self._head, image_features, "image_projection", self.image_projection)

@@ -1,0 +1,111 @@
+"""src/train.py for the MI355X pretraining path (reference src/train.py:56-340).
+
+Same entry points and flow for the VLP pretraining experiments:
+  main(argv)  Hydra-style command line (`experiment=pretrain/pretrain_resnet34_tinybert
+              data.batch_size=256 ...`), configs composed from ../configs with the
+              reference's group names (src/utils/config.py; Hydra is not in this image);
+  train(cfg)  seed (train.yaml `seed`, :86-88) -> instantiate cfg.data (:90) -> for each
+              (datamodule, label_weights) in get_cv_splits() (:105): set
+              model.label_weights, instantiate cfg.model (:109-116) and cfg.trainer
+              (:163), trainer.fit(model, datamodule) (:185) -> per-fold metrics
+              (:188-192), aggregated over folds (:231-262).
+Out of scope: W&B loggers, Lightning callbacks, t-SNE /
+confusion-matrix plots, downstream zero-shot evaluation and the baseline modules.
+
+Multi-GPU: launch one process per GPU (`python -m torch.distributed.run
+--nproc-per-node N src/train.py ...`); train() initialises torch.distributed
+(nccl = RCCL over xGMI) from the launcher's environment and pins each rank to
+LOCAL_RANK.  The module's fused step all-gathers embeddings for the global-batch
+loss and all-reduces gradients itself.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import random
+import sys
+from typing import Any, Dict, List, Optional, Tuple
+
+_PKG = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+if _PKG not in sys.path:
+    sys.path.insert(0, _PKG)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from src.utils.config import compose, instantiate  # noqa: E402
+
+log = logging.getLogger("project")
+
+
+def seed_everything(seed: int) -> None:
+    """lightning.seed_everything(seed, workers=True) (train.py:87-88)."""
+    random.seed(seed)
+    np.random.seed(seed % (2 ** 32))
+    torch.manual_seed(seed)
+    os.environ["PL_GLOBAL_SEED"] = str(seed)
+
+
+def _init_distributed() -> None:
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws > 1 and not torch.distributed.is_initialized():
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        torch.distributed.init_process_group(backend)
+
+
+def train(cfg: Dict[str, Any]) -> Tuple[Dict[str, Any], Dict[str, Any]]:
+    if cfg.get("k_fold_cross_validation", False):
+        log.info("Train: Doing k-fold cross validation.")
+    if cfg.get("seed"):
+        seed_everything(int(cfg["seed"]))
+    _init_distributed()
+    log.info("Train: Instantiating datamodule <%s>", cfg["data"]["_target_"])
+    datamodule = instantiate(cfg["data"])
+    all_fold_metrics: List[Dict[str, Any]] = []
+    objects: Dict[str, Any] = {"cfg": cfg, "datamodule": datamodule}
+    for i, (fold_dm, label_weights) in enumerate(datamodule.get_cv_splits()):
+        model_cfg = dict(cfg["model"])
+        if not model_cfg.get("scheduler"):
+            model_cfg["scheduler"] = None
+        model_cfg["label_weights"] = label_weights
+        if model_cfg.get("downstream_datamodule") in ({}, "null"):
+            model_cfg["downstream_datamodule"] = None
+        log.info("Train: Instantiating model <%s>", model_cfg["_target_"])
+        model = instantiate(model_cfg)
+        log.info("Train: Instantiating trainer <%s>", cfg["trainer"]["_target_"])
+        trainer = instantiate(cfg["trainer"], callbacks=[], logger=None)
+        objects.update(model=model, trainer=trainer)
+        if cfg.get("train", True):
+            trainer.fit(model=model, datamodule=fold_dm)
+            bs = getattr(fold_dm, "batch_size", 0)
+            ws = torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1
+            log.info("Train: %d steps in %.2f s (%.1f image-text pairs/s incl. data loading, %d rank(s))",
+                     trainer.global_step, trainer.fit_seconds,
+                     ws * bs * trainer.global_step / max(trainer.fit_seconds, 1e-9), ws)
+        all_fold_metrics.append(dict(trainer.logged_metrics))
+        if not cfg.get("k_fold_cross_validation", False):
+            break
+    metrics: Dict[str, Any] = {}
+    if all_fold_metrics:
+        keys = set.intersection(*(set(m) for m in all_fold_metrics))
+        for k in sorted(keys):
+            vals = [m[k] for m in all_fold_metrics if isinstance(m[k], (int, float))]
+            if vals:
+                metrics[k] = float(np.mean(vals))
+                metrics[k + "_std"] = float(np.std(vals))
+    return metrics, objects
+
+
+def main(argv: Optional[List[str]] = None) -> Dict[str, Any]:
+    logging.basicConfig(level=os.environ.get("VLP_LOGLEVEL", "INFO"),
+                        format="%(asctime)s %(levelname)s %(message)s")
+    argv = list(sys.argv[1:] if argv is None else argv)
+    cfg = compose("train", argv)
+    metrics, _ = train(cfg)
+    return metrics
+
+
+if __name__ == "__main__":
+    main()

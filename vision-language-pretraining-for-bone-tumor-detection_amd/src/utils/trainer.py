@@ -1,0 +1,131 @@
+"""The subset of lightning.pytorch.Trainer that src/train.py drives for pretraining
+(SURVEY §8(b) "Loop semantics"): per step model.train(), optimizer.zero_grad(),
+loss = training_step(batch, i), loss.backward(), optimizer.step(); epoch hooks;
+validation over [lera_val, mura_val] with dataloader_idx; epoch-interval LR
+schedulers.  Lightning is not in this image; configs/trainer/default.yaml's
+`lightning.pytorch.trainer.Trainer` target resolves here (src/utils/config.py).
+
+MI355X specifics: batches reach the device through DevicePrefetcher (copy of
+batch i+1 on a side stream while step i runs); the loss is read back to the
+host only every `log_every_n_steps` steps so the HIP queue is not drained per
+step.  Multi-GPU: one process per GPU with torch.distributed initialised by
+the launcher (backend nccl = RCCL); the module's fused step performs the
+embedding all-gather and the gradient all-reduce itself, so the model is
+never wrapped in DDP.
+"""
+from __future__ import annotations
+
+import logging
+import math
+import os
+import time
+from typing import List, Optional
+
+import torch
+
+from src.data.PretrainDataModule import DevicePrefetcher
+
+logger = logging.getLogger("project")
+
+
+class Trainer:
+    def __init__(self, min_epochs: int = 1, max_epochs: int = 10, accelerator: str = "auto",
+                 devices="auto", log_every_n_steps: int = 1, max_steps: int = -1,
+                 limit_train_batches: Optional[int] = None, limit_val_batches: Optional[int] = 0,
+                 callbacks: Optional[List] = None, logger=None, enable_checkpointing: bool = False,
+                 default_root_dir: Optional[str] = None, **unused):
+        if max_epochs is not None and min_epochs is not None and min_epochs > max_epochs:
+            raise ValueError("min_epochs > max_epochs")
+        self.min_epochs, self.max_epochs = min_epochs, max_epochs
+        self.accelerator, self.devices = accelerator, devices
+        self.log_every_n_steps = max(1, int(log_every_n_steps))
+        self.max_steps = max_steps
+        self.limit_train_batches, self.limit_val_batches = limit_train_batches, limit_val_batches
+        self.callbacks = list(callbacks or [])
+        self.default_root_dir = default_root_dir
+        self.enable_checkpointing = enable_checkpointing
+        self.global_step = 0
+        self.current_epoch = 0
+        self.logged_metrics = {}
+        self.history = []            # (global_step, loss) at every logging step
+        self.step_times = []
+        if unused:
+            logger.info("Trainer: ignoring Lightning options %s", sorted(unused))
+
+    def _device(self, model):
+        return model.device
+
+    def _log(self, model, step_loss):
+        rec = {"step": self.global_step, "epoch": self.current_epoch, "train/loss": float(step_loss)}
+        for k, v in getattr(model, "logged", {}).items():
+            if torch.is_tensor(v) and v.numel() == 1:
+                rec[k] = float(v.detach())
+        self.logged_metrics.update(rec)
+        self.history.append((self.global_step, float(step_loss)))
+        rank = int(os.environ.get("RANK", "0"))
+        if rank == 0:
+            logger.info("step %d epoch %d loss %.5f", self.global_step, self.current_epoch, float(step_loss))
+
+    def fit(self, model, datamodule=None, train_dataloaders=None, val_dataloaders=None):
+        model.trainer = self
+        if datamodule is not None:
+            train_dataloaders = datamodule.train_dataloader()
+            if self.limit_val_batches:
+                val_dataloaders = datamodule.val_dataloader()
+        conf = model.configure_optimizers()
+        optimizer = conf["optimizer"] if isinstance(conf, dict) else conf
+        sched = conf.get("lr_scheduler") if isinstance(conf, dict) else None
+        self.optimizer = optimizer
+        dev = self._device(model)
+        stop = False
+        t_fit = time.perf_counter()
+        for epoch in range(self.max_epochs):
+            self.current_epoch = epoch
+            model.train()
+            if hasattr(model, "on_train_epoch_start"):
+                model.on_train_epoch_start()
+            for i, batch in enumerate(DevicePrefetcher(train_dataloaders, dev)):
+                if self.limit_train_batches is not None and i >= self.limit_train_batches:
+                    break
+                t0 = time.perf_counter()
+                optimizer.zero_grad(set_to_none=False)
+                loss = model.training_step(batch, i)
+                loss.backward()
+                optimizer.step()
+                self.global_step += 1
+                if self.global_step % self.log_every_n_steps == 0:
+                    lv = loss.detach().item()
+                    if not math.isfinite(lv):
+                        raise FloatingPointError(f"non-finite loss {lv} at step {self.global_step}")
+                    self._log(model, lv)
+                self.step_times.append(time.perf_counter() - t0)
+                if 0 < self.max_steps <= self.global_step:
+                    stop = True
+                    break
+            if hasattr(model, "on_train_epoch_end"):
+                model.on_train_epoch_end()
+            if val_dataloaders and self.limit_val_batches:
+                self.validate(model, val_dataloaders)
+            if sched is not None:
+                s = sched["scheduler"] if isinstance(sched, dict) else sched
+                s.step()
+            if stop and epoch + 1 >= (self.min_epochs or 0):
+                break
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        self.fit_seconds = time.perf_counter() - t_fit
+        return self
+
+    @torch.no_grad()
+    def validate(self, model, val_dataloaders):
+        model.eval()
+        if hasattr(model, "on_validation_epoch_start"):
+            model.on_validation_epoch_start()
+        for idx, loader in enumerate(val_dataloaders):
+            for j, batch in enumerate(DevicePrefetcher(loader, self._device(model))):
+                if self.limit_val_batches is not None and j >= self.limit_val_batches:
+                    break
+                model.validation_step(batch, j, idx)
+        if hasattr(model, "on_validation_epoch_end"):
+            model.on_validation_epoch_end()
+        model.train()

@@ -493,7 +493,10 @@ class ResNet34Tower(ArenaModule):
 class ImageTowerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, tower: ResNet34Tower, x, *params):
-        feat, saved = tower.run_forward(x, tower.training)
+        if x.dtype == torch.uint8:   # collated 1-channel upload (src/data/PretrainDataModule.py)
+            feat, saved = tower.run_forward(None, tower.training, x_u8=x)
+        else:
+            feat, saved = tower.run_forward(x, tower.training)
         ctx.tower = tower
         ctx.saved = saved if torch.is_grad_enabled() or True else None
         return feat.float()
