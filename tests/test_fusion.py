@@ -1,0 +1,181 @@
+"""Late-fusion finetune (reference src/models/baseline/FusionModule.py,
+src/utils/coral_loss/coral.py).
+
+CPU: the oracle and the product CORAL / _compute_loss against golden vectors
+produced by the reference's own coral() and FusionModule._compute_loss
+(tests/golden/make_fusion_golden.py).
+GPU: FusionModule on the HIP ResNet34 tower (fp32 parity mode) against the CPU
+oracle on the same weights and batch: logits and loss |d| <= 1e-4, parameter
+gradients rel-L2 <= 1e-3; bf16 throughput mode loss within 5e-2; a VLP
+checkpoint's image_encoder.model.* weights load into image_network.
+"""
+import functools
+import os
+import types
+
+import pytest
+import torch
+
+from oracle import weights as W
+from oracle.fusion import OracleFusion, coral as oracle_coral
+from src.utils.coral_loss.coral import coral
+
+GOLD = torch.load(os.path.join(os.path.dirname(__file__), "golden", "fusion_loss.pt"), weights_only=True)
+
+
+def _coral_cases():
+    return [k for k in GOLD if k.startswith("coral_")]
+
+
+@pytest.mark.parametrize("name", _coral_cases())
+def test_coral_vs_reference_golden(name):
+    c = GOLD[name]
+    for fn in (coral, oracle_coral):
+        s = c["source"].clone().requires_grad_()
+        t = c["target"].clone().requires_grad_()
+        loss = fn(s, t)
+        assert torch.allclose(loss, c["loss"], rtol=1e-5, atol=1e-7), (name, loss.item(), c["loss"].item())
+        if "grad_source" in c:
+            gs, gt = torch.autograd.grad(loss, (s, t))
+            assert torch.allclose(gs, c["grad_source"], rtol=1e-4, atol=1e-8)
+            assert torch.allclose(gt, c["grad_target"], rtol=1e-4, atol=1e-8)
+    assert torch.isnan(coral(torch.ones(1, 3), torch.randn(4, 3)))       # one-sample domain: NaN as the reference
+
+
+def test_compute_loss_vs_reference_golden():
+    from src.models.baseline.FusionModule import FusionModule
+    for case in GOLD["compute_loss"]:
+        lam = float(case["coral_lambda"])
+        me = types.SimpleNamespace(label_weights=case["label_weights"],
+                                   hparams=types.SimpleNamespace(coral_lambda=lam))
+        o = OracleFusion(tuple(case["label_weights"].tolist()), lam)
+        for fn in (lambda f, lg: FusionModule._compute_loss(me, f, lg, case["labels"], case["dataset"]),
+                   lambda f, lg: o.compute_loss(f, lg, case["labels"], case["dataset"])):
+            f = case["features"].clone().requires_grad_()
+            lg = case["logits"].clone().requires_grad_()
+            tot, cls, cor = fn(f, lg)
+            assert abs(tot.item() - case["loss"].item()) < 1e-6
+            assert abs(cls.item() - case["classification_loss"].item()) < 1e-6
+            assert abs(float(cor.detach()) - case["coral_loss"].item()) < 1e-6
+            gf, gl = torch.autograd.grad(tot, (f, lg), allow_unused=True)
+            assert torch.allclose(gl, case["grad_logits"], rtol=1e-5, atol=1e-8)
+            gf = torch.zeros_like(f) if gf is None else gf
+            assert torch.allclose(gf, case["grad_features"], rtol=1e-4, atol=1e-9)
+
+
+def _fusion_batch(B, H, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    x_u8 = torch.randint(0, 256, (B, 1, H, H), generator=g, dtype=torch.uint8)
+    x = ((x_u8.float() - 127.5) / 73.9).repeat(1, 3, 1, 1)
+    site = torch.nn.functional.one_hot(torch.randint(0, 9, (B,), generator=g), 9).float()
+    age = torch.nn.functional.one_hot(torch.randint(0, 4, (B,), generator=g), 4).float()
+    sex = torch.nn.functional.one_hot(torch.randint(0, 2, (B,), generator=g), 2).float()
+    return {"x-ray": x, "x-ray-u8": x_u8, "tumor": torch.tensor([0, 1] * (B // 2)),
+            "dataset": ["INTERNAL", "INTERNAL", "BTXRD", "BTXRD", "INTERNAL", "BTXRD"][:B] if B <= 6
+            else ["INTERNAL" if i % 2 else "BTXRD" for i in range(B)],
+            "anatomy_site_encoded": site, "age_encoded": age, "sex_encoded": sex}
+
+
+def _oracle(seed=0, lw=(0.7, 2.0), lam=0.5):
+    torch.manual_seed(seed)
+    o = OracleFusion(lw, lam)
+    sd = o.state_dict()
+    for k in sd:
+        if k.startswith("image_network.trunk."):
+            rk = k.replace("image_network.trunk.", "image_encoder.model.")
+            sd[k] = W.value_for(rk, sd[k].shape, seed).to(sd[k].dtype)
+    o.load_state_dict(sd)
+    return o
+
+
+def _hip(dtype, o, lw=(0.7, 2.0), lam=0.5):
+    from src.models.baseline.FusionModule import FusionModule
+    m = FusionModule("resnet34", functools.partial(torch.optim.AdamW, lr=1e-3), label_weights=lw,
+                     coral_lambda=lam, compute_dtype=dtype)
+    m.load_state_dict(o.state_dict_hip_layout(), strict=True)
+    return m
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+@pytest.mark.gpu
+def test_fusion_step_vs_oracle_fp32():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    B, H = 6, 64
+    batch = _fusion_batch(B, H)
+    o = _oracle()
+    m = _hip("fp32", o)
+    o.train()
+    m.train()
+    lo, fo = o(batch["x-ray"], batch["age_encoded"], batch["sex_encoded"], batch["anatomy_site_encoded"])
+    Lo, _, Co = o.compute_loss(fo, lo, batch["tumor"], batch["dataset"])
+    Lo.backward()
+    loss = m.training_step(batch)
+    loss.backward()
+    torch.cuda.synchronize()
+    lm, _ = m(batch["x-ray"], batch["age_encoded"], batch["sex_encoded"], batch["anatomy_site_encoded"])
+    assert (lm.detach().cpu() - lo.detach()).abs().max().item() < 1e-4
+    assert abs(loss.item() - Lo.item()) < 1e-4, (loss.item(), Lo.item())
+    assert float(m.logged["train/coral_loss"].detach()) > 0.0
+    og = {k.replace("image_network.trunk.", "image_network."): p.grad for k, p in o.named_parameters()}
+    for k, p in m.named_parameters():
+        if og[k] is None or og[k].norm() < 1e-6:    # biases feeding BatchNorm1d: analytically 0
+            continue
+        assert p.grad is not None, k
+        assert _rel(p.grad, og[k]) < 1e-3, (k, _rel(p.grad, og[k]))
+
+
+@pytest.mark.gpu
+def test_fusion_bf16_u8_and_optimizer_step(tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    B, H = 6, 64
+    batch = _fusion_batch(B, H, seed=1)
+    o = _oracle(seed=1)
+    m32 = _hip("fp32", o)
+    m16 = _hip("bf16", o)
+    l32 = m32.training_step(batch).item()
+    b16 = {k: v for k, v in batch.items() if k != "x-ray"}          # uint8 upload path
+    opt = m16.configure_optimizers()["optimizer"]
+    w0 = m16.image_network.conv1.weight.detach().clone()
+    loss = m16.training_step(b16)
+    loss.backward()
+    opt.step()
+    assert abs(loss.item() - l32) < 5e-2, (loss.item(), l32)
+    assert not torch.equal(w0, m16.image_network.conv1.weight.detach())
+    assert all(torch.isfinite(p).all() for p in m16.parameters())
+    # vision_encoder_lr groups (:144-170)
+    from src.models.baseline.FusionModule import FusionModule
+    mg = FusionModule("resnet34", functools.partial(torch.optim.AdamW, lr=1e-3), vision_encoder_lr=1e-5)
+    groups = mg.configure_optimizers()["optimizer"].param_groups
+    assert [g["name"] for g in groups] == ["image_backbone", "head_and_remaining_parameters"]
+    assert groups[0]["lr"] == 1e-5 and sum(p.numel() for p in groups[0]["params"]) == 21284672
+    # a VLP checkpoint's image encoder initialises image_network (:82-113)
+    from src.models.pretrain.VisionLanguageModule import VisionLanguageModule
+    v = VisionLanguageModule("resnet34", "tinybert", functools.partial(torch.optim.AdamW, lr=5e-5),
+                             False, False, 512, 312, 128, compute_dtype="bf16")
+    W.apply_recipe(v, 3)
+    path = tmp_path / "vlp.ckpt"
+    torch.save({"state_dict": {k: t.detach().cpu() for k, t in v.state_dict().items()}}, path)
+    mp = FusionModule("resnet34", functools.partial(torch.optim.AdamW, lr=1e-3), pretrained_vlp_module=str(path))
+    assert torch.equal(mp.image_network.layer3.get_submodule("1").conv2.weight.cpu(),
+                       v.image_encoder.model.layer3.get_submodule("1").conv2.weight.cpu())
+    with pytest.raises(ValueError):
+        FusionModule("alexnet", None)
+    with pytest.raises(NotImplementedError):
+        FusionModule("nest_small", None)
+
+
+def test_state_dict_layout_matches_reference_keys():
+    """timm resnet34(num_classes=10) + tabular MLP + combination keys; construction only (no compute)."""
+    from src.models.baseline.FusionModule import FusionModule
+    o = _oracle()
+    m = FusionModule("resnet34", functools.partial(torch.optim.AdamW, lr=1e-3), device="cpu")
+    m.load_state_dict(o.state_dict_hip_layout(), strict=True)
+    assert sum(p.numel() for p in m.parameters()) == 21291329      # 21 284 672 trunk + 5130 fc + 1506 + 21
+    assert torch.equal(m.image_network.fc.weight, o.image_network.fc.weight)
+    assert "image_network.layer4.2.bn2.running_var" in m.state_dict()
