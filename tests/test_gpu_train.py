@@ -77,3 +77,17 @@ def test_train_main_runs_and_is_deterministic():
         assert "train/loss" in metrics
         assert all(torch.isfinite(p).all() for p in objs["model"].parameters())
     assert torch.allclose(torch.tensor(hist[0]), torch.tensor(hist[1]), rtol=1e-5, atol=0)
+
+
+def test_train_fusion_experiment():
+    from src import train as T
+    from src.utils.config import compose
+    cfg = compose("train", ["experiment=baseline_imaging_and_clinical/baseline_imaging_and_clinical_resnet_34",
+                            "data.batch_size=8", "data.image_size=64", "data.n_samples=24", "data.num_workers=0",
+                            "trainer.max_epochs=2", "model.coral_lambda=0.5"])
+    metrics, objs = T.train(cfg)
+    tr = objs["trainer"]
+    assert tr.global_step == 6 and len(tr.history) == 6
+    assert all(torch.isfinite(torch.tensor(l)) for _, l in tr.history)
+    assert objs["model"].label_weights.tolist() != [1.0, 1.0]          # set from the fold's labels
+    assert "train/coral_loss" in tr.logged_metrics

@@ -130,3 +130,26 @@ def test_trainer_loop_semantics():
     assert [c for c in m2.calls if isinstance(c, tuple)] == [("step", 0), ("step", 1)]
     with pytest.raises(ValueError):
         Trainer(min_epochs=3, max_epochs=2)
+
+
+def test_downstream_datamodule_and_fusion_config():
+    from src.data.DownstreamDataModule import DownstreamDataModule
+    with pytest.raises(ValueError):
+        DownstreamDataModule(num_channels=2)
+    with pytest.raises(NotImplementedError):
+        DownstreamDataModule(synthetic=False)
+    c = compose("train", ["experiment=baseline_imaging_and_clinical/baseline_imaging_and_clinical_resnet_34",
+                          "data.num_workers=0", "data.image_size=16", "data.batch_size=4", "data.n_samples=40"])
+    assert c["model"]["_target_"] == "src.models.baseline.FusionModule.FusionModule"
+    assert c["model"]["optimizer"]["_target_"] == "torch.optim.Adam" and c["model"]["scheduler"]["T_max"] == 300
+    dm = instantiate(c["data"])
+    (fold, (w0, w1)), = list(dm.get_cv_splits())
+    labels = torch.cat([b["tumor"] for b in fold.train_dataloader()])
+    assert labels.numel() == 40
+    n0, n1 = int((labels == 0).sum()), int((labels == 1).sum())
+    assert abs(w0 - 40 / (2 * n0)) < 1e-12 and abs(w1 - 40 / (2 * n1)) < 1e-12   # DownstreamDataModule.py:330-332
+    b = next(iter(fold.train_dataloader()))
+    assert b["anatomy_site_encoded"].shape == (4, 9) and b["age_encoded"].shape == (4, 4)
+    assert b["sex_encoded"].shape == (4, 2) and b["x-ray-u8"].dtype == torch.uint8
+    assert torch.cat((b["anatomy_site_encoded"], b["age_encoded"], b["sex_encoded"]), 1).sum(1).eq(3).all()
+    assert len(fold.val_dataloader()) == 2

@@ -9,6 +9,8 @@ Same entry points and flow for the VLP pretraining experiments:
               model.label_weights, instantiate cfg.model (:109-116) and cfg.trainer
               (:163), trainer.fit(model, datamodule) (:185) -> per-fold metrics
               (:188-192), aggregated over folds (:231-262).
+The late-fusion finetune (FusionModule + DownstreamDataModule) runs through the
+same path: `experiment=baseline_imaging_and_clinical/baseline_imaging_and_clinical_resnet_34`.
 Out of scope: W&B loggers, Lightning callbacks, t-SNE /
 confusion-matrix plots, downstream zero-shot evaluation and the baseline modules.
 
@@ -70,7 +72,9 @@ def train(cfg: Dict[str, Any]) -> Tuple[Dict[str, Any], Dict[str, Any]]:
         if not model_cfg.get("scheduler"):
             model_cfg["scheduler"] = None
         model_cfg["label_weights"] = label_weights
-        if model_cfg.get("downstream_datamodule") in ({}, "null"):
+        if "FusionModule" in model_cfg["_target_"]:
+            model_cfg.pop("downstream_datamodule", None)
+        elif model_cfg.get("downstream_datamodule") in ({}, "null"):
             model_cfg["downstream_datamodule"] = None
         log.info("Train: Instantiating model <%s>", model_cfg["_target_"])
         model = instantiate(model_cfg)
