@@ -1,5 +1,5 @@
-"""Stem backward passes at bs=256, 512x512 in isolation (preallocated tensors):
-maxpool_bwd (BN sums of the routed gradient) and maxpool_bwd_apply (dy)."""
+"""Stem maxpool passes at bs=256, 512x512 in isolation (preallocated tensors):
+maxpool_bwd (BN sums of the routed gradient), maxpool_bwd_apply (dy), maxpool_fwd."""
 import os
 import sys
 
@@ -35,4 +35,9 @@ def tm(fn, it=10):
 
 print("maxpool_bwd (sums)  %.1f us" % tm(lambda: ops.maxpool_bwd(dp, idx, y0, sc, sh, mu, ist, s1, s2, stat_rep=64)))
 print("maxpool_bwd_apply   %.1f us" % tm(lambda: ops.maxpool_bwd_apply(dp, idx, y0, sc, sh, mu, ist, gam, s1[:C], s2[:C], dy)))
+po = torch.empty_like(dp)
+pidx = torch.empty_like(idx)
+yarg = torch.empty_like(dp)
+rmask = torch.empty(dp.numel() // 8, dtype=torch.uint8, device=dev)
+print("maxpool_fwd         %.1f us" % tm(lambda: ops.maxpool_fwd(y0, sc, sh, po, pidx, yarg, rmask)))
 print("copy y0->dy (ref)   %.1f us" % tm(lambda: dy.copy_(y0)))

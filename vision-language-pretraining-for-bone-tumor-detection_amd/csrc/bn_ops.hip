@@ -472,18 +472,26 @@ maxpool_fwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const T* __restri
     uint8_t bi[E];
 #pragma unroll
     for (int j = 0; j < E; ++j) { best[j] = -INFINITY; bi[j] = 0; ya[j] = 0.f; }
-    for (int kh = 0; kh < 3; ++kh) {
-      int h = ho * 2 - 1 + kh;
-      if ((unsigned)h >= (unsigned)H) continue;
-      for (int kw = 0; kw < 3; ++kw) {
-        int w = wo * 2 - 1 + kw;
-        if ((unsigned)w >= (unsigned)W) continue;
-        Chunk<T>::unpack(ldg16(y + (((size_t)n * H + h) * W + w) * C + c0), v);
+    // all nine taps are loaded before any is used (clamped in-bounds addresses,
+    // validity applied at the compare), so the gathers of a window fly together
+    const T* img = y + (size_t)n * H * W * C + c0;
+    uint4 raw[9];
+    bool ok[9];
 #pragma unroll
-        for (int j = 0; j < E; ++j) {
-          float q = fmaxf(fmaf(v[j], a[j], b[j]), 0.f);
-          if (q > best[j]) { best[j] = q; bi[j] = (uint8_t)(kh * 3 + kw); ya[j] = v[j]; }
-        }
+    for (int k = 0; k < 9; ++k) {
+      const int h = ho * 2 - 1 + k / 3, w = wo * 2 - 1 + k % 3;
+      ok[k] = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+      const int hc = h < 0 ? 0 : (h >= H ? H - 1 : h), wc = w < 0 ? 0 : (w >= W ? W - 1 : w);
+      raw[k] = ldg16(img + ((size_t)hc * W + wc) * C);
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      if (!ok[k]) continue;
+      Chunk<T>::unpack(raw[k], v);
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        float q = fmaxf(fmaf(v[j], a[j], b[j]), 0.f);
+        if (q > best[j]) { best[j] = q; bi[j] = (uint8_t)k; ya[j] = v[j]; }
       }
     }
     const uint4 pk = Chunk<T>::pack(best);
