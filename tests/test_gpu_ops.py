@@ -480,3 +480,51 @@ def test_stem_wgrad_many_splits(ops):
     ops.stem_wgrad_into(nhwc(dy).to(torch.bfloat16).cuda(), xp, N, H, W, g)
     torch.cuda.synchronize()
     assert rel(g.cpu(), w.grad) < 2e-3
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("H,W", [(16, 32), (15, 16), (18, 18)])
+def test_maxpool_bwd_sums_and_apply(ops, dt, H, W):
+    """Stem backward: the pooled gradient routed to each window's recorded argmax,
+    masked by the stem ReLU, its BN sums (sum g, sum g*xhat) and the folded BN
+    backward dy = k*g + b*y + c, against torch.  Even H, W take the 2x2-block
+    kernel, odd ones the per-pixel kernel."""
+    torch.manual_seed(5)
+    N, C = 3, 64
+    y = torch.randn(N, H, W, C).to(dt)
+    sc, sh = torch.rand(C) + 0.5, torch.randn(C) * 0.3
+    mu, ist, gam = torch.randn(C) * 0.1, torch.rand(C) + 0.5, torch.rand(C) + 0.5
+    z = torch.relu(y.float() * sc + sh)
+    _, ridx = F.max_pool2d(nchw(z), 3, 2, 1, return_indices=True)
+    Ho, Wo = ridx.shape[2], ridx.shape[3]
+    out = torch.empty(N, Ho, Wo, C, dtype=dt, device="cuda")
+    idx = torch.empty(N, Ho, Wo, C, dtype=torch.uint8, device="cuda")
+    ops.maxpool_fwd(y.cuda(), sc.cuda(), sh.cuda(), out, idx)
+    dp = torch.randn(N, Ho, Wo, C).to(dt)
+    # torch routing from the kernel's own argmax taps
+    t = idx.long().cpu()
+    hh = torch.arange(Ho).view(1, Ho, 1, 1) * 2 - 1 + t // 3
+    ww = torch.arange(Wo).view(1, 1, Wo, 1) * 2 - 1 + t % 3
+    g = torch.zeros(N, H, W, C, dtype=torch.float64)
+    n = torch.arange(N).view(N, 1, 1, 1).expand_as(t)
+    c = torch.arange(C).view(1, 1, 1, C).expand_as(t)
+    g.index_put_((n, hh, ww, c), dp.double(), accumulate=True)
+    g = torch.where((y.float() * sc + sh) > 0, g, torch.zeros_like(g))
+    xhat = (y.double() - mu.double()) * ist.double()
+    rg, rgx = g.sum((0, 1, 2)), (g * xhat).sum((0, 1, 2))
+    s1 = torch.zeros(C, dtype=torch.float64, device="cuda")
+    s2 = torch.zeros_like(s1)
+    ops.maxpool_bwd(dp.cuda(), idx, y.cuda(), sc.cuda(), sh.cuda(), mu.cuda(), ist.cuda(), s1, s2)
+    torch.cuda.synchronize()
+    assert torch.allclose(s1.cpu(), rg, rtol=1e-4, atol=1e-3)
+    assert torch.allclose(s2.cpu(), rgx, rtol=1e-4, atol=1e-3)
+    dy = torch.empty(N, H, W, C, dtype=dt, device="cuda")
+    ops.maxpool_bwd_apply(dp.cuda(), idx, y.cuda(), sc.cuda(), sh.cuda(), mu.cuda(), ist.cuda(), gam.cuda(),
+                          s1, s2, dy)
+    torch.cuda.synchronize()
+    cnt = N * H * W
+    k = gam.double() * ist.double()
+    ref = k * g - k * ist.double() * (rgx / cnt) * y.double() + (-k * rg / cnt + k * ist.double() * (rgx / cnt)
+                                                                 * mu.double())
+    tol = 2e-2 if dt == torch.bfloat16 else 1e-4
+    assert torch.allclose(dy.double().cpu(), ref, rtol=tol, atol=tol * ref.abs().max().item())

@@ -696,6 +696,149 @@ maxpool_bwd_kernel(int N, int H, int W, int C, int Ho, int Wo, const T* __restri
   }
 }
 
+// ---- stem backward on 2x2 input blocks (H, W even) ----
+// Input rows {2a, 2a+1} x cols {2b, 2b+1} are covered by exactly the pooled
+// outputs (a|a+1, b|b+1), so one set of four dp/idx gathers serves four input
+// pixels (the per-pixel walk above issues four gathers per pixel).  Taps
+// kh*3+kw: (2a,2b) <- P00 tap 4; (2a,2b+1) <- P00 tap 5, P01 tap 3;
+// (2a+1,2b) <- P00 tap 7, P10 tap 1; (2a+1,2b+1) <- P00 8, P01 6, P10 2, P11 0.
+constexpr int kMpPairs = 8;   // row pairs per block (16 input rows)
+template <typename T>
+struct Mp4Loads {
+  uint4 p[4];     // dp at (a,b) (a,b+1) (a+1,b) (a+1,b+1)
+  uint2 ib[4];
+  uint4 y[4];     // y at (2a,2b) (2a,2b+1) (2a+1,2b) (2a+1,2b+1)
+  bool v01, v10;
+};
+template <typename T>
+__device__ __forceinline__ void mp4_fetch(const T* __restrict__ dp, const uint8_t* __restrict__ idx,
+                                          const T* __restrict__ y, int n, int a, int b, int c0, int C,
+                                          int H, int W, int Ho, int Wo, Mp4Loads<T>& L) {
+  L.v10 = a + 1 < Ho;
+  L.v01 = b + 1 < Wo;
+  const int a1 = L.v10 ? a + 1 : a, b1 = L.v01 ? b + 1 : b;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int ho = (q >> 1) ? a1 : a, wo = (q & 1) ? b1 : b;
+    const size_t po = (((size_t)n * Ho + ho) * Wo + wo) * C + c0;
+    L.p[q] = ldg16(dp + po);
+    if constexpr (Chunk<T>::N == 8) {
+      L.ib[q] = *reinterpret_cast<const uint2*>(idx + po);
+    } else {
+      L.ib[q].x = *reinterpret_cast<const unsigned*>(idx + po);
+      L.ib[q].y = 0;
+    }
+    const size_t yo = (((size_t)n * H + 2 * a + (q >> 1)) * W + 2 * b + (q & 1)) * C + c0;
+    L.y[q] = ldg16(y + yo);
+  }
+}
+template <typename T>
+__device__ __forceinline__ void mp4_route(const Mp4Loads<T>& L, float (*g)[Chunk<T>::N]) {
+  constexpr int E = Chunk<T>::N;
+  float f[4][E];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) Chunk<T>::unpack(L.p[q], f[q]);
+  const bool v11 = L.v01 && L.v10;
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    unsigned t[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t[q] = (((j >> 2) ? L.ib[q].y : L.ib[q].x) >> (8 * (j & 3))) & 255u;
+    g[0][j] = t[0] == 4u ? f[0][j] : 0.f;
+    g[1][j] = (t[0] == 5u ? f[0][j] : 0.f) + ((L.v01 && t[1] == 3u) ? f[1][j] : 0.f);
+    g[2][j] = (t[0] == 7u ? f[0][j] : 0.f) + ((L.v10 && t[2] == 1u) ? f[2][j] : 0.f);
+    g[3][j] = (t[0] == 8u ? f[0][j] : 0.f) + ((L.v01 && t[1] == 6u) ? f[1][j] : 0.f) +
+              ((L.v10 && t[2] == 2u) ? f[2][j] : 0.f) + ((v11 && t[3] == 0u) ? f[3][j] : 0.f);
+  }
+}
+
+template <typename T, bool APPLY>
+__global__ void __launch_bounds__(256)
+maxpool_bwd2_kernel(int N, int H, int W, int C, int Ho, int Wo, const T* __restrict__ dp,
+                    const uint8_t* __restrict__ idx, const T* __restrict__ y,
+                    const float* __restrict__ sc, const float* __restrict__ sh,
+                    const float* __restrict__ mean, const float* __restrict__ istd,
+                    const float* __restrict__ gamma, const double* __restrict__ sg,
+                    const double* __restrict__ sgx, T* __restrict__ dy, double* sum_g, double* sum_gx,
+                    int rep) {
+  constexpr int E = Chunk<T>::N;
+  const int cpr = C / E;
+  const int t = threadIdx.x;
+  const int c0 = (t % cpr) * E;
+  const int bstep = 256 / cpr;
+  const int HP = H / 2, WP = W / 2;
+  const int bands = (HP + kMpPairs - 1) / kMpPairs;
+  const int band = blockIdx.x % bands;
+  const int n = blockIdx.x / bands;
+  float a[E], b[E], mu[E], is[E], ka[E], ba[E], ca[E], ag[E], ax[E];
+  const float inv_count = 1.f / (float)((double)N * H * W);
+#pragma unroll
+  for (int j = 0; j < E; ++j) {
+    const int c = c0 + j;
+    a[j] = sc[c]; b[j] = sh[c]; mu[j] = mean[c]; is[j] = istd[c];
+    ag[j] = ax[j] = 0.f;
+    if constexpr (APPLY) {
+      const float k = gamma[c] * is[j];
+      const float mg = (float)(sg[c] * (double)inv_count), mgx = (float)(sgx[c] * (double)inv_count);
+      ka[j] = k; ba[j] = -k * is[j] * mgx; ca[j] = -k * mg + k * is[j] * mgx * mu[j];
+    } else {
+      ka[j] = ba[j] = ca[j] = 0.f;
+    }
+  }
+  const int b0 = t / cpr;
+  const int nb = b0 < WP ? (WP - b0 + bstep - 1) / bstep : 0;
+  int pairs = HP - band * kMpPairs;
+  if (pairs > kMpPairs) pairs = kMpPairs;
+  const int total = pairs * nb;
+  Mp4Loads<T> cur, nxt;
+  if (total > 0) mp4_fetch<T>(dp, idx, y, n, band * kMpPairs, b0, c0, C, H, W, Ho, Wo, cur);
+  for (int it = 0; it < total; ++it) {
+    const int r = it / nb, jb = it - r * nb;
+    const int pa = band * kMpPairs + r, pb = b0 + jb * bstep;
+    if (it + 1 < total) {
+      const int r1 = (it + 1) / nb, j1 = it + 1 - r1 * nb;
+      mp4_fetch<T>(dp, idx, y, n, band * kMpPairs + r1, b0 + j1 * bstep, c0, C, H, W, Ho, Wo, nxt);
+    }
+    float g[4][E];
+    mp4_route<T>(cur, g);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float yv[E], d[E];
+      Chunk<T>::unpack(cur.y[q], yv);
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        const float gg = fmaf(yv[j], a[j], b[j]) > 0.f ? g[q][j] : 0.f;
+        if constexpr (APPLY) {
+          d[j] = fmaf(ka[j], gg, fmaf(ba[j], yv[j], ca[j]));
+        } else {
+          ag[j] += gg;
+          ax[j] += gg * ((yv[j] - mu[j]) * is[j]);
+        }
+      }
+      if constexpr (APPLY)
+        stg16(dy + (((size_t)n * H + 2 * pa + (q >> 1)) * W + 2 * pb + (q & 1)) * C + c0, Chunk<T>::pack(d));
+    }
+    cur = nxt;
+  }
+  if constexpr (!APPLY) {
+    __shared__ float red[2][256][E];
+#pragma unroll
+    for (int j = 0; j < E; ++j) { red[0][t][j] = ag[j]; red[1][t][j] = ax[j]; }
+    __syncthreads();
+    if (t < cpr) {
+      for (int q = t + cpr; q < 256; q += cpr)
+#pragma unroll
+        for (int j = 0; j < E; ++j) { ag[j] += red[0][q][j]; ax[j] += red[1][q][j]; }
+      const size_t ro = (size_t)(blockIdx.x % rep) * C + c0;
+#pragma unroll
+      for (int j = 0; j < E; ++j) {
+        atomicAdd(sum_g + ro + j, (double)ag[j]);
+        atomicAdd(sum_gx + ro + j, (double)ax[j]);
+      }
+    }
+  }
+}
+
 // ---- global average pool: feat[n][c] = mean_hw x[n][hw][c] ----
 template <typename T>
 __global__ void avgpool_fwd_kernel(int N, int HW, int C, const T* __restrict__ x, T* __restrict__ feat) {
@@ -887,8 +1030,20 @@ VLP_EXPORT int vlp_maxpool_bwd(int dtype, int N, int H, int W, int C, const void
   int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
   int epc = dtype == VLP_BF16 ? 8 : 4;
   if (256 % (C / epc)) return (int)hipErrorInvalidValue;
-  dim3 grid((unsigned)(N * ((H + kMpRows - 1) / kMpRows)));
   if (stat_rep < 1) stat_rep = 1;
+  if (!(H & 1) && !(W & 1)) {
+    dim3 g2((unsigned)(N * ((H / 2 + kMpPairs - 1) / kMpPairs)));
+    if (dtype == VLP_BF16)
+      hipLaunchKernelGGL((maxpool_bwd2_kernel<bf16, false>), g2, dim3(256), 0, st, N, H, W, C, Ho, Wo,
+                         (const bf16*)dp, idx, (const bf16*)y, sc, sh, mean, istd, nullptr, nullptr,
+                         nullptr, nullptr, sum_g, sum_gx, stat_rep);
+    else
+      hipLaunchKernelGGL((maxpool_bwd2_kernel<float, false>), g2, dim3(256), 0, st, N, H, W, C, Ho, Wo,
+                         (const float*)dp, idx, (const float*)y, sc, sh, mean, istd, nullptr, nullptr,
+                         nullptr, nullptr, sum_g, sum_gx, stat_rep);
+    return (int)hipGetLastError();
+  }
+  dim3 grid((unsigned)(N * ((H + kMpRows - 1) / kMpRows)));
   if (dtype == VLP_BF16)
     hipLaunchKernelGGL((maxpool_bwd_kernel<bf16, false>), grid, dim3(256), 0, st, N, H, W, C, Ho, Wo,
                        (const bf16*)dp, idx, (const bf16*)y, sc, sh, mean, istd, nullptr, nullptr, nullptr,
@@ -909,6 +1064,18 @@ VLP_EXPORT int vlp_maxpool_bwd_apply(int dtype, int N, int H, int W, int C, cons
   int Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
   int epc = dtype == VLP_BF16 ? 8 : 4;
   if (256 % (C / epc)) return (int)hipErrorInvalidValue;
+  if (!(H & 1) && !(W & 1)) {
+    dim3 g2((unsigned)(N * ((H / 2 + kMpPairs - 1) / kMpPairs)));
+    if (dtype == VLP_BF16)
+      hipLaunchKernelGGL((maxpool_bwd2_kernel<bf16, true>), g2, dim3(256), 0, st, N, H, W, C, Ho, Wo,
+                         (const bf16*)dp, idx, (const bf16*)y, sc, sh, mean, istd, gamma, sum_g, sum_gx,
+                         (bf16*)dy, nullptr, nullptr, 1);
+    else
+      hipLaunchKernelGGL((maxpool_bwd2_kernel<float, true>), g2, dim3(256), 0, st, N, H, W, C, Ho, Wo,
+                         (const float*)dp, idx, (const float*)y, sc, sh, mean, istd, gamma, sum_g, sum_gx,
+                         (float*)dy, nullptr, nullptr, 1);
+    return (int)hipGetLastError();
+  }
   dim3 grid((unsigned)(N * ((H + kMpRows - 1) / kMpRows)));
   if (dtype == VLP_BF16)
     hipLaunchKernelGGL((maxpool_bwd_kernel<bf16, true>), grid, dim3(256), 0, st, N, H, W, C, Ho, Wo,
