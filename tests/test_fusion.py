@@ -179,3 +179,36 @@ def test_state_dict_layout_matches_reference_keys():
     assert sum(p.numel() for p in m.parameters()) == 21291329      # 21 284 672 trunk + 5130 fc + 1506 + 21
     assert torch.equal(m.image_network.fc.weight, o.image_network.fc.weight)
     assert "image_network.layer4.2.bn2.running_var" in m.state_dict()
+
+
+@pytest.mark.gpu
+def test_fusion_all_reduce_gradients_single_rank():
+    """The trainer's DP hook on FusionModule: tower gradients alias the flat arena, so the
+    reduction is one RCCL call over it plus one over the head (world 1: values unchanged)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import socket
+    import torch.distributed as dist
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(s.getsockname()[1]))
+    s.close()
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        o = _oracle(seed=2)
+        m = _hip("bf16", o)
+        opt = m.configure_optimizers()["optimizer"]
+        batch = _fusion_batch(6, 64, seed=2)
+        for _ in range(2):          # second step: gradients accumulate into the existing p.grad
+            opt.zero_grad(set_to_none=False)
+            m.training_step(batch).backward()
+        tower = m.image_network
+        p0 = tower.conv1.weight
+        assert p0.grad.data_ptr() == tower.arena.gview("conv1.weight").data_ptr()
+        before = {n: p.grad.clone() for n, p in m.named_parameters()}
+        m.all_reduce_gradients(1)
+        torch.cuda.synchronize()
+        for n, p in m.named_parameters():
+            assert torch.equal(p.grad, before[n]), n
+    finally:
+        dist.destroy_process_group()

@@ -124,6 +124,32 @@ class FusionModule(_Base):
     def device(self):
         return self.combination_network.weight.device
 
+    def all_reduce_gradients(self, world: int) -> None:
+        """Data-parallel gradient mean (DDP semantics, called by the trainer after
+        backward): one SUM all-reduce over the tower's flat gradient arena and one
+        over the ~6.7k head gradients, both scaled by 1/world."""
+        dist = torch.distributed
+        tower = self.image_network
+        slots = [(owner._parameters[attr], full) for owner, attr, full in tower._param_slots]
+        aliased = all(p.grad is not None and p.grad.data_ptr() == tower.arena.gview(full).data_ptr()
+                      for p, full in slots)
+        if aliased:          # tower gradients live in the arena: one call over the flat buffer
+            arena = tower.arena.grad
+            dist.all_reduce(arena)
+            arena.mul_(1.0 / world)
+            head = [p for n, p in self.named_parameters()
+                    if p.grad is not None and (not n.startswith("image_network.") or ".fc." in n)]
+        else:
+            head = [p for p in self.parameters() if p.grad is not None]
+        if head:
+            flat = torch.cat([p.grad.reshape(-1) for p in head])
+            dist.all_reduce(flat)
+            flat.mul_(1.0 / world)
+            off = 0
+            for p in head:
+                p.grad.copy_(flat[off:off + p.numel()].view_as(p.grad))
+                off += p.numel()
+
     def get_image_network(self):
         return self.image_network
 

@@ -199,6 +199,10 @@ class _SymCEFn(torch.autograd.Function):
 
 
 class VisionLanguageModule(_Base):
+    # the fused step all-gathers embeddings and all-reduces the gradient arenas
+    # itself (vlp_amd.clip_model.ClipStepFn); trainers must not reduce again
+    handles_dp_collectives = True
+
     def __init__(
         self,
         image_model,

@@ -9,9 +9,13 @@ MI355X specifics: batches reach the device through DevicePrefetcher (copy of
 batch i+1 on a side stream while step i runs); the loss is read back to the
 host only every `log_every_n_steps` steps so the HIP queue is not drained per
 step.  Multi-GPU: one process per GPU with torch.distributed initialised by
-the launcher (backend nccl = RCCL); the module's fused step performs the
-embedding all-gather and the gradient all-reduce itself, so the model is
-never wrapped in DDP.
+the launcher (backend nccl = RCCL); VisionLanguageModule's fused step performs
+the embedding all-gather and the gradient all-reduce itself
+(`handles_dp_collectives`), so the model is never wrapped in DDP.  For other
+modules (FusionModule) the trainer averages gradients after backward as DDP
+would: the module's `all_reduce_gradients()` when it has one (one RCCL call
+over the ResNet34 tower's flat gradient arena), else one flat SUM all-reduce
+over every gradient, divided by the world size.
 """
 from __future__ import annotations
 
@@ -55,6 +59,29 @@ class Trainer:
     def _device(self, model):
         return model.device
 
+    @staticmethod
+    def _dp_world():
+        d = torch.distributed
+        return d.get_world_size() if d.is_available() and d.is_initialized() else 1
+
+    @staticmethod
+    def average_gradients(model, world: int) -> None:
+        """DDP-equivalent gradient mean across ranks (one bucket)."""
+        if hasattr(model, "all_reduce_gradients"):
+            model.all_reduce_gradients(world)
+            return
+        params = [p for p in model.parameters() if p.requires_grad and p.grad is not None]
+        if not params:
+            return
+        flat = torch.cat([p.grad.reshape(-1) for p in params])
+        torch.distributed.all_reduce(flat)
+        flat.mul_(1.0 / world)
+        off = 0
+        for p in params:
+            n = p.numel()
+            p.grad.copy_(flat[off:off + n].view_as(p.grad))
+            off += n
+
     def _log(self, model, step_loss):
         rec = {"step": self.global_step, "epoch": self.current_epoch, "train/loss": float(step_loss)}
         for k, v in getattr(model, "logged", {}).items():
@@ -77,6 +104,8 @@ class Trainer:
         sched = conf.get("lr_scheduler") if isinstance(conf, dict) else None
         self.optimizer = optimizer
         dev = self._device(model)
+        world = self._dp_world()
+        reduce_grads = world > 1 and not getattr(model, "handles_dp_collectives", False)
         stop = False
         t_fit = time.perf_counter()
         for epoch in range(self.max_epochs):
@@ -91,6 +120,8 @@ class Trainer:
                 optimizer.zero_grad(set_to_none=False)
                 loss = model.training_step(batch, i)
                 loss.backward()
+                if reduce_grads:
+                    self.average_gradients(model, world)
                 optimizer.step()
                 self.global_step += 1
                 if self.global_step % self.log_every_n_steps == 0:
