@@ -167,7 +167,7 @@ def _dp_worker(rank, world, port, q):
     m = _Toy()
     data = [{"x": torch.tensor([1.0, 2.0, 3.0]) * (rank + 1)}]
     T(max_epochs=1).fit(m, train_dataloaders=data)
-    q.put((rank, m.w.detach().clone()))
+    q.put((rank, m.w.detach().tolist()))          # plain lists: no fd-shared storage
     dist.barrier()
     dist.destroy_process_group()
 
@@ -186,7 +186,7 @@ def test_trainer_averages_gradients_gloo_ws2():
     procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in range(2))
+    res = {r: torch.tensor(w) for r, w in (q.get(timeout=120) for _ in range(2))}
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
