@@ -18,7 +18,8 @@ pytestmark = pytest.mark.gpu
 
 _ARGS = ["experiment=pretrain/pretrain_resnet34_tinybert", "data.batch_size=4", "data.image_size=64",
          "data.n_samples=16", "data.num_workers=0", "trainer.max_epochs=1", "model.compute_dtype=fp32",
-         "model.text_dropout=0.0"]
+         "model.text_dropout=0.0", "downstream_data.image_size=64", "downstream_data.n_samples=32",
+         "downstream_data.n_val_samples=16", "downstream_data.batch_size=8", "downstream_data.num_workers=0"]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -76,6 +77,10 @@ def test_train_main_runs_and_is_deterministic():
         assert all(torch.isfinite(torch.tensor(h)) for h in hist[-1])
         assert "train/loss" in metrics
         assert all(torch.isfinite(p).all() for p in objs["model"].parameters())
+        # LinearProbeCallback ran at epoch 0 on the HIP encoder's eval-mode features
+        lg = objs["model"].logged
+        assert 0.0 <= float(lg["downstream_validation/linear_probe_auroc"]) <= 1.0
+        assert 0.0 <= float(lg["downstream_validation/linear_probe_balanced_accuracy"]) <= 1.0
     assert torch.allclose(torch.tensor(hist[0]), torch.tensor(hist[1]), rtol=1e-5, atol=0)
 
 

@@ -198,3 +198,51 @@ def test_trainer_averages_gradients_gloo_ws2():
         grads.append(w.grad)
     ref = torch.ones(3) - 0.1 * (grads[0] + grads[1]) / 2
     assert torch.allclose(res[0], res[1]) and torch.allclose(res[0], ref, atol=1e-6)
+
+
+def test_linear_probe_callback_host_logic():
+    """LinearProbeCallback (reference LinearProbeCallback.py:17-116) with a stand-in encoder on CPU:
+    the every-n-epochs gate, the concatenated validation sets and sklearn's metrics."""
+    import numpy as np
+    from sklearn.linear_model import LogisticRegression
+    from sklearn.metrics import balanced_accuracy_score, roc_auc_score
+    from src.data.DownstreamDataModule import DownstreamDataModule
+    from src.utils.LinearProbeCallback import LinearProbeCallback
+
+    dm = DownstreamDataModule(batch_size=8, num_workers=0, image_size=8, n_samples=48, n_val_samples=16)
+    fold, _ = next(dm.get_cv_splits())
+    cb = LinearProbeCallback(fold.train_dataloader(), fold.val_dataloader(), every_n_epochs=5)
+    assert len(cb.val_dataloader.dataset) == 32
+
+    class Enc(torch.nn.Module):
+        def forward(self, x):                              # uint8 [B,1,8,8] -> 64-d features
+            return x.float().flatten(1) / 255.0
+
+    class Mod:
+        image_encoder = Enc()
+        device = torch.device("cpu")
+        logged = {}
+
+        def log(self, k, v, **kw):
+            self.logged[k] = v
+
+    m = Mod()
+    cb.on_validation_start(types_ns(current_epoch=1), m)
+    assert m.logged == {}
+    cb.on_validation_start(types_ns(current_epoch=5), m)
+    X = np.concatenate([b["x-ray-u8"].float().flatten(1).numpy() / 255.0 for b in fold.train_dataloader()])
+    # the train loader shuffles: refit on the callback's own extraction instead
+    Xt, yt = cb._extract_features(Enc(), cb.train_dataloader, torch.device("cpu"))
+    Xv, yv = cb._extract_features(Enc(), cb.val_dataloader, torch.device("cpu"))
+    assert Xt.shape == (48, 64) and Xv.shape == (32, 64) and X.shape == (48, 64)
+    clf = LogisticRegression(max_iter=1000, solver="lbfgs").fit(Xt, yt)
+    # (the fit inside the callback saw the shuffled order: lbfgs agrees to round-off)
+    assert abs(m.logged["downstream_validation/linear_probe_auroc"]
+               - roc_auc_score(yv, clf.predict_proba(Xv)[:, 1])) < 1e-3
+    assert abs(m.logged["downstream_validation/linear_probe_balanced_accuracy"]
+               - balanced_accuracy_score(yv, clf.predict(Xv))) < 0.05
+
+
+def types_ns(**kw):
+    import types
+    return types.SimpleNamespace(sanity_checking=False, **kw)

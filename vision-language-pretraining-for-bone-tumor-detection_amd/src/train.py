@@ -78,8 +78,15 @@ def train(cfg: Dict[str, Any]) -> Tuple[Dict[str, Any], Dict[str, Any]]:
             model_cfg["downstream_datamodule"] = None
         log.info("Train: Instantiating model <%s>", model_cfg["_target_"])
         model = instantiate(model_cfg)
+        callbacks = []
+        if cfg.get("downstream_data") and "VisionLanguageModule" in model_cfg["_target_"]:   # :123-134
+            from src.utils.LinearProbeCallback import LinearProbeCallback
+            ds_dm = instantiate(cfg["downstream_data"])
+            dm, _ = next(ds_dm.get_cv_splits())
+            callbacks.append(LinearProbeCallback(dm.train_dataloader(), dm.val_dataloader()))
+            log.info("Train: Added LinearProbeCallback to callbacks.")
         log.info("Train: Instantiating trainer <%s>", cfg["trainer"]["_target_"])
-        trainer = instantiate(cfg["trainer"], callbacks=[], logger=None)
+        trainer = instantiate(cfg["trainer"], callbacks=callbacks, logger=None)
         objects.update(model=model, trainer=trainer)
         if cfg.get("train", True):
             trainer.fit(model=model, datamodule=fold_dm)

@@ -110,14 +110,16 @@ def compose(config_name: str = "train", overrides: Optional[List[str]] = None,
     choices.update(cli_choice)
     if choices.get("experiment") not in (None, "null"):
         exp = _load(_group_file(config_dir, "experiment", choices["experiment"]))
+        if "experiment" not in [g for _, g, _, _ in entries]:
+            entries.append(("group", "experiment", "experiment", None))
+        at = [g for _, g, _, _ in entries].index("experiment")
         for kind, g, p, c in _parse_defaults(exp.pop("defaults", [])):
             if kind == "override":
                 if g not in cli_choice:          # the command line beats the experiment
                     choices[g] = c
-            elif kind == "group":
-                entries.append(("group", g, p, c))
-        if "experiment" not in [g for _, g, _, _ in entries]:
-            entries.append(("group", "experiment", "experiment", None))
+            elif kind == "group":                # merged before the experiment's own keys (_self_ last)
+                entries.insert(at, ("group", g, p, c))
+                at += 1
     else:
         exp = None
     cfg: dict = {}

@@ -50,6 +50,7 @@ class Trainer:
         self.enable_checkpointing = enable_checkpointing
         self.global_step = 0
         self.current_epoch = 0
+        self.sanity_checking = False
         self.logged_metrics = {}
         self.history = []            # (global_step, loss) at every logging step
         self.step_times = []
@@ -135,6 +136,9 @@ class Trainer:
                     break
             if hasattr(model, "on_train_epoch_end"):
                 model.on_train_epoch_end()
+            for cb in self.callbacks:               # e.g. LinearProbeCallback (every n-th epoch)
+                if hasattr(cb, "on_validation_start"):
+                    cb.on_validation_start(self, model)
             if val_dataloaders and self.limit_val_batches:
                 self.validate(model, val_dataloaders)
             if sched is not None:
