@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--seq-len", type=int, default=40)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--input", default="fp32", choices=["fp32", "u8"],
+                    help="HBM-resident image form: the reference's fp32 3-channel batch or the uint8 upload")
     ap.add_argument("--cpu-sample-batch", type=int, default=32)
     ap.add_argument("--cpu-sample-steps", type=int, default=3)
     ap.add_argument("--roofline-kernel", default="auto")
@@ -69,10 +71,14 @@ def setup_dist(args):
     return 0, 1, 0
 
 
-def make_batch(B, H, T, device, seed):
+def make_batch(B, H, T, device, seed, form="fp32"):
+    """form "fp32": the reference's collated x-ray [B,3,H,W] fp32; "u8": the 1-channel
+    uint8 radiograph (x-ray-u8 [B,1,H,W]) that the module normalises on the device
+    (src/data/PretrainDataModule.py's default upload), same pixels."""
     from tests.golden.synth import synth_batch
-    b = synth_batch(B, H, T, seed)
-    return {"x-ray": b["x-ray"].to(device), "label": b["label"].to(device), "caption": b["caption"],
+    b = synth_batch(B, H, T, seed, with_u8=form == "u8")
+    img = {"x-ray-u8": b["x-ray-u8"].to(device)} if form == "u8" else {"x-ray": b["x-ray"].to(device)}
+    return {**img, "label": b["label"].to(device), "caption": b["caption"],
             "caption_tokenized": {k: v.to(device) for k, v in b["caption_tokenized"].items()}}
 
 
@@ -213,7 +219,7 @@ def main():
                                  False, False, 512, 312, 128, compute_dtype=args.dtype, device=dev)
     model.train()
     opt = model.configure_optimizers()["optimizer"]
-    batch = make_batch(args.batch, args.image_size, args.seq_len, dev, seed=rank)
+    batch = make_batch(args.batch, args.image_size, args.seq_len, dev, seed=rank, form=args.input)
 
     def step():
         opt.zero_grad()
@@ -275,7 +281,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": args.dtype,
-            "data": "synthetic (seeded uint8 radiographs normalised to 3-ch fp32, seeded token ids; random-init weights)",
+            "data": ("synthetic (seeded uint8 radiographs, "
+                     + ("HBM-resident as the uint8 1-channel upload, normalised on the device"
+                        if args.input == "u8" else "normalised to 3-ch fp32")
+                     + "; seeded token ids; random-init weights)"),
             "config": {"workload": "ResNet34+TinyBERT CLIP pretrain step (fwd+bwd+global-batch InfoNCE+AdamW)",
                        "global_batch": world * args.batch, "per_gpu_batch": args.batch,
                        "image_size": args.image_size, "seq_len": args.seq_len,
