@@ -1,28 +1,33 @@
-"""The bf16 throughput path at the benchmark resolution (512x512, T=40).
+"""The bf16 throughput path at the benchmark configuration (BASELINE configs[1]:
+bs = 256, 512 x 512, T = 40) against the fp32 CPU oracle on the same weights
+(the name-keyed recipe) and the same batch.
 
-The oracle-pinned model tests run at 64x64 / 96x96, where layer 1 is 16-24
-pixels wide and the large-tile GEMMs and the row-streaming layer-1 convolution
-(W = 128) never launch.  Here a B=2 step at 512x512 runs once in bf16 and once
-in fp32 parity mode (whose GEMMs are the register-staged fp32 kernels, pinned
-to the oracle by test_gpu_model.py), so every bf16 fast path of the image
-tower is checked end to end against an independent implementation.
+This is the engine the bench measures: the LDS-DMA big-tile GEMMs, the W = 128
+layer-1 rows kernel, the full-size stem and maxpool, the bf16 text tower --
+none of which run in the fp32 parity-mode tests.  One train-mode step (batch-
+statistics BN, text dropout off) on each side; the oracle's fp32 forward +
+backward of the 256-pair batch takes ~45-60 s on 16 host cores.
 
-Both runs use the module's own timm-style init (kaiming, zero-init last BN of
-each block).  Tolerances (bf16 storage + fp32 accumulation vs fp32): loss
-|delta| <= 5e-2, probe features rel-L2 <= 5e-2, conv / projection weight
-gradients rel-L2 <= 0.35.  Weight gradients of train-mode BN stacks are
-sums with heavy cancellation (xhat has zero batch mean), so bf16 rounding of
-the stored activations alone moves them by 10-25 % here (measured with
-tools/diag_bf16.py); a wrong tap, flip or missing term moves them by ~100 %.
+Gates (bf16 storage, fp32 accumulation, vs fp32; measured values are printed):
+  loss |delta| <= 5e-2 (measured ~1e-3)
+  eval-mode probe features (first 32 images) rel-L2 <= 2e-2
+  embeddings rel-L2 <= 2e-2
+  conv weight gradients: rel-L2 <= 0.10 each (BN-stack weight gradients are
+    sums with cancellation: xhat has zero batch mean), median <= 0.03
+  projection gradients rel-L2 <= 0.05
 """
 import functools
+import statistics
 
 import pytest
 import torch
 
+from oracle import weights as W
+from oracle.clip import OracleVLP, compute_loss
 from tests.golden.synth import synth_batch
 
 pytestmark = pytest.mark.gpu
+B, H, T = 256, 512, 40
 
 
 def rel(a, b):
@@ -31,55 +36,68 @@ def rel(a, b):
 
 
 @pytest.fixture(scope="module")
-def steps():
+def runs():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from src.models.pretrain.VisionLanguageModule import VisionLanguageModule
-    B, H, T = 2, 512, 40
-    batch = synth_batch(B, H, T, 7)
-    out = {}
-    init = None
-    for dt in ("fp32", "bf16"):
-        torch.manual_seed(0)
-        m = VisionLanguageModule("resnet34", "tinybert", functools.partial(torch.optim.AdamW, lr=5e-5),
-                                 False, False, 512, 312, 128, compute_dtype=dt, text_dropout=0.0)
-        if init is None:
-            init = {k: v.clone() for k, v in m.state_dict().items()}
+    batch = synth_batch(B, H, T, 11)
+    m = VisionLanguageModule("resnet34", "tinybert", functools.partial(torch.optim.AdamW, lr=5e-5),
+                             False, False, 512, 312, 128, compute_dtype="bf16", text_dropout=0.0)
+    W.apply_recipe(m, 2)
+    o = OracleVLP(128, text_dropout=0.0)
+    W.apply_recipe(o, 2)
+    probe = batch["x-ray"][:32]
+    m.eval()
+    o.eval()
+    with torch.no_grad():
+        f_hip = m.image_encoder(probe.cuda()).float().cpu()
+        f_ora = o.image_encoder(probe)
+    m.train()
+    o.train()
+    loss, li, lt, ie, te = m.training_step_outputs(batch)
+    loss.backward()
+    torch.cuda.synchronize()
+    hip = {"loss": loss.item(), "ie": ie.float().cpu(), "te": te.float().cpu(),
+           "grads": {k: p.grad.float().cpu() for k, p in m.named_parameters() if p.grad is not None}}
+    del m
+    torch.cuda.empty_cache()
+    lg, oie, ote = o(batch)
+    lo = compute_loss(lg)[0]
+    lo.backward()
+    ora = {"loss": lo.item(), "ie": oie.detach(), "te": ote.detach(),
+           "grads": {k: p.grad for k, p in o.named_parameters() if p.grad is not None}}
+    return f_hip, f_ora, hip, ora
+
+
+def test_bf16_loss_features_embeddings_bs256(runs):
+    f_hip, f_ora, hip, ora = runs
+    d = abs(hip["loss"] - ora["loss"])
+    rf, ri, rt = rel(f_hip, f_ora), rel(hip["ie"], ora["ie"]), rel(hip["te"], ora["te"])
+    print(f"bs={B} {H}px T={T}: loss bf16 {hip['loss']:.6f} fp32 {ora['loss']:.6f} |d|={d:.2e}; "
+          f"probe features rel {rf:.2e}; img emb rel {ri:.2e}; txt emb rel {rt:.2e}")
+    assert d <= 5e-2
+    assert rf <= 2e-2 and ri <= 2e-2 and rt <= 2e-2
+
+
+def test_bf16_gradients_bs256(runs):
+    _, _, hip, ora = runs
+    gh, go = hip["grads"], ora["grads"]
+    conv, other = [], []
+    for k, g in go.items():
+        if k not in gh:
+            continue
+        r = rel(gh[k], g)
+        if k.startswith("image_encoder") and g.dim() == 4:
+            conv.append((r, k))
         else:
-            m.load_state_dict(init)
-        m.eval()
-        with torch.no_grad():
-            feat = m.image_encoder(batch["x-ray"].cuda()).float().cpu()
-        m.train()
-        loss = m.training_step(batch)
-        loss.backward()
-        torch.cuda.synchronize()
-        grads = {k: p.grad.detach().float().cpu() for k, p in m.named_parameters() if p.grad is not None}
-        out[dt] = (loss.item(), feat, grads)
-        del m
-        torch.cuda.empty_cache()
-    return out
-
-
-def test_loss_and_features_512(steps):
-    l32, f32, _ = steps["fp32"]
-    l16, f16, _ = steps["bf16"]
-    assert abs(l16 - l32) < 5e-2, (l16, l32)
-    assert rel(f16, f32) < 5e-2
-
-
-def test_image_tower_grads_512(steps):
-    _, _, g32 = steps["fp32"]
-    _, _, g16 = steps["bf16"]
-    bad = []
-    for k, g in g32.items():
-        if not (k.startswith("image_encoder") and k.endswith("weight")) or g.norm() < 1e-8:
-            continue
-        if "bn" in k or "downsample.1" in k:
-            continue
-        r = rel(g16[k], g)
-        if r > 0.35:
-            bad.append((k, r))
-    assert not bad, bad[:8]
+            other.append((r, k))
+    conv.sort(reverse=True)
+    other.sort(reverse=True)
+    print("worst conv weight grads:", [(k, round(r, 4)) for r, k in conv[:6]])
+    print("median conv rel:", statistics.median(r for r, _ in conv))
+    print("worst other grads:", [(k, round(r, 4)) for r, k in other[:8]])
+    assert len(conv) == 36
+    assert conv[0][0] <= 0.10, conv[:4]
+    assert statistics.median(r for r, _ in conv) <= 0.03
     for k in ("image_projection", "text_projection"):
-        assert rel(g16[k], g32[k]) < 0.35, k
+        assert rel(gh[k], go[k]) <= 0.05, k

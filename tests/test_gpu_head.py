@@ -1,0 +1,174 @@
+"""HIP contrastive head vs the reference's own outputs.
+
+The fixtures tests/golden/head_B*.pt and gathered_N2048.pt were produced by the
+reference's `forward` (src/models/pretrain/VisionLanguageModule.py:441-461) and
+`_compute_loss` (:532-554) in the build container (tests/golden/make_golden.py).
+Here the same inputs go through the product path of the training step:
+`_project_normalize` (HIP GEMM + L2 norm) -> `vlp_clip_loss_fused` (one kernel:
+global-batch InfoNCE forward + analytic backward) -> `_project_backward`.
+
+Cases: B = 4, 8, 8 with exp(logit_scale) = 150 > 100 (the clamp: d logit_scale
+must be exactly 0, :456-457), B = 256; and the 8-rank global batch (N = 2048)
+run as 8 launches with offset = r*256, N = 2048 -- exactly what every rank of an
+8-GPU job executes -- whose loss partials, gathered-embedding gradients
+(reduce-scatter = sum over ranks) and d logit_scale (all-reduce) are summed
+as the collectives would.
+
+Tolerances (fp32 on both sides; the reference keeps logit_scale in fp64, which
+promotes its logits and loss to fp64):
+  loss, image/text loss   |delta| <= 1e-5
+  embeddings, logits      rtol 1e-5, atol 1e-5
+  feature / projection / embedding gradients   rtol 1e-4, atol 1e-6 * max|golden|
+  d logit_scale           rel 1e-4 (exactly 0 when clamped)
+"""
+import os
+
+import pytest
+import torch
+
+from oracle import weights as W
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def load(name):
+    return torch.load(os.path.join(GOLD, name), weights_only=True)
+
+
+def head_inputs(B, seed):
+    """The features make_golden.head_case drew (same generator, same order)."""
+    g = torch.Generator().manual_seed(1000 + seed)
+    return torch.randn(B, 512, generator=g), torch.randn(B, 312, generator=g)
+
+
+def close(got, want, rtol, atol_rel, what):
+    got, want = got.detach().double().cpu(), want.detach().double().cpu()
+    atol = atol_rel * max(want.abs().max().item(), 1e-30)
+    err = (got - want).abs().max().item()
+    torch.testing.assert_close(got, want, rtol=rtol, atol=atol, msg=lambda m: f"{what}: {m}")
+    return err
+
+
+def make_head(logit_scale):
+    from vlp_amd.clip_model import ClipHead
+    dev = torch.device("cuda")
+    head = ClipHead(512, 312, 128, "fp32", device=dev)
+    with torch.no_grad():
+        head.arena.view("image_projection").copy_(W.value_for("image_projection", (512, 128)))
+        head.arena.view("text_projection").copy_(W.value_for("text_projection", (312, 128)))
+        head.arena.view("logit_scale").copy_(logit_scale.float())
+    return head
+
+
+def run_head(head, f_img, f_txt):
+    """The ClipStepFn head, world = 1: forward + fused loss + backward."""
+    from vlp_amd import ops
+    from vlp_amd.clip_model import _project_backward, _project_normalize
+    dev = torch.device("cuda")
+    fi, ft = f_img.to(dev).contiguous(), f_txt.to(dev).contiguous()
+    B, E = fi.shape[0], 128
+    wT = head.wcopy()
+    ie, inorm = _project_normalize(head, wT, fi, 512, 512, "image_projection", E)
+    te, tnorm = _project_normalize(head, wT, ft, 312, 312, "text_projection", E)
+    g_img = torch.zeros(B, E, device=dev)
+    g_txt = torch.zeros(B, E, device=dev)
+    small = torch.zeros(4, device=dev)
+    ops.clip_loss_fused(B, B, E, 0, ie, te, head.arena.view("logit_scale"), g_img, g_txt, small[2:3],
+                        small[0:2])
+    out = torch.empty(3, device=dev)
+    ops.clip_loss_finish(small[0:2], B, out)
+    gs = torch.ones(1, device=dev)
+    head.arena.grad.zero_()
+    ops.scale(small[2:3], gs, head.arena.gview("logit_scale"))
+    dfi = _project_backward(head, wT, fi, 512, 512, "image_projection", E, ie, inorm, g_img, gs)
+    dft = _project_backward(head, wT, ft, 312, 312, "text_projection", E, te, tnorm, g_txt, gs)
+    torch.cuda.synchronize()
+    return {"loss": out[0], "image_loss": out[1], "text_loss": out[2], "img_emb": ie, "txt_emb": te,
+            "d_f_img": dfi, "d_f_txt": dft, "d_logit_scale": head.arena.gview("logit_scale").clone(),
+            "d_image_projection": head.arena.gview("image_projection").clone(),
+            "d_text_projection": head.arena.gview("text_projection").clone()}
+
+
+@pytest.mark.parametrize("tag", ["head_B4_s0", "head_B8_s1", "head_B8_s2", "head_B256_s3"])
+def test_clip_loss_fused_vs_reference(tag):
+    from src.models.pretrain.VisionLanguageModule import _LogitsFn
+    gd = load(tag + ".pt")
+    B, seed = int(gd["B"]), int(gd["seed"])
+    f_img, f_txt = head_inputs(B, seed)
+    head = make_head(gd["logit_scale"])
+    r = run_head(head, f_img, f_txt)
+    for k in ("loss", "image_loss", "text_loss"):
+        d = abs(r[k].item() - gd[k].item())
+        assert d <= 1e-5, (k, r[k].item(), gd[k].item())
+    small = B <= 8
+    rows = slice(None) if small else slice(0, 16)
+    sfx = "" if small else "_rows16"
+    close(r["img_emb"][rows], gd["img_emb" + sfx], 1e-5, 1e-5, "img_emb")
+    close(r["txt_emb"][rows], gd["txt_emb" + sfx], 1e-5, 1e-5, "txt_emb")
+    # logits through the module's API path (HIP GEMM + scale, :456-459)
+    lg = _LogitsFn.apply(r["img_emb"], r["txt_emb"], head.arena.view("logit_scale"))
+    close(lg[rows], gd["logits" + sfx], 1e-5, 1e-5, "logits")
+    close(r["d_f_img"][rows], gd["d_f_img" + sfx], 1e-4, 1e-6, "d_f_img")
+    close(r["d_f_txt"][rows], gd["d_f_txt" + sfx], 1e-4, 1e-6, "d_f_txt")
+    close(r["d_image_projection"][:16], gd["d_image_projection_rows16"], 1e-4, 1e-6, "d_image_projection")
+    close(r["d_text_projection"][:16], gd["d_text_projection_rows16"], 1e-4, 1e-6, "d_text_projection")
+    for k in ("d_image_projection", "d_text_projection"):
+        n, ng = r[k].norm().item(), gd[k + "_norm"].item()
+        assert abs(n - ng) <= 1e-4 * ng, (k, n, ng)
+    if not small:
+        for k in ("d_f_img", "d_f_txt"):
+            n, ng = r[k].norm().item(), gd[k + "_norm"].item()
+            assert abs(n - ng) <= 1e-4 * ng, (k, n, ng)
+    dls, gls = r["d_logit_scale"].item(), gd["d_logit_scale"].item()
+    if gls == 0.0:   # clamped branch (exp(logit_scale) = 150 > 100): no gradient at all
+        assert "s2" in tag and dls == 0.0, dls
+    else:
+        assert abs(dls - gls) <= 1e-4 * abs(gls), (dls, gls)
+
+
+def test_clip_loss_fused_global_batch_8_ranks():
+    """The N = 2048 global batch of an 8-GPU job: each rank's launch covers its
+    256 rows (image->text) and 256 columns (text->image) at offset r*256."""
+    from vlp_amd import ops
+    gd = load("gathered_N2048.pt")
+    world, B, E, seed = int(gd["world"]), int(gd["B"]), int(gd["E"]), int(gd["seed"])
+    N = world * B
+    g = torch.Generator().manual_seed(seed)
+    ie = torch.nn.functional.normalize(torch.randn(N, E, generator=g)).cuda()
+    te = torch.nn.functional.normalize(torch.randn(N, E, generator=g)).cuda()
+    ls = torch.tensor([W.value_for("logit_scale", (1,)).item()], device="cuda")
+    parts = torch.zeros(2, dtype=torch.float64, device="cuda")
+    dls = torch.zeros(1, dtype=torch.float64, device="cuda")
+    g_img = torch.zeros(N, E, dtype=torch.float64, device="cuda")
+    g_txt = torch.zeros(N, E, dtype=torch.float64, device="cuda")
+    for r in range(world):
+        gi = torch.zeros(N, E, device="cuda")
+        gt = torch.zeros(N, E, device="cuda")
+        small = torch.zeros(4, device="cuda")
+        ops.clip_loss_fused(B, N, E, r * B, ie, te, ls, gi, gt, small[2:3], small[0:2])
+        # the collectives of ClipStepFn: all-reduce of the loss partials and of the
+        # head gradient (d logit_scale), reduce-scatter (= sum) of the gathered grads
+        parts += small[0:2].double()
+        dls += small[2:3].double()
+        g_img += gi.double()
+        g_txt += gt.double()
+    torch.cuda.synchronize()
+    loss = (parts[0] + parts[1]).item() / (2 * N)
+    li, lt = parts[0].item() / N, parts[1].item() / N
+    assert abs(loss - gd["loss"].item()) <= 1e-5, (loss, gd["loss"].item())
+    assert abs(li - gd["image_loss"].item()) <= 1e-5, (li, gd["image_loss"].item())
+    assert abs(lt - gd["text_loss"].item()) <= 1e-5, (lt, gd["text_loss"].item())
+    gls = gd["d_logit_scale"].item()
+    assert abs(dls.item() - gls) <= 1e-4 * abs(gls), (dls.item(), gls)
+    close(g_img[:8], gd["d_img_rows_0_8"], 1e-4, 1e-6, "d_img rows 0-8")
+    close(g_txt[:8], gd["d_txt_rows_0_8"], 1e-4, 1e-6, "d_txt rows 0-8")
+    for k, t in (("d_img_norm", g_img), ("d_txt_norm", g_txt)):
+        n, ng = t.norm().item(), gd[k].item()
+        assert abs(n - ng) <= 1e-5 * ng, (k, n, ng)

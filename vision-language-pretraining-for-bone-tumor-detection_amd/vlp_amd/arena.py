@@ -87,10 +87,31 @@ class ArenaModule(nn.Module):
     def device(self):
         return self.arena.data.device
 
+    def _aliased(self, p, full):
+        return p.grad is not None and p.grad.data_ptr() == self.arena.gview(full).data_ptr()
+
+    def begin_backward(self):
+        """Call before a backward overwrites the grad arena.  After the first
+        backward, p.grad IS a view of the arena (AccumulateGrad stole it); the
+        backward then overwrites those values with the new gradient, and
+        AccumulateGrad will add what grads_for_autograd returns to them.  So
+        the values p.grad held before this backward (zeros after
+        zero_grad(set_to_none=False), a running sum under gradient
+        accumulation) are kept here and handed back instead of the gradient."""
+        self._prior = None
+        for owner, attr, full in self._param_slots:
+            if self._aliased(owner._parameters[attr], full):
+                self._prior = self.arena.grad.clone()
+                return
+
     def grads_for_autograd(self, existing=None):
         """Per-parameter gradient tensors to hand back from an autograd
-        Function: views of the grad arena (stolen by AccumulateGrad, so p.grad
-        aliases the arena); clones when gradients are being accumulated."""
+        Function, such that p.grad ends up = (its value before the backward)
+        + (the new gradient written into the arena):
+          p.grad None             -> the arena view (AccumulateGrad steals it)
+          p.grad aliases the arena -> the pre-backward values (begin_backward)
+          p.grad elsewhere        -> a copy of the new gradient."""
+        prior = getattr(self, "_prior", None)
         out = []
         for owner, attr, full in self._param_slots:
             p = owner._parameters[attr]
@@ -98,5 +119,13 @@ class ArenaModule(nn.Module):
                 out.append(None)
                 continue
             g = self.arena.gview(full)
-            out.append(g.clone() if p.grad is not None else g)
+            if p.grad is None:
+                out.append(g)
+            elif self._aliased(p, full):
+                if prior is None:
+                    raise RuntimeError("ArenaModule: begin_backward() was not called before this backward")
+                out.append(self.arena.view(full, prior))
+            else:
+                out.append(g.clone())
+        self._prior = None
         return out

@@ -162,6 +162,8 @@ class ClipStepFn(torch.autograd.Function):
         (sv_img, sv_txt, wT, feat_img, h_last, ie, inorm, te, tnorm, g_img_all, g_txt_all, small,
          B, Tn, D, E) = ctx.state
         ctx.state = None
+        for t in (head, img_t, txt_t):
+            t.begin_backward()
         g_img = vdist.reduce_scatter_rows(g_img_all)
         g_txt = vdist.reduce_scatter_rows(g_txt_all)
         gs = dloss.reshape(1).float().contiguous()
@@ -172,11 +174,16 @@ class ClipStepFn(torch.autograd.Function):
         dcls = _project_backward(head, wT, h_last, D, D, "text_projection", E, te, tnorm,
                                  g_txt, gs)
         # data parallel: SUM all-reduce of the flat gradient arenas, the head and
-        # text tower's launched while the (much longer) image backward runs.
+        # text tower's launched while the (much longer) image backward runs, the
+        # image tower's per stage (layer4 first) as the backward leaves each stage.
         # With the text stream the text backward and its collective also run
         # beside the image backward; every tensor crossing streams stays
         # referenced until the join below.
         reducer = vdist.GradReducer()
+        on_stage = None
+        if vdist.world()[1] > 1:
+            def on_stage(off, n):
+                reducer.reduce_span(img_t.arena, off, n)
         s_txt = _text_stream(dcls.device)
         if s_txt is not None:
             main = torch.cuda.current_stream(dcls.device)
@@ -185,14 +192,12 @@ class ClipStepFn(torch.autograd.Function):
                 txt_t.run_backward(sv_txt, dcls)
                 reducer.reduce([txt_t.arena])
             reducer.reduce([head.arena])
-            img_t.run_backward(sv_img, dfeat_img)
-            reducer.reduce([img_t.arena])
+            img_t.run_backward(sv_img, dfeat_img, on_stage_done=on_stage)
             main.wait_stream(s_txt)
         else:
             txt_t.run_backward(sv_txt, dcls)
             reducer.reduce([head.arena, txt_t.arena])
-            img_t.run_backward(sv_img, dfeat_img)
-            reducer.reduce([img_t.arena])
+            img_t.run_backward(sv_img, dfeat_img, on_stage_done=on_stage)
         reducer.wait()
         grads = (head.grads_for_autograd() + img_t.grads_for_autograd() + txt_t.grads_for_autograd())
         return (None, None, None, None, None, None, *grads)

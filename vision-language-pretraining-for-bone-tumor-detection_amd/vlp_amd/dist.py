@@ -7,8 +7,14 @@ Two exchanges per step:
      the gathered embeddings returns to the owners by reduce-scatter.
   2. SUM all-reduce of the flat per-tower gradient arenas (the global loss is
      a sum over ranks' row/column terms, so summed local gradients equal
-     d L_global / d theta).  BatchNorm statistics stay per rank, as the
+     d L_global / d theta), in buckets launched while the backward is still
+     running (GradReducer).  BatchNorm statistics stay per rank, as the
      reference's per-device BN (no SyncBN).
+
+With the gloo backend (CPU tests, and the world-size-2 test of the real HIP
+step that runs two ranks on one GPU) device tensors are staged through host
+memory, since gloo has no reduce-scatter and no device transport: the
+collectives are then synchronous and the result is copied back in place.
 """
 from __future__ import annotations
 
@@ -22,10 +28,26 @@ def world():
     return 0, 1
 
 
+def _staged(t: torch.Tensor) -> bool:
+    """gloo: no reduce-scatter, no device transport -> go through host memory."""
+    return dist.get_backend() == "gloo"
+
+
+class _Done:
+    """Work handle of a collective that already completed (host-staged)."""
+
+    def wait(self):
+        return True
+
+
 def all_gather_rows(x: torch.Tensor) -> torch.Tensor:
     r, w = world()
     if w == 1:
         return x
+    if _staged(x):
+        parts = [torch.empty_like(x, device="cpu") for _ in range(w)]
+        dist.all_gather(parts, x.detach().cpu().contiguous())
+        return torch.cat(parts).to(x.device)
     out = torch.empty((w * x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     dist.all_gather_into_tensor(out, x.contiguous())
     return out
@@ -36,6 +58,10 @@ def reduce_scatter_rows(x_all: torch.Tensor) -> torch.Tensor:
     if w == 1:
         return x_all
     rows = x_all.shape[0] // w
+    if _staged(x_all):
+        h = x_all.detach().to("cpu", copy=True).contiguous()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM)
+        return h[r * rows:(r + 1) * rows].to(x_all.device).contiguous()
     out = torch.empty((rows,) + tuple(x_all.shape[1:]), dtype=x_all.dtype, device=x_all.device)
     dist.reduce_scatter_tensor(out, x_all.contiguous(), op=dist.ReduceOp.SUM)
     return out
@@ -45,23 +71,39 @@ def all_reduce_sum_(t: torch.Tensor, async_op: bool = False):
     r, w = world()
     if w == 1:
         return None
+    if _staged(t) and t.is_cuda:
+        h = t.detach().cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM)
+        t.copy_(h)
+        return _Done() if async_op else None
     return dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=async_op)
 
 
 class GradReducer:
-    """SUM all-reduce of flat gradient arenas.  `reduce(arenas)` launches one
-    collective per arena (async), `wait()` joins them.  Arenas are large
-    contiguous fp32 buffers (the image tower's is 85 MB), which is the bucket
-    size xGMI ring/direct algorithms want."""
+    """SUM all-reduce of flat gradient buffers, launched asynchronously as soon
+    as each bucket is final and joined once at the end of the backward.
+
+    `reduce(arenas)` launches one collective per arena (the head and text
+    arenas: 0.1 / 57 MB); `reduce_span(arena, off, n)` one collective over a
+    contiguous slice of an arena -- the image tower hands over its stages
+    (layer4 -> stem, 52 / 27 / 4.5 / 0.9 MB) the moment their last weight
+    gradient is folded, so all but the stem bucket overlap the rest of the
+    backward (an RCCL collective runs on its own stream after the kernels
+    already queued on the current one).  `wait()` joins them."""
 
     def __init__(self):
         self._work = []
 
     def reduce(self, arenas):
         for a in arenas:
-            w = all_reduce_sum_(a.grad, async_op=True)
-            if w is not None:
-                self._work.append(w)
+            self.reduce_span(a, 0, a.grad.numel())
+
+    def reduce_span(self, arena, off, n):
+        if n <= 0:
+            return
+        w = all_reduce_sum_(arena.grad[off:off + n], async_op=True)
+        if w is not None:
+            self._work.append(w)
 
     def wait(self):
         for w in self._work:

@@ -49,6 +49,13 @@ _WG_STREAMS = {}   # measured: the extra transposed write costs more than it sav
 STAT_REP = 64   # replicas of per-channel fp64 sums (see vlp_stat_reduce)
 
 
+STAGES = ("stem", "layer1", "layer2", "layer3", "layer4")
+
+
+def _stage_of(key: str) -> str:
+    return key.split(".", 1)[0] if key.startswith("layer") else "stem"
+
+
 class _Holder(nn.Module):
     """Parameter/buffer container mirroring one timm submodule (no forward)."""
 
@@ -93,13 +100,22 @@ class ResNet34Tower(ArenaModule):
         self.compute_dtype = compute_dtype
         convs, bns = _tower_specs()
         self._convs = {c.key: c for c in convs}
+        # arena order (internal; the state dict keeps timm's order): one contiguous
+        # range per stage, stem first, so each stage's gradients form one bucket of
+        # the data-parallel all-reduce, launched as soon as the backward leaves it
         specs = []
-        for c in convs:
-            specs.append((c.key + ".weight", (c.Co, c.C, c.KH, c.KW)))
-        for key, C in bns:
-            specs.append((key + ".weight", (C,)))
-            specs.append((key + ".bias", (C,)))
-        # arena order = timm order would interleave; keep convs then BN (order is internal)
+        self._stage_names = {}
+        for st in STAGES:
+            names = []
+            for c in convs:
+                if _stage_of(c.key) == st:
+                    specs.append((c.key + ".weight", (c.Co, c.C, c.KH, c.KW)))
+                    names.append(c.key + ".weight")
+            for key, C in bns:
+                if _stage_of(key) == st:
+                    specs += [(key + ".weight", (C,)), (key + ".bias", (C,))]
+                    names += [key + ".weight", key + ".bias"]
+            self._stage_names[st] = names
         self._init_arena(specs, device=device)
         # module tree with timm names (registration order = timm state_dict order)
         self._bns = {}
@@ -321,9 +337,17 @@ class ResNet34Tower(ArenaModule):
         return feat, saved
 
     # ---------------- backward ----------------
-    def run_backward(self, saved, dfeat: torch.Tensor):
+    def stage_span(self, stage):
+        """(offset, length) of one stage's parameters in the arena."""
+        return self.arena.span(self._stage_names[stage])
+
+    def run_backward(self, saved, dfeat: torch.Tensor, on_stage_done=None):
         """dfeat: [N,512] fp32 gradient of the pooled features.  Writes every
-        parameter gradient into the grad arena (overwriting)."""
+        parameter gradient into the grad arena (overwriting).  on_stage_done(off,
+        n) is called (in backward order: layer4, layer3, layer2, layer1 + stem)
+        once the arena range [off, off+n) holds its final gradients, with every
+        kernel writing it already queued on the current stream -- the data-
+        parallel all-reduce of that bucket is launched there."""
         ws = self._workspace()
         T = self.tdtype
         dev = self.arena.data.device
@@ -333,13 +357,23 @@ class ResNet34Tower(ArenaModule):
             if self._sw is None:
                 self._sw = _WG_STREAMS[dev] = torch.cuda.Stream(device=dev)
         try:
-            self._run_backward(saved, dfeat, ws, T, dev)
+            self._run_backward(saved, dfeat, ws, T, dev, on_stage_done)
         finally:
             if self._sw is not None:   # join: every weight gradient is in the arena
                 torch.cuda.current_stream(dev).wait_stream(self._sw)
             self._sw = None
 
-    def _run_backward(self, saved, dfeat, ws, T, dev):
+    def _stage_done(self, stages, cb, dev):
+        if cb is None:
+            return
+        if self._sw is not None:   # weight gradients queued on the side stream
+            torch.cuda.current_stream(dev).wait_stream(self._sw)
+        spans = [self.stage_span(s) for s in stages]
+        lo = min(o for o, _ in spans)
+        hi = max(o + n for o, n in spans)
+        cb(lo, hi - lo)
+
+    def _run_backward(self, saved, dfeat, ws, T, dev, on_stage_done=None):
         ws["bstat"].zero_()
         dfeat = dfeat.float().contiguous()
         blocks = saved["blocks"]
@@ -437,6 +471,11 @@ class ResNet34Tower(ArenaModule):
                 dout_masked = False
             self._wgrad(ws, c1, dy1, x, dyT=tA)
             dout = dx
+            stage = pre.split(".", 1)[0]
+            if pre.endswith(".0") and stage != "layer1":
+                # first block of a stage: every gradient of that stage is final
+                # (its bn2 sums came from the block above, already folded)
+                self._stage_done([stage], on_stage_done, dev)
         # stem: maxpool -> relu -> bn1 -> conv1
         y0, idx = saved["y0"], saved["idx"]
         sc0, sh0, mu0, is0 = self._coef(ws, "bn1")
@@ -448,6 +487,7 @@ class ResNet34Tower(ArenaModule):
         dy0 = torch.empty_like(y0)
         ops.maxpool_bwd_apply(dout, idx, y0, sc0, sh0, mu0, is0, self.arena.view("bn1.weight"), sg0, sgx0, dy0)
         ops.stem_wgrad_into(dy0, saved["xp"], saved["N"], saved["H"], saved["W"], self.arena.gview("conv1.weight"))
+        self._stage_done(["layer1", "stem"], on_stage_done, dev)
 
     def _tbuf(self, ws, name, C, M):
         """[C][M] bf16 scratch for a transposed output gradient (the weight-gradient
@@ -504,6 +544,7 @@ class ImageTowerFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dfeat):
         tower = ctx.tower
+        tower.begin_backward()
         tower.run_backward(ctx.saved, dfeat)
         ctx.saved = None
         return (None, None, *tower.grads_for_autograd())

@@ -441,6 +441,7 @@ class TextTowerFn(torch.autograd.Function):
         dcls_rows = dh[:, 0, :].contiguous()
         if dh[:, 1:, :].abs().sum().item() != 0:  # pragma: no cover - generic last_hidden_state use
             raise NotImplementedError("TinyBertTower backward supports gradients on the CLS token only")
+        tower.begin_backward()
         tower.run_backward(ctx.sv, dcls_rows)
         ctx.sv = None
         return (None, None, None, None, *tower.grads_for_autograd())
