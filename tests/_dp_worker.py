@@ -31,9 +31,13 @@ def main():
     from src.models.pretrain.VisionLanguageModule import VisionLanguageModule
 
     torch.cuda.set_device(0)
+    torch.manual_seed(0)   # the module's own init, identical on both ranks
     m = VisionLanguageModule("resnet34", "tinybert", functools.partial(torch.optim.AdamW, lr=5e-5),
                              False, False, 512, 312, 128, compute_dtype="fp32", text_dropout=0.0)
-    W.apply_recipe(m, 1)
+    if os.environ.get("DP_INIT", "module") == "recipe":
+        W.apply_recipe(m, 1)
+    if rank == 0:
+        torch.save({k: v.detach().cpu() for k, v in m.state_dict().items()}, os.path.join(outdir, "init.pt"))
     m.train()
     full = synth_batch(world * B, H, T, seed)
     sl = slice(rank * B, (rank + 1) * B)

@@ -14,9 +14,16 @@ The definition it must equal: the oracle's image tower run per 4-row shard
 (train-mode BN statistics per rank, as the reference's per-device BN), the
 features concatenated, the text tower on all 8 captions, and the reference
 _compute_loss on the 8 x 8 logits; gradients of that global loss.
+Weights: the module's own initialisation (timm / HF init, what a training run
+starts from), whose fp32 gradients are well conditioned (HIP fp32 vs the
+oracle ~3e-6 single-GPU), so every non-zero gradient -- stem, downsample convs,
+every BN parameter, projections, logit scale, the whole text tower -- is held to
+the strict fp32 envelope.  (The recipe weights of the other parity tests make
+this small-batch BN stack sensitive to single ReLU flips; see
+test_gpu_model.grad_envelope_check.)
 Tolerances: loss |delta| <= 1e-5 vs the fp64 oracle; every gradient inside
-the fp32 envelope of test_gpu_model.test_grads_vs_oracle_fp32; both ranks
-hold bit-identical gradients after the all-reduce.
+the strict fp32 envelope; both ranks hold bit-identical gradients after the
+all-reduce.
 """
 import os
 import socket
@@ -26,7 +33,6 @@ import sys
 import pytest
 import torch
 
-from oracle import weights as W
 from oracle.clip import OracleVLP, compute_loss, clip_forward
 from tests.conftest import ROOT
 from tests.golden.synth import synth_batch
@@ -59,12 +65,14 @@ def ranks(tmp_path_factory):
     env = dict(os.environ, OMP_NUM_THREADS="4")
     r = subprocess.run(cmd, env=env, timeout=300, capture_output=True, text=True)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    return [torch.load(out / f"r{k}.pt", weights_only=True) for k in range(2)]
+    res = [torch.load(out / f"r{k}.pt", weights_only=True) for k in range(2)]
+    res[0]["init"] = torch.load(out / "init.pt", weights_only=True)
+    return res
 
 
-def _oracle(dt):
+def _oracle(dt, sd):
     o = OracleVLP(128, text_dropout=0.0)
-    W.apply_recipe(o, 1)
+    o.load_state_dict(sd)
     o = o.to(dt)
     o.train()
     full = synth_batch(2 * B, H, T, SEED)
@@ -78,7 +86,7 @@ def _oracle(dt):
 
 
 def test_dp2_loss_is_global_batch_loss(ranks):
-    _, l64, li64, lt64 = _oracle(torch.float64)
+    _, l64, li64, lt64 = _oracle(torch.float64, ranks[0]["init"])
     for r in ranks:
         assert abs(r["loss"] - l64) <= 1e-5, (r["loss"], l64)
         assert abs(r["image_loss"] - li64) <= 1e-5
@@ -90,16 +98,10 @@ def test_dp2_gradients_are_global_gradients(ranks):
     assert g0.keys() == g1.keys()
     for k in g0:
         assert torch.equal(g0[k], g1[k]), f"ranks disagree after the all-reduce: {k}"
-    o32, _, _, _ = _oracle(torch.float32)
-    o64, _, _, _ = _oracle(torch.float64)
-    p32, p64 = dict(o32.named_parameters()), dict(o64.named_parameters())
-    bad, checked = [], 0
-    for k, g in g0.items():
-        r64 = p64[k].grad
-        assert r64 is not None, k
-        e_hip, e_ref = rel(g, r64), rel(p32[k].grad, r64)
-        checked += 1
-        if e_hip > max(4 * e_ref, 2e-3) and (g.double() - r64).norm().item() > 1e-6:
-            bad.append((k, e_hip, e_ref))
-    assert checked > 100
-    assert not bad, bad[:10]
+    from tests.test_gpu_model import grad_envelope_check
+    o32, _, _, _ = _oracle(torch.float32, ranks[0]["init"])
+    o64, _, _, _ = _oracle(torch.float64, ranks[0]["init"])
+    assert len(g0) > 100
+    p64 = dict(o64.named_parameters())
+    named = [(k, g0.get(k)) for k in p64 if p64[k].grad is not None or k in g0]
+    grad_envelope_check(named, o32, o64, strict=True)

@@ -109,17 +109,52 @@ def _oracle_step(batch, seed, dt):
     return o, lo
 
 
+def grad_envelope_check(named_grads, o32, o64, strict):
+    """Every parameter gradient vs the fp64 oracle, judged against the oracle's own
+    fp32 error e_ref (err(HIP, fp64) <= 4 * e_ref, floor 2e-3 / 1e-6 absolute).
+
+    strict=False (large shapes, recipe weights): a ReLU whose pre-activation lies
+    within fp32 rounding of zero can take the other branch in HIP than in the
+    oracle -- one such flip among ~1e5 activations moves the gradients of the
+    layers below it by ~1e-3..1e-2 rel-L2, in either implementation (the fp32
+    oracle itself sits 0.7 % from fp64 on these weights at 128 px, B = 8;
+    tools/diag_blocks.py traces each such step to an exact upstream gradient and
+    an op that matches torch to 2e-5 at that shape).  So per tensor the floor is
+    2e-2, and the whole image-tower gradient (all 36 conv weights as one vector)
+    must stay within max(2 x the fp32 oracle's own error, 5e-3) of fp64."""
+    p32, p64 = dict(o32.named_parameters()), dict(o64.named_parameters())
+    bad, hip_v, ref_v, o32_v = [], [], [], []
+    floor = 2e-3 if strict else 2e-2
+    for k, g in named_grads:
+        g64 = p64[k].grad
+        if g64 is None:
+            assert g is None, k
+            continue
+        e_hip, e_ref = rel(g, g64), rel(p32[k].grad, g64)
+        if e_hip > max(4 * e_ref, floor) and (g.double().cpu() - g64).norm().item() > 1e-6:
+            bad.append((k, e_hip, e_ref))
+        if k.startswith("image_encoder") and g64.dim() == 4:
+            hip_v.append(g.double().cpu().flatten())
+            ref_v.append(g64.double().flatten())
+            o32_v.append(p32[k].grad.double().flatten())
+    tower = rel(torch.cat(hip_v), torch.cat(ref_v))
+    tower32 = rel(torch.cat(o32_v), torch.cat(ref_v))
+    print(f"whole image-tower conv gradient rel-L2 vs fp64: hip {tower:.3e}, fp32 oracle {tower32:.3e}; "
+          f"tensors over the envelope: {bad[:6]}")
+    assert not bad, bad[:10]
+    assert strict or tower <= max(2 * tower32, 5e-3), (tower, tower32)
+
+
 @pytest.mark.parametrize("B,H,T", [(6, 96, 16), (2, 512, 40), (4, 224, 40)],
                          ids=["96px_T16", "bench_512px_T40", "ref_default_224px_T40"])
 def test_grads_vs_oracle_fp32(B, H, T):
-    """Every parameter gradient, judged against the fp32 rounding envelope:
-    err(HIP, oracle-fp64) <= 4 * err(oracle-fp32, oracle-fp64) (or <= 2e-3 /
-    1e-6 absolute, whichever is looser); loss within 1e-5 of the fp64 oracle
-    (north-star gate 1e-3); eval-mode probe features within rel-L2 1e-4.
-    Shapes: 96x96 / T=16; the benchmark resolution and caption length (512x512,
-    T=40: the W=128 layer-1 rows kernel and the full-size stem run); the
-    reference's own training resolution (224x224, PretrainDataModule.py:155;
-    layer 1 is 56 wide there and takes the generic tile path)."""
+    """Parity mode vs the oracle: loss within 1e-5 of the fp64 oracle (north-star
+    gate 1e-3), eval-mode probe features within rel-L2 1e-4, every gradient in
+    the fp32 envelope (grad_envelope_check; strict at 96 px).  Shapes: 96x96 /
+    T=16; the benchmark resolution and caption length (512x512, T=40: the W=128
+    layer-1 rows kernel and the full-size stem run); the reference's own training
+    resolution (224x224, PretrainDataModule.py:155; layer 1 is 56 wide there and
+    takes the generic tile path)."""
     batch = synth_batch(B, H, T, 3)
     m = make_model("fp32", seed=1)
     o32p = make_oracle(1)
@@ -137,17 +172,7 @@ def test_grads_vs_oracle_fp32(B, H, T):
     o64, l64 = _oracle_step(batch, 1, torch.float64)
     print(f"[{H}px T={T}] loss hip {loss.item():.8f} fp64 {l64.item():.8f} fp32 {l32.item():.8f}")
     assert abs(loss.item() - l64.item()) < 1e-5
-    p32, p64 = dict(o32.named_parameters()), dict(o64.named_parameters())
-    bad = []
-    for k, p in m.named_parameters():
-        g64 = p64[k].grad
-        if g64 is None:
-            assert p.grad is None, k
-            continue
-        e_hip, e_ref = rel(p.grad, g64), rel(p32[k].grad, g64)
-        if e_hip > max(4 * e_ref, 2e-3) and (p.grad.double().cpu() - g64).norm().item() > 1e-6:
-            bad.append((k, e_hip, e_ref))
-    assert not bad, bad[:10]
+    grad_envelope_check([(k, p.grad) for k, p in m.named_parameters()], o32, o64, strict=H <= 96)
     o = o32
     # running statistics after one train-mode forward
     sd, osd = m.state_dict(), o.state_dict()
@@ -204,9 +229,11 @@ def test_gradient_accumulation_semantics(api):
     g3 = backward()   # no zero_grad: accumulates
     assert g1.keys() == g2.keys() == g3.keys() and len(g1) > 100
     for k in g1:
-        scale = g1[k].abs().max().item() + 1e-30
-        torch.testing.assert_close(g2[k], g1[k], rtol=1e-5, atol=1e-6 * scale, msg=lambda s: f"{k}: {s}")
-        torch.testing.assert_close(g3[k], 2 * g1[k], rtol=1e-5, atol=2e-6 * scale, msg=lambda s: f"{k}: {s}")
+        # attention key biases have an exactly-zero gradient (softmax shift invariance):
+        # both runs are rounding noise there (~1e-10), hence the absolute floor
+        atol = max(1e-6 * g1[k].abs().max().item(), 1e-8)
+        torch.testing.assert_close(g2[k], g1[k], rtol=1e-5, atol=atol, msg=lambda s: f"{k}: {s}")
+        torch.testing.assert_close(g3[k], 2 * g1[k], rtol=1e-5, atol=2 * atol, msg=lambda s: f"{k}: {s}")
 
 
 def test_uint8_collation_path_matches_float():
@@ -222,3 +249,55 @@ def test_uint8_collation_path_matches_float():
         b2["x-ray-u8"] = batch["x-ray-u8"]
         l2 = m.training_step_outputs(b2)[0].item()
     assert abs(l1 - l2) < 1e-5
+
+
+def test_fused_adamw_matches_torch_and_state_dict_roundtrip():
+    """FusedAdamW (one vlp_adamw launch per arena span) follows torch.optim.AdamW
+    over three steps on the reference's parameter groups; its state_dict holds
+    torch's per-parameter {step, exp_avg, exp_avg_sq} and round-trips: a fresh
+    optimizer resumed from it (or from a torch AdamW state dict) takes the same
+    next step."""
+    from src.models.pretrain.VisionLanguageModule import VisionLanguageModule
+    from vlp_amd.optim import FusedAdamW
+    B, H, T = 4, 64, 12
+    batch = synth_batch(B, H, T, 0)
+
+    def model(fused):
+        m = VisionLanguageModule("resnet34", "tinybert", functools.partial(torch.optim.AdamW, lr=1e-3),
+                                 False, False, 512, 312, 128, compute_dtype="fp32", text_dropout=0.0,
+                                 fused_optimizer=fused)
+        W.apply_recipe(m, 0)
+        m.train()
+        return m, m.configure_optimizers()["optimizer"]
+
+    def step(m, opt):
+        opt.zero_grad()
+        m.training_step(batch).backward()
+        opt.step()
+        torch.cuda.synchronize()
+
+    def flat(m):
+        return torch.cat([p.detach().double().flatten().cpu() for p in m.parameters()])
+
+    mf, of = model(True)
+    mt, ot = model(False)
+    assert isinstance(of, FusedAdamW) and type(ot) is torch.optim.AdamW
+    p0 = flat(mf)
+    for _ in range(3):
+        step(mf, of)
+        step(mt, ot)
+    d_f, d_t = flat(mf) - p0, flat(mt) - p0
+    assert rel(d_f, d_t) < 1e-3, rel(d_f, d_t)
+    sd = of.state_dict()
+    st = next(iter(sd["state"].values()))
+    assert set(st) == {"step", "exp_avg", "exp_avg_sq"} and float(st["step"]) == 3.0
+    for src_sd, src_model in ((sd, mf), (ot.state_dict(), mt)):
+        m2, o2 = model(True)
+        m2.load_state_dict(src_model.state_dict())
+        o2.load_state_dict(src_sd)
+        ref = [p.detach().clone() for p in src_model.parameters()]
+        m_next, o_next = (mf, of) if src_model is mf else (mt, ot)
+        step(m_next, o_next)
+        step(m2, o2)
+        assert rel(flat(m2) - torch.cat([r.double().flatten().cpu() for r in ref]),
+                   flat(m_next) - torch.cat([r.double().flatten().cpu() for r in ref])) < 1e-3

@@ -55,6 +55,8 @@ CONV_CASES = [
     (3, 7, 9, 128, 64, 3, 3, 1, 1),
     (3, 5, 128, 64, 64, 3, 3, 1, 1),    # layer-1 width: row-streaming kernel (bf16)
     (2, 12, 12, 256, 256, 3, 3, 1, 1),  # M, N >= 256: 256x256 large-tile kernel (bf16)
+    (4, 7, 7, 512, 512, 3, 3, 1, 1),    # layer 4 at 224 px, B = 4
+    (4, 14, 14, 256, 512, 3, 3, 2, 1),  # layer-4 stride-2 block at 224 px
 ]
 
 
@@ -169,9 +171,9 @@ def test_conv_wgrad_split_slabs(ops, case, ws_floats):
 
 
 @pytest.mark.parametrize("dt", DT)
-@pytest.mark.parametrize("H,W", [(10, 10), (4, 128)])
-def test_conv_dgrad_bn_epilogue(ops, dt, H, W):
-    N, C, Co, KH, KW, S, P = 2, 64, 64, 3, 3, 1, 1
+@pytest.mark.parametrize("N,H,W,C", [(2, 10, 10, 64), (2, 4, 128, 64), (4, 7, 7, 512), (2, 14, 14, 256)])
+def test_conv_dgrad_bn_epilogue(ops, dt, N, H, W, C):
+    Co, KH, KW, S, P = C, 3, 3, 1, 1
     torch.manual_seed(3)
     dy = torch.randn(N, Co, H, W).to(dt).float()
     w = (torch.randn(Co, C, KH, KW) * 0.05).to(dt).float()
@@ -197,7 +199,8 @@ def test_conv_dgrad_bn_epilogue(ops, dt, H, W):
 
 
 @pytest.mark.parametrize("dt", DT)
-@pytest.mark.parametrize("case", [(2, 10, 10, 64, 64, 1), (2, 4, 128, 64, 64, 1), (2, 12, 12, 64, 128, 2)])
+@pytest.mark.parametrize("case", [(2, 10, 10, 64, 64, 1), (2, 4, 128, 64, 64, 1), (2, 12, 12, 64, 128, 2),
+                                  (4, 7, 7, 512, 512, 1), (4, 14, 14, 256, 512, 2)])
 @pytest.mark.parametrize("with_add", [False, True])
 @pytest.mark.parametrize("bits", [False, True])
 def test_conv_dgrad_relu_epilogue(ops, dt, case, with_add, bits):

@@ -18,7 +18,7 @@ from __future__ import annotations
 from typing import List, Optional
 
 import torch
-from torch.utils.data import DataLoader, Dataset
+from torch.utils.data import DataLoader, Dataset, Subset
 
 from src.data.PretrainDataModule import normalize_u8
 
@@ -101,9 +101,20 @@ class DownstreamDataModule:
             image_size, n_samples, n_val_samples, n_folds, seed)
         self.collate = ClinicalCollator(upload if num_channels == 3 else "fp32", num_channels)
 
+    @staticmethod
+    def _shard(ds):
+        """Data parallel: each rank reads its own interleaved shard of the dataset
+        (DistributedSampler's split, which Lightning's DDP inserts for the
+        reference); the label weights stay those of the whole training set."""
+        d = torch.distributed
+        if not (d.is_available() and d.is_initialized()) or d.get_world_size() == 1:
+            return ds
+        return Subset(ds, list(range(d.get_rank(), len(ds), d.get_world_size())))
+
     def _loader(self, ds, shuffle):
-        return DataLoader(ds, batch_size=self.batch_size, shuffle=shuffle, num_workers=self.num_workers,
-                          collate_fn=self.collate, pin_memory=torch.cuda.is_available())
+        return DataLoader(self._shard(ds), batch_size=self.batch_size, shuffle=shuffle,
+                          num_workers=self.num_workers, collate_fn=self.collate,
+                          pin_memory=torch.cuda.is_available())
 
     def get_cv_splits(self):
         for i in range(self.n_folds):

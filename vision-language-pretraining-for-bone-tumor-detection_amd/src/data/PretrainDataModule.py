@@ -46,9 +46,10 @@ MAX_TOKENS = 40                    # tokenizer max_length (:213)
 _SITES = ("ELBOW", "FINGER", "FOREARM", "HAND", "HUMERUS", "SHOULDER", "WRIST", "FOOT", "KNEE", "HIP")
 
 
-def normalize_u8(x_u8: torch.Tensor, num_channels: int = 3) -> torch.Tensor:
-    """uint8 [B,1,H,W] -> fp32 [B,C,H,W]: (x - 127.5) / 73.9, channel replicated (:165-171)."""
-    x = (x_u8.float() - IMG_MEAN) / IMG_STD
+def normalize_u8(x_u8: torch.Tensor, num_channels: int = 3, mean: float = IMG_MEAN,
+                 std: float = IMG_STD) -> torch.Tensor:
+    """uint8 [B,1,H,W] -> fp32 [B,C,H,W]: (x - mean) / std, channel replicated (:165-171)."""
+    x = (x_u8.float() - mean) / std
     return x.repeat(1, num_channels, 1, 1).contiguous() if num_channels != 1 else x.contiguous()
 
 
@@ -91,12 +92,18 @@ class SyntheticRadiographCaptions(Dataset):
 
 
 class PairCollator:
-    """Per-sample dicts -> the batch dict VisionLanguageModule consumes (default_collate layout)."""
+    """Per-sample dicts -> the batch dict VisionLanguageModule consumes (default_collate layout).
 
-    def __init__(self, upload: str = "u8", num_channels: int = 3):
+    mean / std: the intensity normalisation (the reference's NormalizeIntensityd with
+    the fold's dataset statistics, PretrainDataModule.py:283-288).  The fp32 upload
+    applies it on the host; the u8 upload carries it as "x-ray-u8-norm" (two host
+    floats) and the module applies it on the device (vlp_stem_prep_u8)."""
+
+    def __init__(self, upload: str = "u8", num_channels: int = 3, mean: float = IMG_MEAN, std: float = IMG_STD):
         if upload not in ("u8", "fp32"):
             raise ValueError(f"upload must be 'u8' or 'fp32', got {upload!r}")
         self.upload, self.num_channels = upload, num_channels
+        self.mean, self.std = float(mean), float(std)
 
     def __call__(self, samples: List[dict]) -> dict:
         if not samples:
@@ -113,8 +120,9 @@ class PairCollator:
             if self.num_channels != 3:
                 raise ValueError("the u8 upload feeds the 3-channel ImageNet-layout stem")
             batch["x-ray-u8"] = x_u8
+            batch["x-ray-u8-norm"] = (self.mean, self.std)
         else:
-            batch["x-ray"] = normalize_u8(x_u8, self.num_channels)
+            batch["x-ray"] = normalize_u8(x_u8, self.num_channels, self.mean, self.std)
         return batch
 
 
@@ -220,9 +228,22 @@ class PretrainDataModule:
         self.train_dataset = SyntheticRadiographCaptions(n, image_size, seq_len, seed + 7919 * rank, "MURA")
         self.val_datasets = [SyntheticRadiographCaptions(nv, image_size, seq_len, seed + 1_000 + rank, "LERA"),
                              SyntheticRadiographCaptions(nv, image_size, seq_len, seed + 2_000 + rank, "MURA")]
-        self.collate = PairCollator(upload, num_channels)
+        # per-fold intensity statistics of the training images (the reference computes and
+        # caches them per fold, :217-267, for NormalizeIntensityd)
+        self.image_mean, self.image_std = self._intensity_stats(self.train_dataset)
+        self.collate = PairCollator(upload, num_channels, self.image_mean, self.image_std)
         if not disable_augmentations:
             logger.warning("PretrainDataModule: augmentations are not applied in the MI355X build")
+
+    @staticmethod
+    def _intensity_stats(ds, n: int = 64):
+        """Mean / std of the (histogram-equalised) uint8 pixels over up to n training
+        images; the synthetic U{0..255} pixels give ~127.5 / 73.9."""
+        k = min(n, len(ds))
+        if k == 0:
+            return IMG_MEAN, IMG_STD
+        x = torch.stack([ds[i]["x-ray-u8"] for i in range(k)]).double()
+        return float(x.mean()), float(x.std())
 
     def get_cv_splits(self):
         """(:270) one split; label weights (1, 1) as the pretraining experiments use."""

@@ -208,6 +208,7 @@ class FusionModule(_Base):
 
     def _unpack(self, batch):
         x = batch["x-ray"] if "x-ray" in batch else batch["x-ray-u8"]
+        self.image_network.u8_norm = tuple(batch.get("x-ray-u8-norm", (127.5, 73.9)))
         return (x, batch["tumor"], batch["dataset"], batch["anatomy_site_encoded"], batch["age_encoded"],
                 batch["sex_encoded"])
 

@@ -198,6 +198,15 @@ class _SymCEFn(torch.autograd.Function):
         return out
 
 
+def _logit_scale_fp64(module, state_dict, prefix, local_metadata):
+    """The reference's logit_scale is float64 (torch.tensor([np.log(1/0.07)]), :111);
+    the HIP head keeps it in its fp32 arena, the checkpoint carries the reference
+    dtype (loading casts back)."""
+    k = prefix + "logit_scale"
+    if k in state_dict:
+        state_dict[k] = state_dict[k].double()
+
+
 class VisionLanguageModule(_Base):
     # the fused step all-gathers embeddings and all-reduces the gradient arenas
     # itself (vlp_amd.clip_model.ClipStepFn); trainers must not reduce again
@@ -268,6 +277,7 @@ class VisionLanguageModule(_Base):
             self.downstream_val_dataloaders = dm.val_dataloader()
         self.train_image_embeddings_and_labels_cached = {}
         self.val_image_embeddings_and_labels_cached = {}
+        self._register_state_dict_hook(_logit_scale_fp64)
         logger.info("VisionLanguageModule (MI355X): initialized, compute_dtype=%s", compute_dtype)
 
     # ---------------- device moves keep arenas aliased ----------------
@@ -351,6 +361,7 @@ class VisionLanguageModule(_Base):
     def forward(self, batch):
         """:441-461 — returns (logits, image_embeddings, text_embeddings)."""
         x = batch["x-ray"] if "x-ray" in batch else batch["x-ray-u8"]   # u8: on-device normalise
+        self.image_encoder.model.u8_norm = tuple(batch.get("x-ray-u8-norm", (127.5, 73.9)))
         image_features = self.image_encoder(x.to(self.device, non_blocking=True))
         text_features = self.text_encoder(**{k: v.to(self.device, non_blocking=True)
                                              for k, v in batch["caption_tokenized"].items()})
@@ -386,7 +397,9 @@ class VisionLanguageModule(_Base):
         tt = tt.to(dev, non_blocking=True) if tt is not None else None
         if self.hparams["deduplicate"] or self.hparams["masked_loss"]:
             raise DeprecationWarning("deduplicate / masked loss were removed by the reference (:535-545)")
-        return ClipStepFn.apply(self._towers(), x, x_u8, ids, am, tt, *self._all_params())
+        towers = self._towers()
+        towers.u8_norm = tuple(batch.get("x-ray-u8-norm", (127.5, 73.9)))   # the collator's normalisation
+        return ClipStepFn.apply(towers, x, x_u8, ids, am, tt, *self._all_params())
 
     def training_step(self, batch, batch_idx=None):
         """:634-645 (fused: the logits matrix is never materialised)."""
@@ -531,8 +544,12 @@ class VisionLanguageModule(_Base):
         """Lightning-format checkpoint ({"state_dict", "hyper_parameters"}); loaded
         with weights_only=True (hyper-parameters holding objects must be passed
         again as kwargs, as src/train.py:198 does for the datamodule)."""
+        from src.utils.config import instantiate
         ckpt = torch.load(checkpoint_path, map_location="cpu", weights_only=True)
         hp = dict(ckpt.get("hyper_parameters", {}))
+        # factories saved as {_target_, _partial_} nodes (src/utils/trainer.serializable_hparams)
+        hp = {k: instantiate(v) if isinstance(v, dict) and "_target_" in v else v for k, v in hp.items()}
+        hp.pop("num_optimized_params", None)
         hp.update(kwargs)
         model = cls(**hp)
         model.load_state_dict(ckpt["state_dict"], strict=strict)

@@ -7,12 +7,17 @@ Same entry points and flow for the VLP pretraining experiments:
   train(cfg)  seed (train.yaml `seed`, :86-88) -> instantiate cfg.data (:90) -> for each
               (datamodule, label_weights) in get_cv_splits() (:105): set
               model.label_weights, instantiate cfg.model (:109-116) and cfg.trainer
-              (:163), trainer.fit(model, datamodule) (:185) -> per-fold metrics
-              (:188-192), aggregated over folds (:231-262).
+              (:163) with the configured callbacks (:123; Lightning's ModelCheckpoint /
+              EarlyStopping / LearningRateMonitor resolve to src/utils/trainer.py) ->
+              trainer.fit(model, datamodule) (:171) -> per-fold metrics -> for a
+              VisionLanguageModule with downstream data: reload the best checkpoint
+              (:189-198) and evaluate downstream precision@k (:204) -> metrics
+              aggregated over folds (:231-262).
 The late-fusion finetune (FusionModule + DownstreamDataModule) runs through the
 same path: `experiment=baseline_imaging_and_clinical/baseline_imaging_and_clinical_resnet_34`.
-Out of scope: W&B loggers, Lightning callbacks, t-SNE /
-confusion-matrix plots, downstream zero-shot evaluation and the baseline modules.
+Out of scope: W&B loggers (configured loggers whose package is
+absent are skipped with a warning), t-SNE / confusion-matrix plots, downstream
+zero-shot evaluation and the OnlyImaging baseline module.
 
 Multi-GPU: launch one process per GPU (`python -m torch.distributed.run
 --nproc-per-node N src/train.py ...`); train() initialises torch.distributed
@@ -57,6 +62,32 @@ def _init_distributed() -> None:
         torch.distributed.init_process_group(backend)
 
 
+def instantiate_callbacks(cb_cfg) -> List[Any]:
+    """src/utils/instantiators.py:instantiate_callbacks: every node with a _target_."""
+    out = []
+    for name, node in (cb_cfg or {}).items():
+        if isinstance(node, dict) and "_target_" in node:
+            log.info("Train: Instantiating callback <%s>", node["_target_"])
+            out.append(instantiate(node))
+    return out
+
+
+def instantiate_loggers(lg_cfg) -> List[Any]:
+    """Loggers whose package is installed; the others (wandb here) are skipped."""
+    import importlib.util
+    out = []
+    for name, node in (lg_cfg or {}).items():
+        if not (isinstance(node, dict) and "_target_" in node):
+            continue
+        pkg = node["_target_"].split(".")[0]
+        need = "wandb" if "wandb" in node["_target_"].lower() else pkg
+        if importlib.util.find_spec(pkg) is None or importlib.util.find_spec(need) is None:
+            log.warning("Train: logger <%s> skipped (%s is not installed)", node["_target_"], need)
+            continue
+        out.append(instantiate(node))
+    return out
+
+
 def train(cfg: Dict[str, Any]) -> Tuple[Dict[str, Any], Dict[str, Any]]:
     if cfg.get("k_fold_cross_validation", False):
         log.info("Train: Doing k-fold cross validation.")
@@ -74,11 +105,13 @@ def train(cfg: Dict[str, Any]) -> Tuple[Dict[str, Any], Dict[str, Any]]:
         model_cfg["label_weights"] = label_weights
         if "FusionModule" in model_cfg["_target_"]:
             model_cfg.pop("downstream_datamodule", None)
-        elif model_cfg.get("downstream_datamodule") in ({}, "null"):
+        elif not isinstance(model_cfg.get("downstream_datamodule"), dict) or not model_cfg["downstream_datamodule"]:
+            # model/vision_language.yaml names the group option ("downstream"); the experiments
+            # interpolate the composed ${downstream_data} node, anything else means none
             model_cfg["downstream_datamodule"] = None
         log.info("Train: Instantiating model <%s>", model_cfg["_target_"])
         model = instantiate(model_cfg)
-        callbacks = []
+        callbacks = instantiate_callbacks(cfg.get("callbacks"))
         if cfg.get("downstream_data") and "VisionLanguageModule" in model_cfg["_target_"]:   # :123-134
             from src.utils.LinearProbeCallback import LinearProbeCallback
             ds_dm = instantiate(cfg["downstream_data"])
@@ -86,8 +119,13 @@ def train(cfg: Dict[str, Any]) -> Tuple[Dict[str, Any], Dict[str, Any]]:
             callbacks.append(LinearProbeCallback(dm.train_dataloader(), dm.val_dataloader()))
             log.info("Train: Added LinearProbeCallback to callbacks.")
         log.info("Train: Instantiating trainer <%s>", cfg["trainer"]["_target_"])
-        trainer = instantiate(cfg["trainer"], callbacks=callbacks, logger=None)
-        objects.update(model=model, trainer=trainer)
+        loggers = instantiate_loggers(cfg.get("logger"))
+        tkw = {"callbacks": callbacks, "logger": loggers or None}
+        out_dir = (cfg.get("paths") or {}).get("output_dir")
+        if out_dir and "default_root_dir" not in cfg["trainer"]:
+            tkw["default_root_dir"] = out_dir
+        trainer = instantiate(cfg["trainer"], **tkw)
+        objects.update(model=model, trainer=trainer, callbacks=callbacks)
         if cfg.get("train", True):
             trainer.fit(model=model, datamodule=fold_dm)
             bs = getattr(fold_dm, "batch_size", 0)
@@ -95,7 +133,21 @@ def train(cfg: Dict[str, Any]) -> Tuple[Dict[str, Any], Dict[str, Any]]:
             log.info("Train: %d steps in %.2f s (%.1f image-text pairs/s incl. data loading, %d rank(s))",
                      trainer.global_step, trainer.fit_seconds,
                      ws * bs * trainer.global_step / max(trainer.fit_seconds, 1e-9), ws)
-        all_fold_metrics.append(dict(trainer.logged_metrics))
+        fold_metrics = dict(trainer.logged_metrics)
+        if "VisionLanguageModule" in model_cfg["_target_"] and cfg.get("downstream_data"):   # :189-210
+            ck = trainer.checkpoint_callback
+            if ck is not None and ck.best_model_path and os.path.exists(ck.best_model_path):
+                log.info("Train: Using best model path from trainer: %s", ck.best_model_path)
+                ds = instantiate(cfg["downstream_data"])
+                model = type(model).load_from_checkpoint(ck.best_model_path, downstream_datamodule=ds,
+                                                         device=model.device)
+                objects["model"] = model
+            else:
+                log.warning("Train: No best model path found in trainer, using current model weights.")
+            if getattr(model, "downstream_datamodule", None) is not None:
+                for k, v in model.evaluate_downstream_precision_at_k(mode="entire").items():
+                    fold_metrics[f"downstream_entire/label_precision_at_{k}"] = v
+        all_fold_metrics.append(fold_metrics)
         if not cfg.get("k_fold_cross_validation", False):
             break
     metrics: Dict[str, Any] = {}

@@ -10,10 +10,19 @@ reference's configs use (configs/train.yaml, configs/experiment/pretrain/*.yaml)
   * `${a.b}` interpolation (a whole-string reference keeps the referenced
     node's type; embedded references are substituted as text);
   * command-line overrides `experiment=pretrain/x`, `group=choice`, `a.b=value`;
+  * group files with their own `defaults` list (configs/callbacks/*.yaml: plain
+    names are options of the same group, merged in order around `_self_`);
+  * the resolvers the reference configs use: `${oc.env:VAR[,default]}` (an
+    unset PROJECT_ROOT falls back to the working directory) and
+    `${hydra:runtime.output_dir}` / `${hydra:runtime.cwd}` (run directory
+    logs/<task_name>/runs/<timestamp> under the working directory, as Hydra's);
+    an interpolation whose key does not exist stays unresolved text (Hydra
+    resolves lazily, so such a node only fails where it is used);
   * hydra.utils.instantiate semantics: `_target_` is imported and called with
     the other keys (recursively instantiated), `_partial_: true` returns a
-    functools.partial.  `lightning.pytorch.trainer.Trainer` resolves to
-    src.utils.trainer.Trainer when Lightning is absent.
+    functools.partial.  Lightning targets resolve to src.utils.trainer
+    (Trainer, ModelCheckpoint, EarlyStopping, LearningRateMonitor) when
+    Lightning is absent.
 """
 from __future__ import annotations
 
@@ -30,7 +39,11 @@ import yaml
 CONFIG_DIR = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", "..", "configs"))
 _INTERP = re.compile(r"\$\{([^}]+)\}")
 _FALLBACK_TARGETS = {"lightning.pytorch.trainer.Trainer": "src.utils.trainer.Trainer",
-                     "lightning.Trainer": "src.utils.trainer.Trainer"}
+                     "lightning.Trainer": "src.utils.trainer.Trainer",
+                     "lightning.pytorch.callbacks.ModelCheckpoint": "src.utils.trainer.ModelCheckpoint",
+                     "lightning.pytorch.callbacks.EarlyStopping": "src.utils.trainer.EarlyStopping",
+                     "lightning.pytorch.callbacks.LearningRateMonitor": "src.utils.trainer.LearningRateMonitor"}
+_RUN_STAMP = None
 
 
 def _load(path: str) -> dict:
@@ -44,6 +57,27 @@ def _group_file(root: str, group: str, choice: str) -> str:
     if not os.path.exists(p):
         raise FileNotFoundError(f"config group {group!r} has no option {choice!r} ({p})")
     return p
+
+
+def _load_group(root: str, group: str, choice: str) -> dict:
+    """A group option, with its own defaults list (options of the same group)."""
+    node = _load(_group_file(root, group, choice))
+    if not isinstance(node, dict):
+        return node
+    defs = node.pop("defaults", None)
+    if not defs:
+        return node
+    out: dict = {}
+    if "_self_" not in defs:
+        defs = list(defs) + ["_self_"]
+    for e in defs:
+        if e == "_self_":
+            merge(out, node)
+        elif isinstance(e, str):
+            merge(out, _load_group(root, group, e))
+        else:
+            raise ValueError(f"unsupported defaults entry {e!r} in {group}/{choice}")
+    return out
 
 
 def merge(dst: dict, src: dict) -> dict:
@@ -133,8 +167,11 @@ def compose(config_name: str = "train", overrides: Optional[List[str]] = None,
             choice = choices.get(g, c) if pkg == g else c
             if choice in (None, "null"):
                 continue
-            node = _load(_group_file(config_dir, g, choice))
-            merge(cfg.setdefault(pkg, {}), node)
+            node = _load_group(config_dir, g, choice)
+            if isinstance(node, dict):
+                merge(cfg.setdefault(pkg, {}), node)
+            else:
+                cfg[pkg] = {} if node is None else node
     for k, v in plain:
         _set_path(cfg, k, yaml.safe_load(v))
     return resolve(cfg)
@@ -143,6 +180,28 @@ def compose(config_name: str = "train", overrides: Optional[List[str]] = None,
 def resolve(cfg: dict) -> dict:
     """Resolve ${...} interpolations against the root (repeat until stable)."""
     root = copy.deepcopy(cfg)
+
+    def lookup(key, depth):
+        if key.startswith("oc.env:"):
+            var, _, default = key[len("oc.env:"):].partition(",")
+            val = os.environ.get(var.strip())
+            if val is None:
+                val = default.strip() if default else (os.getcwd() if var.strip() == "PROJECT_ROOT" else None)
+            if val is None:
+                raise KeyError(f"interpolation ${{{key}}}: environment variable {var} is not set")
+            return val
+        if key.startswith("hydra:"):
+            what = key[len("hydra:"):].strip()
+            if what == "runtime.cwd":
+                return os.getcwd()
+            if what == "runtime.output_dir":
+                global _RUN_STAMP
+                if _RUN_STAMP is None:
+                    import time
+                    _RUN_STAMP = time.strftime("%Y-%m-%d_%H-%M-%S")
+                return os.path.join(os.getcwd(), "logs", str(root.get("task_name", "train")), "runs", _RUN_STAMP)
+            raise KeyError(f"unsupported hydra resolver ${{{key}}}")
+        return res(copy.deepcopy(_get_path(root, key)), depth + 1)
 
     def res(node, depth=0):
         if depth > 32:
@@ -153,10 +212,15 @@ def resolve(cfg: dict) -> dict:
             return [res(v, depth) for v in node]
         if isinstance(node, str):
             m = _INTERP.fullmatch(node)
-            if m:
-                return res(copy.deepcopy(_get_path(root, m.group(1).strip())), depth + 1)
-            if _INTERP.search(node):
-                return _INTERP.sub(lambda mm: str(res(_get_path(root, mm.group(1).strip()), depth + 1)), node)
+            try:
+                if m:
+                    return lookup(m.group(1).strip(), depth)
+                if _INTERP.search(node):
+                    return _INTERP.sub(lambda mm: str(lookup(mm.group(1).strip(), depth)), node)
+            except KeyError as e:
+                if "missing key" in str(e):
+                    return node          # unresolvable: stays text until (unless) it is used
+                raise
         return node
 
     return res(root)

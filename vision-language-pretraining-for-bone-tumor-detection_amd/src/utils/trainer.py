@@ -16,12 +16,23 @@ modules (FusionModule) the trainer averages gradients after backward as DDP
 would: the module's `all_reduce_gradients()` when it has one (one RCCL call
 over the ResNet34 tower's flat gradient arena), else one flat SUM all-reduce
 over every gradient, divided by the world size.
+
+Callbacks (the Lightning ones the reference configs name resolve here when
+Lightning is absent, src/utils/config.py): ModelCheckpoint (best-k by a
+monitored metric, Lightning checkpoint dict {state_dict, hyper_parameters,
+epoch, global_step}; `trainer.checkpoint_callback.best_model_path` feeds
+src/train.py's post-fit reload as in the reference :189-198), EarlyStopping
+(patience on a monitored metric) and LearningRateMonitor.  Validation runs
+every epoch over all batches unless limit_val_batches says otherwise
+(Lightning's defaults).
 """
 from __future__ import annotations
 
+import functools
 import logging
 import math
 import os
+import re
 import time
 from typing import List, Optional
 
@@ -32,12 +43,156 @@ from src.data.PretrainDataModule import DevicePrefetcher
 logger = logging.getLogger("project")
 
 
+def _metric(trainer, key):
+    v = trainer.logged_metrics.get(key)
+    if v is None:
+        return None
+    return float(v.detach()) if torch.is_tensor(v) else float(v)
+
+
+def _rank0():
+    d = torch.distributed
+    return not (d.is_available() and d.is_initialized()) or d.get_rank() == 0
+
+
+def serializable_hparams(hp) -> dict:
+    """Module hyper-parameters as a weights_only-loadable dict: primitives kept,
+    functools.partial (optimizer / scheduler factories) as a `_target_` /
+    `_partial_` node that src/utils/config.instantiate rebuilds, other objects
+    (the downstream datamodule) dropped -- load_from_checkpoint takes them as
+    kwargs again, as src/train.py:198 does."""
+    def conv(v):
+        if v is None or isinstance(v, (bool, int, float, str)):
+            return v
+        if isinstance(v, (list, tuple)):
+            out = [conv(x) for x in v]
+            return None if any(x is _DROP for x in out) else out
+        if isinstance(v, dict):
+            return {k: conv(x) for k, x in v.items() if conv(x) is not _DROP}
+        if isinstance(v, functools.partial):
+            f = v.func
+            return {"_target_": f"{f.__module__}.{f.__qualname__}", "_partial_": True,
+                    **{k: conv(x) for k, x in v.keywords.items()}}
+        return _DROP
+    out = {}
+    for k, v in dict(hp or {}).items():
+        c = conv(v)
+        if c is not _DROP:
+            out[k] = c
+    return out
+
+
+_DROP = object()
+
+
+class ModelCheckpoint:
+    """lightning.pytorch.callbacks.ModelCheckpoint (the options the reference
+    configs use: monitor, mode, filename with {epoch} / {metric[:fmt]} fields,
+    save_top_k, auto_insert_metric_name, dirpath).  monitor=None keeps the last
+    epoch's checkpoint (Lightning's default checkpointing)."""
+
+    def __init__(self, dirpath: Optional[str] = None, filename: Optional[str] = None, monitor: Optional[str] = None,
+                 mode: str = "min", save_top_k: int = 1, auto_insert_metric_name: bool = True,
+                 save_last: bool = False, verbose: bool = False, **unused):
+        if mode not in ("min", "max"):
+            raise ValueError(f"ModelCheckpoint: mode must be 'min' or 'max', got {mode!r}")
+        self.dirpath, self.filename, self.monitor, self.mode = dirpath, filename, monitor, mode
+        self.save_top_k, self.auto_insert_metric_name = save_top_k, auto_insert_metric_name
+        self.best_model_path, self.best_model_score = "", None
+        self._kept = []   # (score, path), best first
+
+    def _format(self, trainer, score):
+        name = self.filename or ("{epoch}-{step}" if self.monitor is None else "{epoch}-{" + self.monitor + "}")
+        vals = {"epoch": trainer.current_epoch, "step": trainer.global_step}
+
+        def sub(m):
+            key, _, fmt = m.group(1).partition(":")
+            v = vals.get(key, _metric(trainer, key))
+            txt = "nan" if v is None else format(v, fmt) if fmt else str(v)
+            return (f"{key}={txt}" if self.auto_insert_metric_name else txt).replace("/", "_")
+        return re.sub(r"\{([^}]+)\}", sub, name) + ".ckpt"
+
+    def _better(self, a, b):
+        return b is None or (a < b if self.mode == "min" else a > b)
+
+    def on_validation_end(self, trainer, pl_module):
+        if self.save_top_k == 0:
+            return
+        score = None
+        if self.monitor is not None:
+            score = _metric(trainer, self.monitor)
+            if score is None or not math.isfinite(score):
+                return
+            worst = self._kept[-1][0] if len(self._kept) >= self.save_top_k > 0 else None
+            if worst is not None and not self._better(score, worst):
+                return
+        d = self.dirpath or os.path.join(trainer.default_root_dir, "checkpoints")
+        path = os.path.join(d, self._format(trainer, score))
+        if _rank0():
+            os.makedirs(d, exist_ok=True)
+            trainer.save_checkpoint(path, pl_module)
+        if self.monitor is None:
+            for _, old in self._kept:
+                if old != path and _rank0() and os.path.exists(old):
+                    os.remove(old)
+            self._kept = [(None, path)]
+        else:
+            self._kept.append((score, path))
+            self._kept.sort(key=lambda t: t[0], reverse=self.mode == "max")
+            while self.save_top_k > 0 and len(self._kept) > self.save_top_k:
+                _, old = self._kept.pop()
+                if _rank0() and os.path.exists(old):
+                    os.remove(old)
+        self.best_model_path = self._kept[0][1]
+        self.best_model_score = self._kept[0][0]
+
+
+class EarlyStopping:
+    """lightning.pytorch.callbacks.EarlyStopping: stop once the monitored metric
+    has not improved (by more than min_delta) for `patience` validation rounds."""
+
+    def __init__(self, monitor: str, mode: str = "min", patience: int = 3, min_delta: float = 0.0,
+                 verbose: bool = False, **unused):
+        self.monitor, self.mode, self.patience, self.min_delta, self.verbose = monitor, mode, patience, min_delta, verbose
+        self.best, self.wait = None, 0
+
+    def on_validation_end(self, trainer, pl_module):
+        v = _metric(trainer, self.monitor)
+        if v is None:
+            return
+        improved = self.best is None or (v < self.best - self.min_delta if self.mode == "min"
+                                         else v > self.best + self.min_delta)
+        if improved:
+            self.best, self.wait = v, 0
+            return
+        self.wait += 1
+        if self.wait >= self.patience:
+            trainer.should_stop = True
+            if self.verbose:
+                logger.info("EarlyStopping: %s did not improve for %d rounds (best %.5f)", self.monitor,
+                            self.wait, self.best)
+
+
+class LearningRateMonitor:
+    """lightning.pytorch.callbacks.LearningRateMonitor: logs each param group's lr."""
+
+    def __init__(self, logging_interval: Optional[str] = None, **unused):
+        self.logging_interval = logging_interval
+
+    def on_train_epoch_end(self, trainer, pl_module):
+        opt = getattr(trainer, "optimizer", None)
+        if opt is None:
+            return
+        for i, g in enumerate(opt.param_groups):
+            trainer.logged_metrics[f"lr-{type(opt).__name__}/{g.get('name', i)}"] = g["lr"]
+
+
 class Trainer:
     def __init__(self, min_epochs: int = 1, max_epochs: int = 10, accelerator: str = "auto",
                  devices="auto", log_every_n_steps: int = 1, max_steps: int = -1,
-                 limit_train_batches: Optional[int] = None, limit_val_batches: Optional[int] = 0,
-                 callbacks: Optional[List] = None, logger=None, enable_checkpointing: bool = False,
-                 default_root_dir: Optional[str] = None, **unused):
+                 limit_train_batches: Optional[int] = None, limit_val_batches: Optional[int] = None,
+                 callbacks: Optional[List] = None, logger=None, enable_checkpointing: bool = True,
+                 default_root_dir: Optional[str] = None, check_val_every_n_epoch: int = 1, **unused):
         if max_epochs is not None and min_epochs is not None and min_epochs > max_epochs:
             raise ValueError("min_epochs > max_epochs")
         self.min_epochs, self.max_epochs = min_epochs, max_epochs
@@ -46,8 +201,12 @@ class Trainer:
         self.max_steps = max_steps
         self.limit_train_batches, self.limit_val_batches = limit_train_batches, limit_val_batches
         self.callbacks = list(callbacks or [])
-        self.default_root_dir = default_root_dir
+        self.default_root_dir = default_root_dir or os.getcwd()
         self.enable_checkpointing = enable_checkpointing
+        self.check_val_every_n_epoch = max(1, int(check_val_every_n_epoch))
+        if enable_checkpointing and not any(isinstance(c, ModelCheckpoint) for c in self.callbacks):
+            self.callbacks.append(ModelCheckpoint())     # Lightning's default: the last epoch
+        self.should_stop = False
         self.global_step = 0
         self.current_epoch = 0
         self.sanity_checking = False
@@ -59,6 +218,26 @@ class Trainer:
 
     def _device(self, model):
         return model.device
+
+    @property
+    def checkpoint_callback(self):
+        return next((c for c in self.callbacks if isinstance(c, ModelCheckpoint)), None)
+
+    @property
+    def callback_metrics(self):
+        return self.logged_metrics
+
+    def _hook(self, name, model):
+        for cb in self.callbacks:
+            fn = getattr(cb, name, None)
+            if fn is not None:
+                fn(self, model)
+
+    def save_checkpoint(self, path, model):
+        """Lightning checkpoint dict, loadable with torch.load(weights_only=True)."""
+        sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+        torch.save({"state_dict": sd, "hyper_parameters": serializable_hparams(getattr(model, "hparams", {})),
+                    "epoch": self.current_epoch, "global_step": self.global_step}, path)
 
     @staticmethod
     def _dp_world():
@@ -98,7 +277,7 @@ class Trainer:
         model.trainer = self
         if datamodule is not None:
             train_dataloaders = datamodule.train_dataloader()
-            if self.limit_val_batches:
+            if self.limit_val_batches != 0 and hasattr(datamodule, "val_dataloader"):
                 val_dataloaders = datamodule.val_dataloader()
         conf = model.configure_optimizers()
         optimizer = conf["optimizer"] if isinstance(conf, dict) else conf
@@ -136,15 +315,16 @@ class Trainer:
                     break
             if hasattr(model, "on_train_epoch_end"):
                 model.on_train_epoch_end()
-            for cb in self.callbacks:               # e.g. LinearProbeCallback (every n-th epoch)
-                if hasattr(cb, "on_validation_start"):
-                    cb.on_validation_start(self, model)
-            if val_dataloaders and self.limit_val_batches:
-                self.validate(model, val_dataloaders)
+            self._hook("on_train_epoch_end", model)
+            if (epoch + 1) % self.check_val_every_n_epoch == 0:
+                self._hook("on_validation_start", model)   # e.g. LinearProbeCallback (every n-th epoch)
+                if val_dataloaders and self.limit_val_batches != 0:
+                    self.validate(model, val_dataloaders)
+                self._hook("on_validation_end", model)    # checkpointing, early stopping
             if sched is not None:
                 s = sched["scheduler"] if isinstance(sched, dict) else sched
                 s.step()
-            if stop and epoch + 1 >= (self.min_epochs or 0):
+            if (stop or self.should_stop) and epoch + 1 >= (self.min_epochs or 0):
                 break
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
@@ -163,4 +343,9 @@ class Trainer:
                 model.validation_step(batch, j, idx)
         if hasattr(model, "on_validation_epoch_end"):
             model.on_validation_epoch_end()
+        for k, v in getattr(model, "logged", {}).items():
+            if k.startswith("val") and torch.is_tensor(v) and v.numel() == 1:
+                self.logged_metrics[k] = float(v.detach())
+            elif k.startswith("val") and isinstance(v, (int, float)):
+                self.logged_metrics[k] = float(v)
         model.train()

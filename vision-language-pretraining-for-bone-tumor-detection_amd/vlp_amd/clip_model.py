@@ -116,6 +116,7 @@ class ClipStepFn(torch.autograd.Function):
     def forward(ctx, model, x, x_u8, input_ids, attention_mask, token_type_ids, *params):
         img_t, txt_t, head = model.image_tower, model.text_tower, model.head
         training = model.training
+        u8n = getattr(model, "u8_norm", (127.5, 73.9))
         main = torch.cuda.current_stream(input_ids.device) if input_ids.is_cuda else None
         s_txt = _text_stream(input_ids.device)
         if s_txt is not None:
@@ -125,10 +126,10 @@ class ClipStepFn(torch.autograd.Function):
                 # only the CLS token's last hidden state is used (TextEncoder, :57-60)
                 h_last, sv_txt = txt_t.run_forward(input_ids, attention_mask, token_type_ids, training,
                                                    cls_only=True)
-            feat_img, sv_img = img_t.run_forward(x, training, x_u8=x_u8)
+            feat_img, sv_img = img_t.run_forward(x, training, x_u8=x_u8, u8_norm=u8n)
             main.wait_stream(s_txt)   # join before the head
         else:
-            feat_img, sv_img = img_t.run_forward(x, training, x_u8=x_u8)
+            feat_img, sv_img = img_t.run_forward(x, training, x_u8=x_u8, u8_norm=u8n)
             h_last, sv_txt = txt_t.run_forward(input_ids, attention_mask, token_type_ids, training, cls_only=True)
         B, Tn = input_ids.shape
         D, E = txt_t.cfg.hidden, head.embedding_dim

@@ -165,6 +165,8 @@ class ResNet34Tower(ArenaModule):
                 self._blocks.append((pre, (pre + ".downsample.0") in self._convs))
         self.reset_parameters()
         self._ws = {}  # per-device workspaces (packed weights, wgrad buffers, BN coefficients)
+        self._dbg = None   # dict: block -> (gradient of its output, masked) during backward
+        self.u8_norm = (127.5, 73.9)   # (mean, std) of the uint8 upload; set per batch by the module
 
     # ---------------- init (timm ResNet.init_weights) ----------------
     @torch.no_grad()
@@ -388,6 +390,8 @@ class ResNet34Tower(ArenaModule):
             M = N * Hh * Ww
             last = dout is None
             dbc = dfeat if last else None
+            if self._dbg is not None and dout is not None:   # diagnostics (tools/diag_blocks.py)
+                self._dbg[pre] = (dout.detach().clone(), dout_masked)
             HW = Hh * Ww
             c1, c2 = self._convs[pre + ".conv1"], self._convs[pre + ".conv2"]
             k1, k2 = pre + ".bn1", pre + ".bn2"
@@ -470,6 +474,10 @@ class ResNet34Tower(ArenaModule):
                 dx = ops.conv_dgrad(dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, addend=addend)
                 dout_masked = False
             self._wgrad(ws, c1, dy1, x, dyT=tA)
+            if self._dbg is not None:
+                self._dbg[pre + "/dy2"] = (dy2.detach().clone(), False)
+                self._dbg[pre + "/g1"] = (g1.detach().clone(), False)
+                self._dbg[pre + "/dy1"] = (dy1.detach().clone(), False)
             dout = dx
             stage = pre.split(".", 1)[0]
             if pre.endswith(".0") and stage != "layer1":
@@ -534,7 +542,7 @@ class ImageTowerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, tower: ResNet34Tower, x, *params):
         if x.dtype == torch.uint8:   # collated 1-channel upload (src/data/PretrainDataModule.py)
-            feat, saved = tower.run_forward(None, tower.training, x_u8=x)
+            feat, saved = tower.run_forward(None, tower.training, x_u8=x, u8_norm=tower.u8_norm)
         else:
             feat, saved = tower.run_forward(x, tower.training)
         ctx.tower = tower
