@@ -263,10 +263,13 @@ def test_fused_adamw_matches_torch_and_state_dict_roundtrip():
     batch = synth_batch(B, H, T, 0)
 
     def model(fused):
+        # the module's own init: its gradients are well conditioned, so the two runs stay
+        # on one trajectory (the recipe weights' BN stack turns fp32 update rounding into
+        # ~1 % gradient differences by step 2, see grad_envelope_check)
+        torch.manual_seed(0)
         m = VisionLanguageModule("resnet34", "tinybert", functools.partial(torch.optim.AdamW, lr=1e-3),
                                  False, False, 512, 312, 128, compute_dtype="fp32", text_dropout=0.0,
                                  fused_optimizer=fused)
-        W.apply_recipe(m, 0)
         m.train()
         return m, m.configure_optimizers()["optimizer"]
 
@@ -277,7 +280,10 @@ def test_fused_adamw_matches_torch_and_state_dict_roundtrip():
         torch.cuda.synchronize()
 
     def flat(m):
-        return torch.cat([p.detach().double().flatten().cpu() for p in m.parameters()])
+        # attention key biases have an exactly-zero true gradient (softmax shift invariance):
+        # AdamW turns their rounding noise into +-lr steps, different in every run
+        return torch.cat([p.detach().double().flatten().cpu() for k, p in m.named_parameters()
+                          if "attention.self.key.bias" not in k])
 
     mf, of = model(True)
     mt, ot = model(False)
@@ -295,7 +301,7 @@ def test_fused_adamw_matches_torch_and_state_dict_roundtrip():
         m2, o2 = model(True)
         m2.load_state_dict(src_model.state_dict())
         o2.load_state_dict(src_sd)
-        ref = [p.detach().clone() for p in src_model.parameters()]
+        ref = [p.detach().clone() for k, p in src_model.named_parameters() if "attention.self.key.bias" not in k]
         m_next, o_next = (mf, of) if src_model is mf else (mt, ot)
         step(m_next, o_next)
         step(m2, o2)

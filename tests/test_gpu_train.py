@@ -64,15 +64,22 @@ def test_api_forward_u8_equals_fp32_eval():
     assert ((fu - fo).norm() / fo.norm()).item() < 1e-4                    # linear-probe features vs oracle
 
 
-def test_train_main_runs_and_is_deterministic():
+def test_train_main_runs_and_is_deterministic(tmp_path):
+    """Also: validation over [lera, mura] every epoch, the reference's
+    checkpoint_combined callback keeps the best val/combined/loss checkpoint, and
+    the post-fit step reloads it and evaluates downstream precision@k (:189-210)."""
     from src import train as T
     from src.utils.config import compose
     hist = []
-    for _ in range(2):
-        cfg = compose("train", _ARGS)
+    for run in range(2):
+        cfg = compose("train", _ARGS + [f"paths.output_dir={tmp_path / str(run)}"])
         metrics, objs = T.train(cfg)
         tr = objs["trainer"]
         assert tr.global_step == 4
+        ck = tr.checkpoint_callback
+        assert ck.monitor == "val/combined/loss" and ck.best_model_path.startswith(str(tmp_path / str(run)))
+        assert "val/combined/loss" in tr.logged_metrics and "best_model" in objs
+        assert any(k.startswith("downstream_entire/label_precision_at_") for k in metrics)
         hist.append([l for _, l in tr.history])
         assert all(torch.isfinite(torch.tensor(h)) for h in hist[-1])
         assert "train/loss" in metrics

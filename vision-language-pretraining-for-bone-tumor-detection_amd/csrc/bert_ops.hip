@@ -245,109 +245,290 @@ colsum_vec_kernel(int M, int N, const bf16* __restrict__ x, int ld, float* __res
 }
 
 // ---------------- attention ----------------
-// One workgroup per (sequence b, head h).  qkv: [B*T][3*Dm] rows (q | k | v),
-// head slice [h*dh, (h+1)*dh).  Saves softmax probabilities P[b][h][T][T] (fp32).
+// BertSelfAttention (transformers, called through VisionLanguageModule.py:45,
+// 57-60): S = Q K^T * scale + ext_mask, P = softmax(S), P' = dropout(P),
+// ctx = P' V.  ONE WAVE per (sequence b, head h): the token dimension is padded
+// to TB*16 (T <= 64) and the head dimension (26 for TinyBERT) to 32, and every
+// product is a chain of 16x16 MFMA tiles on LDS-staged operands:
+//   bf16: v_mfma_f32_16x16x32_bf16 (one K-step of 32),
+//   fp32 (parity mode): v_mfma_f32_16x16x4f32 x 4 per K-step of 16 (exact fp32 fma).
+// Convention (mma()): D[m][n] = sum_k X[m][k] * Y[n][k] over row-major LDS
+// images X, Y (k contiguous); lane l = 16g + i ends up holding D[4g + r][i],
+// r = 0..3.  So with Y = the query rows, each lane owns ONE query i and four
+// consecutive keys / head channels, and the softmax row reductions are two
+// cross-lane xor-shuffles (lanes i, i+16, i+32, i+48) -- a wavefront-reduced
+// softmax with no LDS traffic.
+// The masked-key bias is HF's: scores + finfo(fp32).min where attention_mask == 0
+// (modeling_bert get_extended_attention_mask); padded key slots (j >= T) are -inf.
+// P (fp32, pre-dropout, [B][H][T][T]) is saved for the backward.
 constexpr int kMaxT = 64;
 constexpr int kMaxDh = 32;
 
+template <typename T> struct AttnMma;
+template <> struct AttnMma<bf16> {
+  static constexpr int KS = 32;   // k per MFMA step
+  __device__ static __forceinline__ void mma(v4f& acc, const bf16* X, int ldx, int xr, const bf16* Y, int ldy,
+                                             int yr, int k0) {
+    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+    const v8bf a = *reinterpret_cast<const v8bf*>(X + (xr + i) * ldx + k0 + 8 * g);
+    const v8bf b = *reinterpret_cast<const v8bf*>(Y + (yr + i) * ldy + k0 + 8 * g);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+  }
+};
+template <> struct AttnMma<float> {
+  static constexpr int KS = 16;
+  __device__ static __forceinline__ void mma(v4f& acc, const float* X, int ldx, int xr, const float* Y, int ldy,
+                                             int yr, int k0) {
+    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+    const v4f a = *reinterpret_cast<const v4f*>(X + (xr + i) * ldx + k0 + 4 * g);
+    const v4f b = *reinterpret_cast<const v4f*>(Y + (yr + i) * ldy + k0 + 4 * g);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
+  }
+};
+
+// row reductions over the 4 lanes (i, i+16, i+32, i+48) holding one query
+__device__ __forceinline__ float q4_max(float v) {
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  return fmaxf(v, __shfl_xor(v, 32, 64));
+}
+__device__ __forceinline__ float q4_sum(float v) {
+  v += __shfl_xor(v, 16, 64);
+  return v + __shfl_xor(v, 32, 64);
+}
+
+// LDS image geometry (elements): rows of a "k = head channel" image hold DP = 32
+// values (+ pad), rows of a "k = token" image TPK = TB*16 values, rounded up to
+// the MFMA K-step (+ pad); pads keep 16-B row alignment and spread LDS banks.
+template <typename T, int TB>
+struct AttnGeom {
+  static constexpr int TP = TB * 16;                                   // padded tokens
+  static constexpr int KS = AttnMma<T>::KS;
+  static constexpr int TK = (TP + KS - 1) / KS * KS;                   // token-k extent
+  static constexpr int PADE = 16 / (int)sizeof(T);                     // one 16-B pad
+  static constexpr int LD = 32 + PADE;                                 // k = channel
+  static constexpr int LT = TK + PADE;                                 // k = token
+};
+
 template <typename T>
-__global__ void __launch_bounds__(256)
-attn_fwd_kernel(int B, int Tn, int H, int dh, const T* __restrict__ qkv,
-                const int64_t* __restrict__ amask, T* __restrict__ ctx, float* __restrict__ P,
-                float scale, float p, uint64_t seed) {
-  __shared__ float q[kMaxT][kMaxDh + 1], k[kMaxT][kMaxDh + 1], v[kMaxT][kMaxDh + 1];
-  __shared__ float S[kMaxT][kMaxT + 1];
-  const int b = blockIdx.x / H, h = blockIdx.x % H;
-  const int Dm = H * dh, ld = 3 * Dm;
-  for (int e = threadIdx.x; e < Tn * dh; e += blockDim.x) {
-    int t = e / dh, d = e % dh;
-    const T* r = qkv + (size_t)(b * Tn + t) * ld + h * dh + d;
-    q[t][d] = to_f(r[0]);
-    k[t][d] = to_f(r[Dm]);
-    v[t][d] = to_f(r[2 * Dm]);
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < Tn * Tn; e += blockDim.x) {
-    int i = e / Tn, j = e % Tn;
-    float s = 0.f;
-    for (int d = 0; d < dh; ++d) s += q[i][d] * k[j][d];
-    s *= scale;
-    if (amask && amask[b * Tn + j] == 0) s = -1e30f;
-    S[i][j] = s;
-  }
-  __syncthreads();
-  // row softmax: one wave per row
-  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
-  for (int i = wv; i < Tn; i += 4) {
-    float x = l < Tn ? S[i][l] : -INFINITY;
-    float mx = warp_max(x);
-    float ex = l < Tn ? __expf(x - mx) : 0.f;
-    float sum = warp_sum(ex);
-    if (l < Tn) {
-      float pr = ex / sum;
-      P[(((size_t)b * H + h) * Tn + i) * Tn + l] = pr;
-      if (p > 0.f) pr *= drop_scale(seed, (((uint64_t)b * H + h) * Tn + i) * Tn + l, p);
-      S[i][l] = pr;
-    }
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < Tn * dh; e += blockDim.x) {
-    int i = e / dh, d = e % dh;
-    float s = 0.f;
-    for (int j = 0; j < Tn; ++j) s += S[i][j] * v[j][d];
-    ctx[(size_t)(b * Tn + i) * Dm + h * dh + d] = from_f<T>(s);
+__device__ __forceinline__ void zero_lds(T* p, int n) {
+  for (int e = threadIdx.x & 63; e < n; e += 64) p[e] = from_f<T>(0.f);
+}
+
+// rows t < Tn, channels d < dh of one head slice -> LDS image (row-major or transposed)
+template <typename T>
+__device__ __forceinline__ void load_head(T* dst, int ld, bool transpose, const T* src, size_t src_ld, int Tn,
+                                          int dh) {
+  for (int e = threadIdx.x & 63; e < Tn * dh; e += 64) {
+    const int t = e / dh, d = e - t * dh;
+    const T v = src[(size_t)t * src_ld + d];
+    if (transpose) dst[d * ld + t] = v;
+    else dst[t * ld + d] = v;
   }
 }
 
-template <typename T>
-__global__ void __launch_bounds__(256)
+template <typename T, int TB>
+__global__ void __launch_bounds__(64)
+attn_fwd_kernel(int B, int Tn, int H, int dh, const T* __restrict__ qkv, const int64_t* __restrict__ amask,
+                T* __restrict__ ctx, float* __restrict__ P, float scale, float p, uint64_t seed) {
+  using G = AttnGeom<T, TB>;
+  using M = AttnMma<T>;
+  __shared__ __attribute__((aligned(16))) T sQ[G::TP * G::LD];
+  __shared__ __attribute__((aligned(16))) T sK[G::TP * G::LD];
+  __shared__ __attribute__((aligned(16))) T sVt[32 * G::LT];   // V^T: [d][j]
+  __shared__ __attribute__((aligned(16))) T sP[G::TP * G::LT];  // P': [i][j]
+  const int b = blockIdx.x / H, h = blockIdx.x - (blockIdx.x / H) * H;
+  const int Dm = H * dh;
+  const size_t ld = 3 * (size_t)Dm;
+  const int l = threadIdx.x & 63, li = l & 15, lg = l >> 4;
+  zero_lds(sQ, G::TP * G::LD);
+  zero_lds(sK, G::TP * G::LD);
+  zero_lds(sVt, 32 * G::LT);
+  zero_lds(sP, G::TP * G::LT);
+  __syncthreads();
+  const T* base = qkv + (size_t)b * Tn * ld + h * dh;
+  load_head(sQ, G::LD, false, base, ld, Tn, dh);
+  load_head(sK, G::LD, false, base + Dm, ld, Tn, dh);
+  load_head(sVt, G::LT, true, base + 2 * Dm, ld, Tn, dh);
+  __syncthreads();
+  // key bias per lane: keys j = jb*16 + 4*lg + r
+  float kb[TB][4];
+#pragma unroll
+  for (int jb = 0; jb < TB; ++jb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = jb * 16 + 4 * lg + r;
+      kb[jb][r] = j >= Tn ? -INFINITY : (amask && amask[(size_t)b * Tn + j] == 0 ? -3.402823466e38f : 0.f);
+    }
+#pragma unroll
+  for (int ib = 0; ib < TB; ++ib) {
+    // S[i][j] for the 16 queries of block ib: lane holds query ib*16 + li, keys 4lg+r of each key block
+    v4f s[TB];
+#pragma unroll
+    for (int jb = 0; jb < TB; ++jb) {
+      s[jb] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k0 = 0; k0 < 32; k0 += M::KS) M::mma(s[jb], sK, G::LD, jb * 16, sQ, G::LD, ib * 16, k0);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int jb = 0; jb < TB; ++jb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s[jb][r] = s[jb][r] * scale + kb[jb][r];
+        mx = fmaxf(mx, s[jb][r]);
+      }
+    mx = q4_max(mx);
+    float sum = 0.f;
+#pragma unroll
+    for (int jb = 0; jb < TB; ++jb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s[jb][r] = __expf(s[jb][r] - mx);
+        sum += s[jb][r];
+      }
+    const float inv = 1.f / q4_sum(sum);
+    const int i = ib * 16 + li;
+#pragma unroll
+    for (int jb = 0; jb < TB; ++jb) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = jb * 16 + 4 * lg + r;
+        float pr = s[jb][r] * inv;
+        if (i < Tn && j < Tn) {
+          P[(((size_t)b * H + h) * Tn + i) * Tn + j] = pr;
+          if (p > 0.f) pr *= drop_scale(seed, (((uint64_t)b * H + h) * Tn + i) * Tn + j, p);
+        } else {
+          pr = 0.f;
+        }
+        sP[i * G::LT + j] = from_f<T>(pr);
+      }
+    }
+  }
+  __syncthreads();
+  // ctx[i][d] = sum_j P'[i][j] V[j][d]: X = V^T (rows d), Y = P' (rows i)
+#pragma unroll
+  for (int ib = 0; ib < TB; ++ib) {
+    const int i = ib * 16 + li;
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      v4f o = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k0 = 0; k0 < G::TK; k0 += M::KS) M::mma(o, sVt, G::LT, db * 16, sP, G::LT, ib * 16, k0);
+      if (i < Tn) {
+        T* dst = ctx + ((size_t)b * Tn + i) * Dm + h * dh;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int d = db * 16 + 4 * lg + r;
+          if (d < dh) dst[d] = from_f<T>(o[r]);
+        }
+      }
+    }
+  }
+}
+
+// Backward of attn_fwd_kernel, one wave per (b, h):
+//   dP' = dctx V^T ; dP = dP' * dropout mask ; dS = P (dP - rowsum(P dP))
+//   dq = scale * dS K ;  dk = scale * dS^T Q ;  dv = P'^T dctx
+template <typename T, int TB>
+__global__ void __launch_bounds__(64)
 attn_bwd_kernel(int B, int Tn, int H, int dh, const T* __restrict__ qkv, const float* __restrict__ P,
                 const T* __restrict__ dctx, T* __restrict__ dqkv, float scale, float p, uint64_t seed) {
-  __shared__ float q[kMaxT][kMaxDh + 1], k[kMaxT][kMaxDh + 1], v[kMaxT][kMaxDh + 1];
-  __shared__ float dc[kMaxT][kMaxDh + 1];
-  __shared__ float Pd[kMaxT][kMaxT + 1], dS[kMaxT][kMaxT + 1];
-  const int b = blockIdx.x / H, h = blockIdx.x % H;
-  const int Dm = H * dh, ld = 3 * Dm;
-  for (int e = threadIdx.x; e < Tn * dh; e += blockDim.x) {
-    int t = e / dh, d = e % dh;
-    const T* r = qkv + (size_t)(b * Tn + t) * ld + h * dh + d;
-    q[t][d] = to_f(r[0]);
-    k[t][d] = to_f(r[Dm]);
-    v[t][d] = to_f(r[2 * Dm]);
-    dc[t][d] = to_f(dctx[(size_t)(b * Tn + t) * Dm + h * dh + d]);
-  }
+  using G = AttnGeom<T, TB>;
+  using M = AttnMma<T>;
+  __shared__ __attribute__((aligned(16))) T sV[G::TP * G::LD];     // V: [j][d]
+  __shared__ __attribute__((aligned(16))) T sdO[G::TP * G::LD];    // dctx: [i][d]
+  __shared__ __attribute__((aligned(16))) T sKt[32 * G::LT];       // K^T: [d][j]
+  __shared__ __attribute__((aligned(16))) T sQt[32 * G::LT];       // Q^T: [d][i]
+  __shared__ __attribute__((aligned(16))) T sdOt[32 * G::LT];      // dctx^T: [d][i]
+  __shared__ __attribute__((aligned(16))) T sdS[G::TP * G::LT];    // dS: [i][j]
+  __shared__ __attribute__((aligned(16))) T sdSt[G::TP * G::LT];   // dS^T: [j][i]
+  __shared__ __attribute__((aligned(16))) T sPdt[G::TP * G::LT];   // P'^T: [j][i]
+  const int b = blockIdx.x / H, h = blockIdx.x - (blockIdx.x / H) * H;
+  const int Dm = H * dh;
+  const size_t ld = 3 * (size_t)Dm;
+  const int l = threadIdx.x & 63, li = l & 15, lg = l >> 4;
+  zero_lds(sV, G::TP * G::LD);
+  zero_lds(sdO, G::TP * G::LD);
+  zero_lds(sKt, 32 * G::LT);
+  zero_lds(sQt, 32 * G::LT);
+  zero_lds(sdOt, 32 * G::LT);
+  zero_lds(sdS, G::TP * G::LT);
+  zero_lds(sdSt, G::TP * G::LT);
+  zero_lds(sPdt, G::TP * G::LT);
+  __syncthreads();
+  const T* base = qkv + (size_t)b * Tn * ld + h * dh;
+  const T* dbase = dctx + (size_t)b * Tn * Dm + h * dh;
+  load_head(sQt, G::LT, true, base, ld, Tn, dh);
+  load_head(sKt, G::LT, true, base + Dm, ld, Tn, dh);
+  load_head(sV, G::LD, false, base + 2 * Dm, ld, Tn, dh);
+  load_head(sdO, G::LD, false, dbase, Dm, Tn, dh);
+  load_head(sdOt, G::LT, true, dbase, Dm, Tn, dh);
+  __syncthreads();
   const float* Pb = P + ((size_t)b * H + h) * Tn * Tn;
-  __syncthreads();
-  // dPd = dctx . v^T ; dP = dPd * mask ; keep Pd = P * mask for dv
-  for (int e = threadIdx.x; e < Tn * Tn; e += blockDim.x) {
-    int i = e / Tn, j = e % Tn;
-    float s = 0.f;
-    for (int d = 0; d < dh; ++d) s += dc[i][d] * v[j][d];
-    float m = p > 0.f ? drop_scale(seed, (((uint64_t)b * H + h) * Tn + i) * Tn + j, p) : 1.f;
-    dS[i][j] = s * m;
-    Pd[i][j] = Pb[e] * m;
-  }
-  __syncthreads();
-  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
-  for (int i = wv; i < Tn; i += 4) {
-    float pr = l < Tn ? Pb[i * Tn + l] : 0.f;
-    float dp = l < Tn ? dS[i][l] : 0.f;
-    float dot = warp_sum(pr * dp);
-    if (l < Tn) dS[i][l] = pr * (dp - dot);
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < Tn * dh; e += blockDim.x) {
-    int t = e / dh, d = e % dh;
-    float sq = 0.f, sk = 0.f, sv = 0.f;
-    for (int j = 0; j < Tn; ++j) {
-      sq += dS[t][j] * k[j][d];
-      sk += dS[j][t] * q[j][d];
-      sv += Pd[j][t] * dc[j][d];
+#pragma unroll
+  for (int ib = 0; ib < TB; ++ib) {
+    const int i = ib * 16 + li;
+    // dP'[i][j] = sum_d dO[i][d] V[j][d]: X = V (rows j), Y = dO (rows i)
+    v4f dp[TB];
+#pragma unroll
+    for (int jb = 0; jb < TB; ++jb) {
+      dp[jb] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k0 = 0; k0 < 32; k0 += M::KS) M::mma(dp[jb], sV, G::LD, jb * 16, sdO, G::LD, ib * 16, k0);
     }
-    T* r = dqkv + (size_t)(b * Tn + t) * ld + h * dh + d;
-    r[0] = from_f<T>(sq * scale);
-    r[Dm] = from_f<T>(sk * scale);
-    r[2 * Dm] = from_f<T>(sv);
+    float pr[TB][4], pd[TB][4];
+    float dot = 0.f;
+#pragma unroll
+    for (int jb = 0; jb < TB; ++jb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = jb * 16 + 4 * lg + r;
+        const bool ok = i < Tn && j < Tn;
+        const float m = (ok && p > 0.f) ? drop_scale(seed, (((uint64_t)b * H + h) * Tn + i) * Tn + j, p) : 1.f;
+        pr[jb][r] = ok ? Pb[(size_t)i * Tn + j] : 0.f;
+        pd[jb][r] = pr[jb][r] * m;        // P' (what multiplied V)
+        dp[jb][r] *= m;                   // dP
+        dot += pr[jb][r] * dp[jb][r];
+      }
+    dot = q4_sum(dot);
+#pragma unroll
+    for (int jb = 0; jb < TB; ++jb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = jb * 16 + 4 * lg + r;
+        const float ds = pr[jb][r] * (dp[jb][r] - dot);
+        sdS[i * G::LT + j] = from_f<T>(ds);
+        sdSt[j * G::LT + i] = from_f<T>(ds);
+        sPdt[j * G::LT + i] = from_f<T>(pd[jb][r]);
+      }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int nb = 0; nb < TB; ++nb) {
+    const int t = nb * 16 + li;
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      v4f dq = v4f{0.f, 0.f, 0.f, 0.f}, dk = dq, dv = dq;
+#pragma unroll
+      for (int k0 = 0; k0 < G::TK; k0 += M::KS) {
+        M::mma(dq, sKt, G::LT, db * 16, sdS, G::LT, nb * 16, k0);     // dq[t=i][d]
+        M::mma(dk, sQt, G::LT, db * 16, sdSt, G::LT, nb * 16, k0);    // dk[t=j][d]
+        M::mma(dv, sdOt, G::LT, db * 16, sPdt, G::LT, nb * 16, k0);   // dv[t=j][d]
+      }
+      if (t < Tn) {
+        T* r0 = dqkv + ((size_t)b * Tn + t) * ld + h * dh;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int d = db * 16 + 4 * lg + r;
+          if (d < dh) {
+            r0[d] = from_f<T>(dq[r] * scale);
+            r0[Dm + d] = from_f<T>(dk[r] * scale);
+            r0[2 * Dm + d] = from_f<T>(dv[r]);
+          }
+        }
+      }
+    }
   }
 }
 
@@ -373,6 +554,9 @@ __global__ void embed_bwd_kernel(int M, int Tn, int D, const int64_t* __restrict
                                  const T* __restrict__ de, float* dwemb) {
   const int row = blockIdx.x;
   const int64_t id = ids[row];
+  // nn.Embedding(vocab, hidden, padding_idx=pad_token_id = 0) (BertEmbeddings): the
+  // padding row never receives a gradient
+  if (id == 0) return;
   for (int c = threadIdx.x; c < D; c += blockDim.x)
     atomicAdd(dwemb + (size_t)id * D + c, to_f(de[(size_t)row * D + c]));
 }
@@ -559,31 +743,48 @@ VLP_EXPORT int vlp_layernorm_bwd(int dtype, int M, int D, const void* dy, float 
   return (int)hipGetLastError();
 }
 
+template <typename T, int TB>
+static void launch_attn_fwd(int B, int Tn, int H, int dh, const void* qkv, const long long* amask, void* ctx,
+                            float* P, float scale, float p, unsigned long long seed, hipStream_t st) {
+  hipLaunchKernelGGL((attn_fwd_kernel<T, TB>), dim3(B * H), dim3(64), 0, st, B, Tn, H, dh, (const T*)qkv,
+                     (const int64_t*)amask, (T*)ctx, P, scale, p, (uint64_t)seed);
+}
+template <typename T, int TB>
+static void launch_attn_bwd(int B, int Tn, int H, int dh, const void* qkv, const float* P, const void* dctx,
+                            void* dqkv, float scale, float p, unsigned long long seed, hipStream_t st) {
+  hipLaunchKernelGGL((attn_bwd_kernel<T, TB>), dim3(B * H), dim3(64), 0, st, B, Tn, H, dh, (const T*)qkv, P,
+                     (const T*)dctx, (T*)dqkv, scale, p, (uint64_t)seed);
+}
+
 VLP_EXPORT int vlp_attn_fwd(int dtype, int B, int Tn, int H, int dh, const void* qkv,
                             const long long* amask, void* ctx, float* P, float scale, float p,
                             unsigned long long seed, void* stream) {
-  if (Tn > kMaxT || dh > kMaxDh) return (int)hipErrorInvalidValue;
+  if (Tn < 1 || Tn > kMaxT || dh < 1 || dh > kMaxDh || B < 1 || H < 1) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == VLP_BF16)
-    hipLaunchKernelGGL(attn_fwd_kernel<bf16>, dim3(B * H), dim3(256), 0, st, B, Tn, H, dh,
-                       (const bf16*)qkv, (const int64_t*)amask, (bf16*)ctx, P, scale, p, seed);
-  else
-    hipLaunchKernelGGL(attn_fwd_kernel<float>, dim3(B * H), dim3(256), 0, st, B, Tn, H, dh,
-                       (const float*)qkv, (const int64_t*)amask, (float*)ctx, P, scale, p, seed);
+  const bool small = Tn <= 48;
+  if (dtype == VLP_BF16) {
+    if (small) launch_attn_fwd<bf16, 3>(B, Tn, H, dh, qkv, amask, ctx, P, scale, p, seed, st);
+    else launch_attn_fwd<bf16, 4>(B, Tn, H, dh, qkv, amask, ctx, P, scale, p, seed, st);
+  } else {
+    if (small) launch_attn_fwd<float, 3>(B, Tn, H, dh, qkv, amask, ctx, P, scale, p, seed, st);
+    else launch_attn_fwd<float, 4>(B, Tn, H, dh, qkv, amask, ctx, P, scale, p, seed, st);
+  }
   return (int)hipGetLastError();
 }
 
 VLP_EXPORT int vlp_attn_bwd(int dtype, int B, int Tn, int H, int dh, const void* qkv, const float* P,
                             const void* dctx, void* dqkv, float scale, float p,
                             unsigned long long seed, void* stream) {
-  if (Tn > kMaxT || dh > kMaxDh) return (int)hipErrorInvalidValue;
+  if (Tn < 1 || Tn > kMaxT || dh < 1 || dh > kMaxDh || B < 1 || H < 1) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == VLP_BF16)
-    hipLaunchKernelGGL(attn_bwd_kernel<bf16>, dim3(B * H), dim3(256), 0, st, B, Tn, H, dh,
-                       (const bf16*)qkv, P, (const bf16*)dctx, (bf16*)dqkv, scale, p, seed);
-  else
-    hipLaunchKernelGGL(attn_bwd_kernel<float>, dim3(B * H), dim3(256), 0, st, B, Tn, H, dh,
-                       (const float*)qkv, P, (const float*)dctx, (float*)dqkv, scale, p, seed);
+  const bool small = Tn <= 48;
+  if (dtype == VLP_BF16) {
+    if (small) launch_attn_bwd<bf16, 3>(B, Tn, H, dh, qkv, P, dctx, dqkv, scale, p, seed, st);
+    else launch_attn_bwd<bf16, 4>(B, Tn, H, dh, qkv, P, dctx, dqkv, scale, p, seed, st);
+  } else {
+    if (small) launch_attn_bwd<float, 3>(B, Tn, H, dh, qkv, P, dctx, dqkv, scale, p, seed, st);
+    else launch_attn_bwd<float, 4>(B, Tn, H, dh, qkv, P, dctx, dqkv, scale, p, seed, st);
+  }
   return (int)hipGetLastError();
 }
 

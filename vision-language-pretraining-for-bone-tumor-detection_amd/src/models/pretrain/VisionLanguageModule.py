@@ -480,7 +480,9 @@ class VisionLanguageModule(_Base):
                 raise ValueError(f"Invalid mode: {mode}. Supported modes are: 'entire', 'validation'.")
             for batch in all_batches:
                 labels = batch["tumor"].to(device=self.device, dtype=torch.int64)
-                f = self.image_encoder(batch["x-ray"].to(self.device))
+                x = batch["x-ray"] if "x-ray" in batch else batch["x-ray-u8"]   # u8: on-device normalise
+                self.image_encoder.model.u8_norm = tuple(batch.get("x-ray-u8-norm", (127.5, 73.9)))
+                f = self.image_encoder(x.to(self.device))
                 e = _EmbedFn.apply(self._head, f, "image_projection", self.image_projection)
                 emb.append(e)
                 labs.append(labels)

@@ -141,7 +141,7 @@ def train(cfg: Dict[str, Any]) -> Tuple[Dict[str, Any], Dict[str, Any]]:
                 ds = instantiate(cfg["downstream_data"])
                 model = type(model).load_from_checkpoint(ck.best_model_path, downstream_datamodule=ds,
                                                          device=model.device)
-                objects["model"] = model
+                objects["best_model"] = model   # objects["model"] stays the trained module, as in the reference
             else:
                 log.warning("Train: No best model path found in trainer, using current model weights.")
             if getattr(model, "downstream_datamodule", None) is not None:
