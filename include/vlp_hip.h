@@ -109,6 +109,24 @@ int vlp_stem_wgrad_ws(int dtype, const void* dy, const void* xp, float* split_ws
                       int* nsplit, int N, int H, int W, void* stream);
 int vlp_stem_wgrad_fold(int nsplit, const float* split_ws, float* grad, void* stream);
 
+/* single-channel stem for the 1-channel uint8 upload (the reference replicates
+ * the grayscale radiograph to 3 identical channels, PretrainDataModule.py:167-171,
+ * so conv1 = a 1-channel 7x7/2 conv with the channel-summed weights: K = 64
+ * instead of 256).  Image: 4 copies shifted by 0/2/4/6 pixels,
+ * xs[4][N][Hp][Wp1] (vlp_stem1_geom; returns non-zero when Wo % 4 != 0, then the
+ * caller uses the 3-channel path); weights W1[64][8][8] (vlp_pack_stem1);
+ * vlp_stem1_wgrad_ws + vlp_stem1_wgrad_fold give the [64][3][7][7] gradient
+ * (identical for the three channels). */
+int vlp_stem1_geom(int H, int W, int* Ho, int* Wo, int* Hp, int* Wp1);
+int vlp_stem1_prep_u8(int dtype, const uint8_t* x_u8, void* xs, int N, int H, int W, float mean, float std,
+                      void* stream);
+int vlp_pack_stem1(int dtype, const float* w, void* wp, void* stream);
+int vlp_stem1_fwd(int dtype, const void* xs, const void* wp, void* y, int N, int H, int W,
+                  double* stat_sum, double* stat_sumsq, int stat_rep, void* stream);
+int vlp_stem1_wgrad_ws(int dtype, const void* dy, const void* xs, float* split_ws, long long ws_floats,
+                       int* nsplit, int N, int H, int W, void* stream);
+int vlp_stem1_wgrad_fold(int nsplit, const float* split_ws, float* grad, void* stream);
+
 /* ---------------- image tower: BatchNorm / residual / pooling ----------------
  * Replace timm resnet34's BatchNorm2d (train-mode batch statistics), ReLU,
  * residual add, maxpool 3x3/2 and global average pool (VisionLanguageModule.py:30-35).

@@ -531,3 +531,44 @@ def test_maxpool_bwd_sums_and_apply(ops, dt, H, W):
                                                                  * mu.double())
     tol = 2e-2 if dt == torch.bfloat16 else 1e-4
     assert torch.allclose(dy.double().cpu(), ref, rtol=tol, atol=tol * ref.abs().max().item())
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("N,H,W", [(2, 32, 32), (3, 48, 64), (8, 128, 128), (2, 224, 224)])
+def test_stem1_single_channel_fwd_wgrad(ops, dt, N, H, W):
+    """The single-channel stem of the uint8 upload (K = 64, channel-summed weights,
+    4 shifted image copies) equals torch's 3-channel conv on the replicated
+    normalised image, forward (+ BN sums) and the [64][3][7][7] weight gradient
+    through the split slabs (N = 8, 128^2: 32768 output pixels, many splits)."""
+    g = torch.Generator().manual_seed(H + N)
+    mean, std = 127.5, 73.9
+    x8 = torch.randint(0, 256, (N, 1, H, W), generator=g, dtype=torch.uint8)
+    x = ((x8.float() - mean) / std).to(dt).float().repeat(1, 3, 1, 1)
+    w = (torch.randn(64, 3, 7, 7, generator=g) * 0.1).requires_grad_()
+    y = F.conv2d(x, w, stride=2, padding=3)
+    dy = torch.randn(y.shape, generator=g).to(dt).float()
+    y.backward(dy)
+    Ho, Wo, Hp, Wp1 = ops.stem1_geom(H, W)
+    assert (Ho, Wo) == tuple(y.shape[2:])
+    xs = torch.full((4, N, Hp, Wp1), float("nan"), device="cuda").to(dt)   # the prep writes every element
+    ops.stem1_prep_u8(x8.cuda(), xs, mean, std)
+    wp1 = torch.empty(64, 64, dtype=dt, device="cuda")
+    ops.pack_stem1(w.detach().cuda(), wp1)
+    yd = torch.empty(N, Ho, Wo, 64, dtype=dt, device="cuda")
+    s1 = torch.zeros(64, dtype=torch.float64, device="cuda")
+    s2 = torch.zeros_like(s1)
+    ops.stem1_fwd(xs, wp1, N, H, W, yd, s1, s2)
+    gw = torch.full((64, 3, 7, 7), float("nan"), device="cuda")
+    ops.stem1_wgrad_into(nhwc(dy).to(dt).cuda(), xs, N, H, W, gw)
+    torch.cuda.synchronize()
+    assert not torch.isnan(xs.float()).any()
+    assert rel(nchw(yd.float().cpu()), y.detach()) < tol(dt)
+    assert rel(s1.cpu(), y.detach().sum((0, 2, 3))) < tol(dt)
+    assert rel(s2.cpu(), (y.detach() ** 2).sum((0, 2, 3))) < tol(dt)
+    assert rel(gw.cpu(), w.grad) < tol(dt) / 2, rel(gw.cpu(), w.grad)
+    assert torch.equal(gw[:, 0], gw[:, 1]) and torch.equal(gw[:, 0], gw[:, 2])
+
+
+def test_stem1_geom_rejects_unaligned(ops):
+    assert ops.stem1_geom(100, 100) is None        # Wo = 50: the 3-channel path takes it
+    assert ops.stem1_geom(512, 512) == (256, 256, 518, 520)

@@ -1,0 +1,16 @@
+# build a variant of libvlp_hip.so with extra -D flags into build_exp/<name>/libvlp_hip.so
+#   tools/build_variant.sh NAME "-DVLP_BIG_SCHED=1 ..."
+set -e
+NAME=$1; FLAGS=$2
+ROOT=$(cd $(dirname $0)/.. && pwd)
+CSRC=$ROOT/vision-language-pretraining-for-bone-tumor-detection_amd/csrc
+OUT=$ROOT/build_exp/$NAME
+mkdir -p $OUT/obj
+for f in conv_ops bn_ops bert_ops head_ops optim_ops probe_ops retrieval_ops; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -fvisibility=hidden \
+    -Wno-unused-result $FLAGS -c $CSRC/$f.hip -o $OUT/obj/$f.o &
+done
+wait
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $OUT/libvlp_hip.so $OUT/obj/*.o
+rm -rf $OUT/obj
+echo built $OUT/libvlp_hip.so

@@ -701,6 +701,127 @@ static PixStep make_stem_pixstep(const StemGeom& g, int BK) {
   return p;
 }
 
+// ---- single-channel stem (the grayscale radiograph's 3 identical channels) ----
+// conv(x replicated to 3 channels, w) = conv(x, w1) with w1 = sum_c w[:, c]: a
+// K = (kh:8, kw:8) = 64 GEMM instead of the 4-channel K = 256 one.  A 16-B chunk
+// (8 bf16 / 4 fp32) is 8 (4) consecutive kw of one kh; to keep every chunk 16-B
+// aligned for LDS-DMA the padded image is stored in 4 copies shifted by 0, 2, 4,
+// 6 pixels: output column wo reads copy s = wo & 3 at column 2wo - 2s (a multiple
+// of 8).  Xs[s][n][Hp][Wp1], Wp1 = round8(2Wo + 8), zero outside the image.
+// Requires Wo % 4 == 0 (then s is constant along the pixel walk of a K-step).
+struct Stem1Geom {
+  int N, Ho, Wo, Hp, Wp1, M;
+  size_t copy;   // elements per shifted copy
+  FastDiv fd_howo, fd_wo;
+};
+template <typename T>
+struct Stem1A {
+  static constexpr bool kKContig = true;
+  static constexpr bool kDirect = false;
+  Stem1Geom g; const T* xs;
+  struct State { const T* base; bool ok; };
+  __device__ size_t pix(int m) const {   // element offset of (copy, n, 2ho, 2wo - 2s)
+    const int n = fdiv(m, g.fd_howo);
+    const int r = m - n * g.Ho * g.Wo;
+    const int ho = fdiv(r, g.fd_wo);
+    const int wo = r - ho * g.Wo;
+    const int sh = wo & 3;
+    return (size_t)sh * g.copy + ((size_t)n * g.Hp + 2 * ho) * g.Wp1 + 2 * wo - 2 * sh;
+  }
+  __device__ State fixed(int m) const {
+    State s;
+    s.ok = m < g.M;
+    s.base = xs + pix(s.ok ? m : 0);
+    return s;
+  }
+  __device__ uint4 load(const State& s, int k) const {   // k = kh * 8 + kw0
+    const int kh = k >> 3, kw = k & 7;
+    if (!s.ok || kh >= 7) return zero4();
+    return ldg16(s.base + (size_t)kh * g.Wp1 + kw);
+  }
+  static constexpr bool kBuf = true;
+  struct BState { unsigned base; int khlim; };
+  struct BStep { unsigned delta; int kh; };
+  __device__ rsrc_t rsrc() const { return buf_rsrc(xs, (unsigned)(4 * g.copy * sizeof(T))); }
+  __device__ BState bstart(int m, int koff, int) const {
+    const bool ok = m < g.M;
+    const size_t e = pix(ok ? m : 0) + (size_t)(koff >> 3) * g.Wp1;
+    return BState{(unsigned)(e * sizeof(T)), ok ? 7 - (koff >> 3) : -1000};
+  }
+  __device__ BStep bstep(int k0) const { return BStep{(unsigned)((size_t)(k0 >> 3) * g.Wp1 * sizeof(T)), k0 >> 3}; }
+  __device__ unsigned boff(BState& s, const BStep& st) const { return st.kh < s.khlim ? s.base + st.delta : kOOB; }
+};
+template <typename T>
+struct Stem1WgradB {   // B(n = kh*8 + kw, k = pixel m), MN-contiguous chunks of 8 (4) kw
+  static constexpr bool kKContig = false;
+  static constexpr bool kDirect = false;
+  Stem1Geom g; const T* xs;
+  struct State { int off; bool ok; };
+  __device__ State fixed(int col) const { return State{(col >> 3) * g.Wp1 + (col & 7), (col >> 3) < 7}; }
+  __device__ uint4 load(const State& s, int m) const {
+    if (!s.ok || m >= g.M) return zero4();
+    const int n = fdiv(m, g.fd_howo);
+    const int r = m - n * g.Ho * g.Wo;
+    const int ho = fdiv(r, g.fd_wo);
+    const int wo = r - ho * g.Wo;
+    const int sh = wo & 3;
+    return ldg16(xs + (size_t)sh * g.copy + ((size_t)n * g.Hp + 2 * ho) * g.Wp1 + 2 * wo - 2 * sh + s.off);
+  }
+  static constexpr bool kBuf = true;
+  PixStep ps;   // deltas in elements of one copy (make_stem1_pixstep)
+  struct BRow { unsigned poff; int ho, wo, mm; };
+  typedef unsigned BCol;
+  __device__ rsrc_t rsrc() const { return buf_rsrc(xs, (unsigned)(4 * g.copy * sizeof(T))); }
+  __device__ void blocate(BRow& r) const {
+    const int m = r.mm < g.M ? r.mm : 0;
+    const int n = fdiv(m, g.fd_howo);
+    const int rr = m - n * g.Ho * g.Wo;
+    r.ho = fdiv(rr, g.fd_wo);
+    r.wo = rr - r.ho * g.Wo;
+    const int sh = r.wo & 3;
+    r.poff = (unsigned)(((size_t)sh * g.copy + ((size_t)n * g.Hp + 2 * r.ho) * g.Wp1 + 2 * r.wo - 2 * sh) * sizeof(T));
+  }
+  __device__ BRow brstart(int k, int kb) const {
+    BRow r;
+    r.mm = kb + k;
+    blocate(r);
+    return r;
+  }
+  __device__ BCol bcstart(int col) const {
+    const State f = fixed(col);
+    return f.ok ? (unsigned)(f.off * (int)sizeof(T)) : kOOB;
+  }
+  __device__ unsigned boff(const BRow& r, const BCol& c) const { return r.mm < g.M ? r.poff + c : kOOB; }
+  __device__ void bradvance(BRow& r) const {
+    r.mm += Elem<T>::BK;
+    if (ps.small) {
+      blocate(r);
+      return;
+    }
+    // Wo % 4 == 0 and BK % 4 == 0: the copy index (wo & 3) never changes along the walk
+    r.wo += ps.dwo;
+    r.ho += ps.dho;
+    r.poff += ps.dpoff * (int)sizeof(T);
+    const bool cw = r.wo >= g.Wo;
+    r.wo = cw ? r.wo - g.Wo : r.wo;
+    r.ho = cw ? r.ho + 1 : r.ho;
+    r.poff = cw ? r.poff + ps.carry_w * (int)sizeof(T) : r.poff;
+    const bool ch = r.ho >= g.Ho;
+    r.ho = ch ? r.ho - g.Ho : r.ho;
+    r.poff = ch ? r.poff + ps.carry_h * (int)sizeof(T) : r.poff;
+  }
+};
+static PixStep make_stem1_pixstep(const Stem1Geom& g, int BK) {
+  PixStep p;
+  p.small = g.Ho * g.Wo <= BK;
+  p.dho = BK / g.Wo;
+  p.dwo = BK % g.Wo;
+  p.dpoff = p.dwo * 2 + p.dho * 2 * g.Wp1;
+  p.carry_w = 2 * g.Wp1 - 2 * g.Wo;                  // wo -= Wo, ho += 1
+  p.carry_h = g.Hp * g.Wp1 - 2 * g.Ho * g.Wp1;       // ho -= Ho, n += 1
+  return p;
+}
+
 typedef const __attribute__((address_space(3))) float* lds_fp;
 template <class E, class = void> struct CoefTrait { static constexpr int value = 0; };
 template <class E> struct CoefTrait<E, std::void_t<decltype(E::kCoefs)>> { static constexpr int value = E::kCoefs; };
@@ -1468,6 +1589,85 @@ __global__ void stem_prep_u8_kernel(const uint8_t* __restrict__ x, T* __restrict
   }
 }
 
+static Stem1Geom make_stem1(int N, int H, int W) {
+  Stem1Geom g;
+  g.N = N;
+  g.Ho = (H + 6 - 7) / 2 + 1;
+  g.Wo = (W + 6 - 7) / 2 + 1;
+  g.Hp = 2 * g.Ho + 6;
+  g.Wp1 = (2 * g.Wo + 8 + 7) / 8 * 8;
+  g.M = N * g.Ho * g.Wo;
+  g.copy = (size_t)N * g.Hp * g.Wp1;
+  g.fd_howo = make_fastdiv(g.Ho * g.Wo);
+  g.fd_wo = make_fastdiv(g.Wo);
+  return g;
+}
+// uint8 [N][1][H][W] -> normalised single-channel padded image in 4 shifted copies
+// (Xs[s][n][h][j] = Xpad[n][h][j + 2s], Xpad = the image at (3, 3), zeros around);
+// one thread per 8 output elements, every element written (no pre-zeroing)
+template <typename T>
+__global__ void stem1_prep_u8_kernel(const uint8_t* __restrict__ x, T* __restrict__ xs, Stem1Geom g, int H, int W,
+                                     float mean, float inv_std) {
+  const size_t rows = 4 * (size_t)g.N * g.Hp;
+  const int cpr = g.Wp1 / 8;
+  const size_t total = rows * cpr;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % cpr);
+    const size_t row = i / cpr;
+    const int hp = (int)(row % g.Hp);
+    const size_t t = row / g.Hp;
+    const int n = (int)(t % g.N), sh = (int)(t / g.N);
+    const int h = hp - 3;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int w = c * 8 + j + 2 * sh - 3;
+      v[j] = (h >= 0 && h < H && w >= 0 && w < W) ? ((float)x[((size_t)n * H + h) * W + w] - mean) * inv_std : 0.f;
+    }
+    T* dst = xs + row * g.Wp1 + c * 8;
+    if constexpr (sizeof(T) == 2) {
+      stg16(dst, Chunk<bf16>::pack(v));
+    } else {
+      stg16(dst, Chunk<float>::pack(v));
+      stg16(dst + 4, Chunk<float>::pack(v + 4));
+    }
+  }
+}
+// stem [64][3][7][7] -> W1[64][kh:8][kw:8] = sum over the 3 channels (zeros outside)
+template <typename T>
+__global__ void pack_stem1_kernel(const float* __restrict__ w, T* __restrict__ wp) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 64 * 64) return;
+  const int co = i >> 6, kh = (i >> 3) & 7, kw = i & 7;
+  float v = 0.f;
+  if (kh < 7 && kw < 7)
+    v = w[((co * 3 + 0) * 7 + kh) * 7 + kw] + w[((co * 3 + 1) * 7 + kh) * 7 + kw] + w[((co * 3 + 2) * 7 + kh) * 7 + kw];
+  wp[i] = from_f<T>(v);
+}
+// slabs [ks][64][64] of d/dW1 -> the parameter's [64][3][7][7] gradient: the three
+// channels carry identical images, so each receives the same gradient
+__global__ void __launch_bounds__(256) stem1_wgrad_fold_kernel(int ks, const float* __restrict__ ws,
+                                                               float* __restrict__ g) {
+  __shared__ float part[4][64];
+  const int e = blockIdx.x * 64 + (threadIdx.x & 63), grp = threadIdx.x >> 6;   // e < 64 * 64
+  const float* p = ws + e;
+  float a0 = 0.f, a1 = 0.f;
+  int s = grp;
+  for (; s + 4 < ks; s += 8) { a0 += p[(size_t)s * 64 * 64]; a1 += p[(size_t)(s + 4) * 64 * 64]; }
+  if (s < ks) a0 += p[(size_t)s * 64 * 64];
+  part[grp][threadIdx.x & 63] = a0 + a1;
+  __syncthreads();
+  if (grp == 0) {
+    const int co = e >> 6, kh = (e >> 3) & 7, kw = e & 7;
+    if (kh < 7 && kw < 7) {
+      const int l = threadIdx.x & 63;
+      const float v = (part[0][l] + part[1][l]) + (part[2][l] + part[3][l]);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) g[((co * 3 + c) * 7 + kh) * 7 + kw] = v;
+    }
+  }
+}
+
 }  // namespace vlp
 
 using namespace vlp;
@@ -1671,4 +1871,91 @@ VLP_EXPORT int vlp_stem_wgrad(int dtype, const void* dy, const void* xp, float* 
   MNMat<float> la{(const float*)dy, 64, 64, g.M};
   StemWgradB<float> lb{g, (const float*)xp, make_stem_pixstep(g, Elem<float>::BK)};
   return gemm_wgrad<float>(64, 224, g.M, la, lb, ep, st);
+}
+
+// ---------------- single-channel stem (Stem1*) ----------------
+VLP_EXPORT int vlp_stem1_geom(int H, int W, int* Ho, int* Wo, int* Hp, int* Wp1) {
+  Stem1Geom g = make_stem1(1, H, W);
+  *Ho = g.Ho; *Wo = g.Wo; *Hp = g.Hp; *Wp1 = g.Wp1;
+  return g.Wo % 4 == 0 ? 0 : (int)hipErrorInvalidValue;   // the shifted-copy walk needs Wo % 4 == 0
+}
+
+VLP_EXPORT int vlp_stem1_prep_u8(int dtype, const uint8_t* x, void* xs, int N, int H, int W, float mean, float std,
+                                 void* stream) {
+  Stem1Geom g = make_stem1(N, H, W);
+  if (g.Wo % 4 || 4 * g.copy * (dtype == VLP_BF16 ? 2 : 4) >= (1ull << 31)) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  const size_t total = 4 * g.copy / 8;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 65536) blocks = 65536;
+  if (dtype == VLP_BF16)
+    hipLaunchKernelGGL(stem1_prep_u8_kernel<bf16>, dim3(blocks), dim3(256), 0, st, x, (bf16*)xs, g, H, W, mean,
+                       1.f / std);
+  else
+    hipLaunchKernelGGL(stem1_prep_u8_kernel<float>, dim3(blocks), dim3(256), 0, st, x, (float*)xs, g, H, W, mean,
+                       1.f / std);
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_pack_stem1(int dtype, const float* w, void* wp, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == VLP_BF16)
+    hipLaunchKernelGGL(pack_stem1_kernel<bf16>, dim3(16), dim3(256), 0, st, w, (bf16*)wp);
+  else
+    hipLaunchKernelGGL(pack_stem1_kernel<float>, dim3(16), dim3(256), 0, st, w, (float*)wp);
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_stem1_fwd(int dtype, const void* xs, const void* wp, void* y, int N, int H, int W,
+                             double* stat_sum, double* stat_sumsq, int stat_rep, void* stream) {
+  Stem1Geom g = make_stem1(N, H, W);
+  if (g.Wo % 4) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == VLP_BF16) {
+    Stem1A<bf16> la{g, (const bf16*)xs};
+    KMat<bf16> lb{(const bf16*)wp, 64, 64, 64};
+    EpiConvFwd<bf16> ep{stat_sum, stat_sumsq, stat_rep, (bf16*)y, 64};
+    return launch_gemm_bk<256, 64, 4, 1>(g.M, 64, 64, 1, la, lb, ep, st);
+  }
+  Stem1A<float> la{g, (const float*)xs};
+  KMat<float> lb{(const float*)wp, 64, 64, 64};
+  EpiConvFwd<float> ep{stat_sum, stat_sumsq, stat_rep, (float*)y, 64};
+  return launch_gemm<float, 256, 64, 4>(g.M, 64, 64, 1, la, lb, ep, st);
+}
+
+// d/dW1 through per-split fp32 slabs [ks][64][64] (no atomics) -> vlp_stem1_wgrad_fold
+VLP_EXPORT int vlp_stem1_wgrad_ws(int dtype, const void* dy, const void* xs, float* split_ws, long long ws_floats,
+                                  int* nsplit, int N, int H, int W, void* stream) {
+  Stem1Geom g = make_stem1(N, H, W);
+  hipStream_t st = (hipStream_t)stream;
+  if (!nsplit || g.Wo % 4) return (int)hipErrorInvalidValue;
+  const long long slab = 64 * 64;
+  const long long fit = ws_floats / slab;
+  const int max_ks = (int)(fit < 4096 ? fit : 4096);
+  if (max_ks < 1) return (int)hipErrorInvalidValue;
+  EpiSplitStore ep{nullptr, nullptr, split_ws, 64, (size_t)slab};
+  if (dtype != VLP_BF16) {   // fp32 parity mode: split-K with fp32 atomics into slab 0
+    if (hipMemsetAsync(split_ws, 0, slab * sizeof(float), st) != hipSuccess) return (int)hipGetLastError();
+    *nsplit = 1;
+    MNMat<float> la{(const float*)dy, 64, 64, g.M};
+    Stem1WgradB<float> lb{g, (const float*)xs, make_stem1_pixstep(g, Elem<float>::BK)};
+    EpiAtomic epa{nullptr, nullptr, split_ws, 64, 1.0f};
+    return gemm_wgrad<float>(64, 56, g.M, la, lb, epa, st);
+  }
+  int mink = 2048;
+  const int need = (g.M + (max_ks < 512 ? max_ks : 512) - 1) / (max_ks < 512 ? max_ks : 512);
+  if (mink < need) mink = need;
+  Stem1WgradB<bf16> lb{g, (const bf16*)xs, make_stem1_pixstep(g, Elem<bf16>::BK)};
+  MNMat<bf16> la{(const bf16*)dy, 64, 64, g.M};
+  const int r = launch_gemm_bk<64, 64, 1, 4>(64, 56, g.M, -mink, la, lb, ep, st);
+  if (r) return r;
+  *nsplit = last_ksplit();
+  return *nsplit > max_ks ? (int)hipErrorInvalidValue : 0;
+}
+
+VLP_EXPORT int vlp_stem1_wgrad_fold(int nsplit, const float* split_ws, float* grad, void* stream) {
+  if (nsplit < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(stem1_wgrad_fold_kernel, dim3(64 * 64 / 64), dim3(256), 0, (hipStream_t)stream, nsplit,
+                     split_ws, grad);
+  return (int)hipGetLastError();
 }

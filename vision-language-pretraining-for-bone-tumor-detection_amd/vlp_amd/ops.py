@@ -151,6 +151,46 @@ def stem_geom(H, W):
     return a.value, b.value, c.value, d.value
 
 
+def stem1_geom(H, W):
+    """(Ho, Wo, Hp, Wp1) of the single-channel stem, or None when it does not apply
+    (Wo % 4 != 0: the caller takes the 3-channel path)."""
+    import ctypes
+    a, b, c, d = (ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int())
+    r = lib()._dll.vlp_stem1_geom(H, W, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c), ctypes.byref(d))
+    return None if r else (a.value, b.value, c.value, d.value)
+
+
+def stem1_prep_u8(x_u8, xs, mean, std):
+    N, H, W = x_u8.shape[0], x_u8.shape[-2], x_u8.shape[-1]
+    lib().vlp_stem1_prep_u8(dcode(xs), ptr(x_u8), ptr(xs), N, H, W, float(mean), float(std), _s())
+
+
+def pack_stem1(w, wp1):
+    lib().vlp_pack_stem1(dcode(wp1), ptr(w), ptr(wp1), _s())
+
+
+def stem1_fwd(xs, wp1, N, H, W, y, stat_sum, stat_sumsq, stat_rep=1):
+    tk = ktimer.begin("stem_fwd", 2.0 * y.numel() * 147)
+    lib().vlp_stem1_fwd(dcode(xs), ptr(xs), ptr(wp1), ptr(y), N, H, W, ptr(stat_sum), ptr(stat_sumsq),
+                        int(stat_rep), _s())
+    ktimer.end(tk)
+
+
+def stem1_wgrad_into(dy, xs, N, H, W, grad):
+    """grad[64][3][7][7] = stem weight gradient of the single-channel path (overwrites)."""
+    import ctypes
+    ws = _WGRAD_WS.get(dy.device)
+    if ws is None:
+        ws = torch.empty(WGRAD_WS_FLOATS, dtype=torch.float32, device=dy.device)
+        _WGRAD_WS[dy.device] = ws
+    ns = ctypes.c_int(0)
+    tk = ktimer.begin("stem_wgrad", 2.0 * dy.numel() * 147)
+    lib().vlp_stem1_wgrad_ws(dcode(dy), ptr(dy), ptr(xs), ptr(ws), ws.numel(), ctypes.addressof(ns), N, H, W, _s())
+    ktimer.end(tk)
+    lib().vlp_stem1_wgrad_fold(ns.value, ptr(ws), ptr(grad), _s())
+    return grad
+
+
 def stem_prep(x_nchw, xp):
     N, _, H, W = x_nchw.shape
     lib().vlp_stem_prep(dcode(xp), ptr(x_nchw), ptr(xp), N, H, W, _s())

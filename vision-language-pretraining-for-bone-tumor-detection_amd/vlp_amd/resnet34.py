@@ -47,6 +47,8 @@ _USE_DYT = os.environ.get("VLP_WGRAD_DYT", "0") != "0"
 _USE_WG_STREAM = os.environ.get("VLP_WGRAD_STREAM", "0") != "0"
 _WG_STREAMS = {}   # measured: the extra transposed write costs more than it saves
 STAT_REP = 64   # replicas of per-channel fp64 sums (see vlp_stat_reduce)
+# single-channel stem for the uint8 upload (VLP_STEM1=0: always the 3-channel NHWC4 path)
+_USE_STEM1 = os.environ.get("VLP_STEM1", "1") != "0"
 
 
 STAGES = ("stem", "layer1", "layer2", "layer3", "layer4")
@@ -280,22 +282,41 @@ class ResNet34Tower(ArenaModule):
         dev = self.arena.data.device
         src = x if x is not None else x_u8
         N, H, W = src.shape[0], src.shape[-2], src.shape[-1]
-        Ho, Wo, Hp, Wp = ops.stem_geom(H, W)
-        xp_key = ("xp", N, H, W)
-        xp = ws.get(xp_key)
-        if xp is None:
-            xp = torch.zeros(N, Hp, Wp, 4, dtype=T, device=dev)  # padding stays zero
-            ws[xp_key] = xp
-        if x is not None:
-            ops.stem_prep(x.contiguous(), xp)
-        else:
-            ops.stem_prep_u8(x_u8.contiguous(), xp, u8_norm[0], u8_norm[1])
         ws["fstat"].zero_()
-        saved = {"N": N, "H": H, "W": W, "xp": xp, "training": training}
-        # stem
-        y0 = torch.empty(N, Ho, Wo, 64, dtype=T, device=dev)
-        s, ss = self._fstat(ws, "bn1", full=True)
-        ops.stem_fwd(xp, ws["conv1.wp"], N, H, W, y0, s, ss, STAT_REP)
+        # the 1-channel uint8 upload carries ONE grayscale channel (the reference
+        # replicates it 3x, PretrainDataModule.py:167-171): the stem then runs as a
+        # K = 64 single-channel conv with channel-summed weights (vlp_stem1_*)
+        g1 = ops.stem1_geom(H, W) if (x is None and _USE_STEM1) else None
+        if g1 is not None:
+            Ho, Wo, Hp, Wp1 = g1
+            key = ("xs", N, H, W)
+            xs = ws.get(key)
+            if xs is None:
+                xs = torch.empty(4, N, Hp, Wp1, dtype=T, device=dev)   # fully written by the prep
+                ws[key] = xs
+            ops.stem1_prep_u8(x_u8.contiguous(), xs, u8_norm[0], u8_norm[1])
+            if "conv1.wp1" not in ws:
+                ws["conv1.wp1"] = torch.empty(64, 64, dtype=T, device=dev)
+            ops.pack_stem1(self.arena.view("conv1.weight"), ws["conv1.wp1"])
+            saved = {"N": N, "H": H, "W": W, "xs": xs, "training": training}
+            y0 = torch.empty(N, Ho, Wo, 64, dtype=T, device=dev)
+            s, ss = self._fstat(ws, "bn1", full=True)
+            ops.stem1_fwd(xs, ws["conv1.wp1"], N, H, W, y0, s, ss, STAT_REP)
+        else:
+            Ho, Wo, Hp, Wp = ops.stem_geom(H, W)
+            xp_key = ("xp", N, H, W)
+            xp = ws.get(xp_key)
+            if xp is None:
+                xp = torch.zeros(N, Hp, Wp, 4, dtype=T, device=dev)  # padding stays zero
+                ws[xp_key] = xp
+            if x is not None:
+                ops.stem_prep(x.contiguous(), xp)
+            else:
+                ops.stem_prep_u8(x_u8.contiguous(), xp, u8_norm[0], u8_norm[1])
+            saved = {"N": N, "H": H, "W": W, "xp": xp, "training": training}
+            y0 = torch.empty(N, Ho, Wo, 64, dtype=T, device=dev)
+            s, ss = self._fstat(ws, "bn1", full=True)
+            ops.stem_fwd(xp, ws["conv1.wp"], N, H, W, y0, s, ss, STAT_REP)
         sc0, sh0 = self._bn_finalize(ws, "bn1", N * Ho * Wo, training)
         Hq, Wq = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
         p = torch.empty(N, Hq, Wq, 64, dtype=T, device=dev)
@@ -494,7 +515,12 @@ class ResNet34Tower(ArenaModule):
         sg0, sgx0 = sg0f[:64], sgx0f[:64]
         dy0 = torch.empty_like(y0)
         ops.maxpool_bwd_apply(dout, idx, y0, sc0, sh0, mu0, is0, self.arena.view("bn1.weight"), sg0, sgx0, dy0)
-        ops.stem_wgrad_into(dy0, saved["xp"], saved["N"], saved["H"], saved["W"], self.arena.gview("conv1.weight"))
+        if "xs" in saved:
+            ops.stem1_wgrad_into(dy0, saved["xs"], saved["N"], saved["H"], saved["W"],
+                                 self.arena.gview("conv1.weight"))
+        else:
+            ops.stem_wgrad_into(dy0, saved["xp"], saved["N"], saved["H"], saved["W"],
+                                self.arena.gview("conv1.weight"))
         self._stage_done(["layer1", "stem"], on_stage_done, dev)
 
     def _tbuf(self, ws, name, C, M):
