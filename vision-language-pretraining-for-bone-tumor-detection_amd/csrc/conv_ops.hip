@@ -345,6 +345,14 @@ struct EpiS2Remap {
                        float (&s2)[8]) const {
     inner.row8(grow(row), col, v, p, s1, s2);
   }
+  static constexpr int kCoefs = CoefTrait<EP>::value;
+  static constexpr int kPreDepth = PreDepthTrait<EP>::value;
+  __device__ const float* coef(int k) const { return inner.coef(k); }
+  template <int NC>
+  __device__ void row8r(int row, int col, const float (&v)[8], const RowPre& p, float (&s1)[8],
+                        float (&s2)[8], const float (&cf)[NC][8]) const {
+    inner.row8r(grow(row), col, v, p, s1, s2, cf);
+  }
   __device__ void store8(int row, int col, const uint4& u) const { inner.store8(grow(row), col, u); }
 };
 // class B operand: B(ci, k = (a, b, co)) = Wt[ci][kh0 + 2a][kw0 + 2b][co]
@@ -823,8 +831,6 @@ static PixStep make_stem1_pixstep(const Stem1Geom& g, int BK) {
 }
 
 typedef const __attribute__((address_space(3))) float* lds_fp;
-template <class E, class = void> struct CoefTrait { static constexpr int value = 0; };
-template <class E> struct CoefTrait<E, std::void_t<decltype(E::kCoefs)>> { static constexpr int value = E::kCoefs; };
 
 // 8 consecutive per-channel coefficients as two 16-B loads
 __device__ __forceinline__ void ld8f(const float* p, float (&o)[8]) {
@@ -888,6 +894,12 @@ struct EpiDgradBN {
                        float (&s2)[8], lds_fp cf) const {
     row8c(row, col, v, p, s1, s2, cf, cf + 64, cf + 128, cf + 192);
   }
+  static constexpr int kPreDepth = 16;   // one 16-B operand per row chunk
+  __device__ void row8r(int row, int col, const float (&v)[8], const RowPre& p, float (&s1)[8],
+                        float (&s2)[8], const float (&cf)[4][8]) const {
+    row8c(row, col, v, p, s1, s2, RegCoef{cf[0], col}, RegCoef{cf[1], col}, RegCoef{cf[2], col},
+          RegCoef{cf[3], col});
+  }
   template <class FP>
   __device__ void row8c(int row, int col, const float (&v)[8], const RowPre& p, float (&s1)[8],
                         float (&s2)[8], FP csc, FP csh, FP cmu, FP cis) const {
@@ -943,6 +955,7 @@ struct EpiDgradAdd {
   __device__ void pre8(int row, int col, RowPre& p) const {
     if (addend) p.u[0] = ldg16(addend + (size_t)row * C + col);
   }
+  static constexpr int kPreDepth = 16;
   __device__ void row8(int row, int col, const float (&v)[8], const RowPre& p, float (&)[8], float (&)[8]) const {
     const size_t o = (size_t)row * C + col;
     float d[8];
@@ -1024,6 +1037,11 @@ struct EpiDgradRelu {
   __device__ void row8(int row, int col, const float (&v)[8], const RowPre& p, float (&s1)[8],
                        float (&s2)[8], lds_fp cf) const {
     row8c(row, col, v, p, s1, s2, cf, cf + 64);
+  }
+  static constexpr int kPreDepth = BITS ? 8 : 6;
+  __device__ void row8r(int row, int col, const float (&v)[8], const RowPre& p, float (&s1)[8],
+                        float (&s2)[8], const float (&cf)[2][8]) const {
+    row8c(row, col, v, p, s1, s2, RegCoef{cf[0], col}, RegCoef{cf[1], col});
   }
   template <class FP>
   __device__ void row8c(int row, int col, const float (&v)[8], const RowPre& p, float (&s1)[8],

@@ -186,6 +186,20 @@ template <class E> struct RowTrait<E, std::void_t<decltype(E::kRow)>> {
 template <class L> struct DirectTrait<L, std::void_t<decltype(L::kDirect)>> {
   static constexpr bool value = L::kDirect;
 };
+// row-chunk epilogues: per-channel coefficient arrays (E::kCoefs, E::coef(k))
+// and how many row chunks of operands to keep in flight (E::kPreDepth)
+template <class E, class = void> struct CoefTrait { static constexpr int value = 0; };
+template <class E> struct CoefTrait<E, std::void_t<decltype(E::kCoefs)>> { static constexpr int value = E::kCoefs; };
+template <class E, class = void> struct PreDepthTrait { static constexpr int value = 8; };
+template <class E> struct PreDepthTrait<E, std::void_t<decltype(E::kPreDepth)>> {
+  static constexpr int value = E::kPreDepth;
+};
+// a thread's 8 coefficients held in registers, indexed by global column
+// (c[col + j] = p[j]) like the global / LDS coefficient pointers
+struct RegCoef {
+  const float* p; int base;
+  __device__ __forceinline__ float operator[](int i) const { return p[i - base]; }
+};
 
 template <typename T, int BM, class L>
 struct GStager {
@@ -589,27 +603,54 @@ __device__ __forceinline__ void ms_epilogue(const GemmShape& sh, const EP& ep, v
         *reinterpret_cast<v4bf*>(stg + rowl * BN + (((coll >> 3) ^ (rowl & (CPR - 1))) << 3) + (coll & 4)) = ob;
       }
     }
-    __syncthreads();
+    // the thread's operand rows (D chunks ahead) and its 8 columns' per-channel
+    // coefficients are requested while the staged tile settles: the loads of
+    // the row loop overlap each other instead of one round trip per row
+    constexpr int RS = NT / CPR;
+    constexpr int NIT = (BM + RS - 1) / RS;
+    constexpr int D = PreDepthTrait<EP>::value < NIT ? PreDepthTrait<EP>::value : NIT;
+    constexpr int NCF = CoefTrait<EP>::value;
     const int c = threadIdx.x % CPR;
     const int col = col0 + c * 8;
+    const int r0 = threadIdx.x / CPR;
+    const bool cok = col < sh.N;
+    RowPre pre[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      const int r = r0 + i * RS;
+      if (cok && r < BM && row0 + r < sh.M) ep.pre8(row0 + r, col, pre[i]);
+    }
+    float cf[NCF > 0 ? NCF : 1][8];
+    if constexpr (NCF > 0) {
+      if (cok) {
+#pragma unroll
+        for (int k = 0; k < NCF; ++k) {
+          const v4f a = *reinterpret_cast<const v4f*>(ep.coef(k) + col);
+          const v4f b = *reinterpret_cast<const v4f*>(ep.coef(k) + col + 4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { cf[k][j] = a[j]; cf[k][4 + j] = b[j]; }
+        }
+      }
+    }
+    __syncthreads();
     float s1[8], s2[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
-    // operands of the next row chunk are fetched while this one is finished
-    constexpr int RS = NT / CPR;
-    int r = threadIdx.x / CPR;
-    RowPre cur;
-    if (row0 + r < sh.M && col < sh.N) ep.pre8(row0 + r, col, cur);
-    for (; r < BM; r += RS) {
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int r = r0 + i * RS;
       const int row = row0 + r;
-      RowPre nxt;
-      if (r + RS < BM && row + RS < sh.M && col < sh.N) ep.pre8(row + RS, col, nxt);
-      if (row < sh.M && col < sh.N) {
+      const RowPre cur = pre[i % D];
+      if (i + D < NIT) {
+        const int rn = r + D * RS;
+        if (cok && rn < BM && row0 + rn < sh.M) ep.pre8(row0 + rn, col, pre[i % D]);
+      }
+      if (cok && r < BM && row < sh.M) {
         float v[8];
         Chunk<bf16>::unpack(*reinterpret_cast<const uint4*>(stg + r * BN + ((c ^ (r & (CPR - 1))) << 3)), v);
-        ep.row8(row, col, v, cur, s1, s2);
+        if constexpr (NCF > 0) ep.row8r(row, col, v, cur, s1, s2, cf);
+        else ep.row8(row, col, v, cur, s1, s2);
       }
-      cur = nxt;
     }
     if constexpr (EP::kStats) {
       __syncthreads();
@@ -913,8 +954,15 @@ struct BStager<BM, L, NT, false> {
   }
 };
 
+// at least two waves per SIMD: the 4-wave tiles (128x128, 256x64) then fit in
+// 256 registers, so two workgroups share a CU (their LDS rings allow it) and
+// one's epilogue overlaps the other's main loop; the 8-wave tiles have two
+// waves per SIMD anyway
+#ifndef VLP_WAVES_PER_EU
+#define VLP_WAVES_PER_EU 2
+#endif
 template <int BM, int BN, int WGM, int WGN, class LA, class LB, class EP>
-__global__ void __launch_bounds__(WGM * WGN * 64)
+__global__ void __launch_bounds__(WGM * WGN * 64) __attribute__((amdgpu_waves_per_eu(VLP_WAVES_PER_EU)))
 gemm_bk_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   constexpr int NT = WGM * WGN * 64;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
@@ -1026,7 +1074,7 @@ gemm_bk_kernel(GemmShape sh, LA la, LB lb, EP ep) {
 // so each fetch has ~two iterations of MFMA work to land in, and the
 // operand traffic per FLOP halves against 128x128 (256x256: 128 FLOP/B).
 template <int BM, int BN, int WGM, int WGN, class LA, class LB, class EP>
-__global__ void __launch_bounds__(WGM * WGN * 64)
+__global__ void __launch_bounds__(WGM * WGN * 64) __attribute__((amdgpu_waves_per_eu(VLP_WAVES_PER_EU)))
 gemm_big_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   constexpr int NT = WGM * WGN * 64;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
