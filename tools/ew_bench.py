@@ -1,5 +1,6 @@
-"""Time the streaming BN elementwise kernels at the bs=256 layer-1 size
-(bn_add_relu with identity + mask bits, bn_bwd_apply one side).
+"""Time the streaming BN elementwise kernels at the bs=256 ResNet34 sizes against
+a plain device copy of the same bytes (torch copy_), to place them against the
+achievable HBM rate.
   python tools/ew_bench.py"""
 import os
 import sys
@@ -10,17 +11,6 @@ import torch  # noqa: E402
 from vlp_amd import ops  # noqa: E402
 
 dev = torch.device("cuda", 0)
-N, H, W, C = 256, 128, 128, 64
-M = N * H * W
-y = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
-idt = torch.randn_like(y)
-out = torch.empty_like(y)
-m = torch.empty(y.numel() // 8, dtype=torch.uint8, device=dev)
-sc, sh = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev)
-mu, ist, gam = torch.zeros(C, device=dev), torch.ones(C, device=dev), torch.ones(C, device=dev)
-sg = torch.zeros(C, dtype=torch.float64, device=dev)
-sgx = torch.zeros_like(sg)
-dy = torch.empty_like(y)
 
 
 def tm(fn, it=10):
@@ -36,7 +26,23 @@ def tm(fn, it=10):
     return e0.elapsed_time(e1) / it * 1000
 
 
-t1 = tm(lambda: ops.bn_add_relu(y, sc, sh, idt, None, None, out, relu_mask=m))
-t2 = tm(lambda: ops.bn_bwd_apply(M, C, idt, None, 1, None, (y, mu, ist, gam, sg, sgx, dy), None, None, y))
-print(f"bn_add_relu {t1:7.1f} us ({4 * y.numel() * 2 / t1 / 1e6:5.2f} TB/s)  "
-      f"bn_bwd_apply {t2:7.1f} us ({3 * y.numel() * 2 / t2 / 1e6:5.2f} TB/s)")
+for (H, C) in [(128, 64), (64, 128), (32, 256), (16, 512)]:
+    N = 256
+    M = N * H * H
+    y = torch.randn(N, H, H, C, device=dev).to(torch.bfloat16)
+    idt = torch.randn_like(y)
+    out = torch.empty_like(y)
+    m = torch.empty(y.numel() // 8, dtype=torch.uint8, device=dev)
+    sc, sh = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev)
+    mu, ist, gam = torch.zeros(C, device=dev), torch.ones(C, device=dev), torch.ones(C, device=dev)
+    sg = torch.zeros(C, dtype=torch.float64, device=dev)
+    sgx = torch.zeros_like(sg)
+    dy = torch.empty_like(y)
+    B = y.numel() * 2
+    tc = tm(lambda: out.copy_(y))
+    t0 = tm(lambda: ops.bn_add_relu(y, sc, sh, None, None, None, out))
+    t1 = tm(lambda: ops.bn_add_relu(y, sc, sh, idt, None, None, out, relu_mask=m))
+    t2 = tm(lambda: ops.bn_bwd_apply(M, C, idt, None, 1, None, (y, mu, ist, gam, sg, sgx, dy), None, None, y))
+    print(f"{H:3d}x{H:<3d}x{C:3d}: copy {tc:7.1f} us {2 * B / tc / 1e6:5.2f} TB/s | "
+          f"bn_relu {t0:7.1f} us {2 * B / t0 / 1e6:5.2f} | bn_add_relu+mask {t1:7.1f} us {3.0625 * B / t1 / 1e6:5.2f} | "
+          f"bn_bwd_apply {t2:7.1f} us {3 * B / t2 / 1e6:5.2f} TB/s", flush=True)
