@@ -51,6 +51,21 @@ def main():
                 fn = lambda: ops.conv_fwd(x, wp, Co, KH, KW, S, P, stat_sum=s1, stat_sumsq=s2, stat_rep=64)  # noqa: E731
             elif op == "dgrad":
                 fn = lambda: ops.conv_dgrad(dy, wt, H, W, C, KH, KW, S, P)  # noqa: E731
+            elif op == "dgrad_bn":     # + ReLU-mask of bn(y), BN backward sums (EpiDgradBN)
+                yb = (torch.randn(N, H, W, C, device=dev)).to(torch.bfloat16)
+                cf = [torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1,
+                      torch.zeros(C, device=dev), torch.ones(C, device=dev)]
+                t1, t2 = torch.zeros(64 * C, dtype=torch.float64, device=dev), torch.zeros(64 * C, dtype=torch.float64, device=dev)
+                fn = lambda: ops.conv_dgrad(dy, wt, H, W, C, KH, KW, S, P, y_bn=yb, bn=tuple(cf),  # noqa: E731
+                                            stat1=t1, stat2=t2, stat_rep=64)
+            elif op == "dgrad_relu":   # + addend, ReLU bit mask, BN backward sums (EpiDgradRelu<bits>)
+                yb = (torch.randn(N, H, W, C, device=dev)).to(torch.bfloat16)
+                ad = (torch.randn(N, H, W, C, device=dev)).to(torch.bfloat16)
+                mk = torch.randint(0, 255, (N * H * W * C // 8,), dtype=torch.uint8, device=dev)
+                mu, ist = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+                t1, t2 = torch.zeros(64 * C, dtype=torch.float64, device=dev), torch.zeros(64 * C, dtype=torch.float64, device=dev)
+                fn = lambda: ops.conv_dgrad_relu(dy, wt, H, W, C, KH, KW, S, P, mk, yb, mu, ist, t1, t2,  # noqa: E731
+                                                 addend=ad, stat_rep=64)
             else:
                 gw = torch.empty(Co, C, KH, KW, device=dev)
                 fn = lambda: ops.conv_wgrad_into(dy, x, KH, KW, S, P, gw)  # noqa: E731

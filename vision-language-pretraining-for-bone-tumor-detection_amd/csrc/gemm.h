@@ -306,6 +306,40 @@ __device__ __forceinline__ void asm_lds_wait() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 }
+// The same fragment from a per-(slot, fragment) lane address: the k-substep
+// (+4*CPB KiB) and the upper k-half (+512 B) are immediate offsets of the
+// instruction, so a wave keeps one address VGPR per fragment and slot instead
+// of one per read (mn8_off is additive in both: neither changes the swizzle).
+template <int RB>
+__device__ __forceinline__ unsigned mn_frag_base(const char* lds, int rb) {
+  const int l = threadIdx.x & 63;
+  const int i = l & 15, g = l >> 4;
+  const int q = i >> 2, p = i & 3;
+  return lds_addr(lds + mn8_off<RB / 128>(8 * g + q, rb + 4 * p));
+}
+template <int OFF>
+__device__ __forceinline__ v8bf frag_tr_at(unsigned base) {
+  v4bf lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(base), "n"(OFF));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(base), "n"(OFF + 512));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+// fragment j of a wave's column of 16-row fragments: fragments j and j + 4 are
+// 1 KiB apart (the next 64-row block, same swizzle), so 4 base addresses serve
+// any number of fragments
+template <int RB, int J>
+__device__ __forceinline__ v8bf frag_tr_sub(unsigned base, int s) {
+  constexpr int S1 = 4 * (RB / 128) * 1024;
+  constexpr int OJ = (J >> 2) * 1024;
+  return s == 0 ? frag_tr_at<OJ>(base) : frag_tr_at<S1 + OJ>(base);
+}
+template <int I, int N, class Fn>
+__device__ __forceinline__ void static_for(Fn&& fn) {
+  if constexpr (I < N) {
+    fn(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(fn);
+  }
+}
 template <bool KC, int RB>
 __device__ __forceinline__ v8bf frag_big(const char* lds, int rb, int s) {
 #ifdef VLP_DBG_NOTR   // timing-only experiment: MN images read as if K-contig (wrong values)
@@ -1016,7 +1050,7 @@ gemm_bk_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   sb.issue(lb, nk > 0 ? rb : rz, kb, smem + s0 + ABYTES, wv);
 
   // one K-step: tile t sits in ring slot SL; tile t+1 is fetched into 1-SL
-  auto body = [&](auto slc, int t) {
+  auto body = [&](auto slc, int t) __attribute__((always_inline)) {
     constexpr int SL = decltype(slc)::value;
     wait_vmcnt<0>();
     raw_barrier();
@@ -1128,13 +1162,39 @@ gemm_big_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   sb.issue(lb, nk > 0 ? rb : rz, kb, smem + s0 + ABYTES, wv);
   sa.issue(la, nk > 1 ? ra : rz, kb + BK, smem + (STAGE - s0), wv);
   sb.issue(lb, nk > 1 ? rb : rz, kb + BK, smem + (STAGE - s0) + ABYTES, wv);
+  // MN-contig operands: one LDS address per (ring slot, fragment)
+  constexpr int QA = MB < 4 ? MB : 4, QB = NB < 4 ? NB : 4;
+  unsigned abase[2][LA::kKContig ? 1 : QA], bbase[2][LB::kKContig ? 1 : QB];
+  if constexpr (!LA::kKContig) {
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl)
+#pragma unroll
+      for (int a = 0; a < QA; ++a) abase[sl][a] = mn_frag_base<BM * 2>(smem + sl * STAGE, wm * WTM + a * 16);
+  }
+  if constexpr (!LB::kKContig) {
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl)
+#pragma unroll
+      for (int b = 0; b < QB; ++b)
+        bbase[sl][b] = mn_frag_base<BN * 2>(smem + sl * STAGE + ABYTES, wn * WTN + b * 16);
+  }
+  auto fragA = [&](auto slc, const char* ia, auto ac, int s) __attribute__((always_inline)) {
+    constexpr int a = decltype(ac)::value;
+    if constexpr (LA::kKContig) return frag_big<true, BM * 2>(ia, wm * WTM + a * 16, s);
+    else return frag_tr_sub<BM * 2, a>(abase[decltype(slc)::value][a & 3], s);
+  };
+  auto fragB = [&](auto slc, const char* ib, auto bc, int s) __attribute__((always_inline)) {
+    constexpr int b = decltype(bc)::value;
+    if constexpr (LB::kKContig) return frag_big<true, BN * 2>(ib, wn * WTN + b * 16, s);
+    else return frag_tr_sub<BN * 2, b>(bbase[decltype(slc)::value][b & 3], s);
+  };
 
 #if VLP_BIG_PRIO
   // static priority for the second-dispatched half (MI355X_MICROARCH.md, "Two waves
   // per SIMD" item 4): waves 4-7 are the arbitration losers on every segment
   if (wv >= (WGM * WGN) / 2) __builtin_amdgcn_s_setprio(1);
 #endif
-  auto body = [&](auto slc, int t) {
+  auto body = [&](auto slc, int t) __attribute__((always_inline)) {
     constexpr int SL = decltype(slc)::value;
     wait_vmcnt<NI>();
     raw_barrier();
@@ -1143,10 +1203,8 @@ gemm_big_kernel(GemmShape sh, LA la, LB lb, EP ep) {
     v8bf fa[2][MB], fb[2][NB];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-#pragma unroll
-      for (int a = 0; a < MB; ++a) fa[s][a] = frag_big<LA::kKContig, BM * 2>(ia, wm * WTM + a * 16, s);
-#pragma unroll
-      for (int b = 0; b < NB; ++b) fb[s][b] = frag_big<LB::kKContig, BN * 2>(ib, wn * WTN + b * 16, s);
+      static_for<0, MB>([&](auto ac) { fa[s][decltype(ac)::value] = fragA(slc, ia, ac, s); });
+      static_for<0, NB>([&](auto bc) { fb[s][decltype(bc)::value] = fragB(slc, ib, bc, s); });
     }
     if constexpr (!LA::kKContig || !LB::kKContig) asm_lds_wait();
 #pragma unroll
