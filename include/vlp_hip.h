@@ -247,6 +247,42 @@ int vlp_scatter_rows(int dtype, int R, int D, const void* in, int ldi, void* out
  * (fp32 vlp_linear_fwd of normalised embeddings). */
 int vlp_row_topk(int R, int N, const float* x, long long ldx, int K, float* vals, int* idx, void* stream);
 
+/* ---------------- NesT image encoder (BASELINE configs[3]) ----------------
+ * Replace timm nest.py's pieces behind ImageEncoder's timm.create_model("nest_small", ...)
+ * (VisionLanguageModule.py:27-35).  Blocked local attention: qkv[BT*N][3C] rows (q | k | v,
+ * head h at h*32), out[BT*N][C] head-major (h*32 + d; timm's d*H + h order is folded into
+ * the proj weight with vlp_nest_permute_cols), lse[BT*H*N] (log2 domain), head dim 32.
+ * Backward: delta[BT*H*N] scratch; writes every column of dqkv. */
+int vlp_nest_attn_fwd(int dtype, int BT, int H, int N, int dh, const void* qkv, void* out, float* lse,
+                      float scale, void* stream);
+int vlp_nest_attn_bwd(int dtype, int BT, int H, int N, int dh, const void* qkv, const void* out,
+                      const void* dout, const float* lse, float* delta, void* dqkv, float scale, void* stream);
+/* blockify (timm nest.blockify, + pos[Hg*Wg][bs*bs][C] when non-NULL): NHWC image
+ * x[B][Hg*bs][Wg*bs][C] -> tokens y[B][Hg*Wg][bs*bs][C]; inverse = deblockify (y <- x tokens) */
+int vlp_nest_blockify(int dtype, int B, int Hg, int Wg, int bs, int C, const void* x, const float* pos,
+                      void* y, int inverse, void* stream);
+/* dpos[t][c] = sum_b dy[b][t][c] over the B samples of a level input [B][TN][C] */
+int vlp_nest_pos_grad(int dtype, int B, int TN, int C, const void* dy, float* dpos, void* stream);
+/* ConvPool's max pool 3x3 / 2, padding 1 (NHWC); idx = window tap 0..8 */
+int vlp_nest_maxpool_fwd(int dtype, int B, int H, int W, int C, const void* x, void* y, uint8_t* idx,
+                         void* stream);
+int vlp_nest_maxpool_bwd(int dtype, int B, int H, int W, int C, const void* dy, const uint8_t* idx,
+                         void* dx, void* stream);
+/* patch-embed im2col: 4x4/4 patches -> out[B*(H/4)*(W/4)][48] in level-0 blocked token order;
+ * exactly one of x (fp32 [B][3][H][W], normalised) / x_u8 ([B][1][H][W], (v-mean)/std) */
+int vlp_nest_patch_prep(int dtype, int B, int H, int W, int bs, const float* x, const uint8_t* x_u8,
+                        float mean, float std_, void* out, void* stream);
+/* y[m][n] += bias[n] */
+int vlp_nest_add_bias(int dtype, long long M, int N, void* y, const float* bias, void* stream);
+/* proj weight input columns: dst[n][h*Dh + d] = src[n][d*H + h] (fp32 -> dtype_out), and back */
+int vlp_nest_permute_cols(int dtype_out, int Nr, int H, int Dh, const float* src, void* dst, void* stream);
+int vlp_nest_unpermute_cols(int Nr, int H, int Dh, const float* src, float* dst, void* stream);
+/* DropPath: mode 0 x += s[m / rows] * y; mode 1 y = s[m / rows] * x */
+int vlp_nest_rowscale(int dtype, long long M, int N, int rows, const float* s, void* x, void* y, int mode,
+                      void* stream);
+/* global average pool backward: dy[b*HW + p][c] = dfeat[b][c] * inv */
+int vlp_nest_bcast(int dtype, int B, int HW, int C, const float* dfeat, float inv, void* dy, void* stream);
+
 /* ---------------- contrastive head ----------------
  * Replace VisionLanguageModule.forward (VisionLanguageModule.py:441-461: projections,
  * F.normalize, logit_scale.exp().clamp(max=100) * img @ txt.T) and

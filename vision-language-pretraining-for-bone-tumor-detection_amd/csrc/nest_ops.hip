@@ -1,0 +1,729 @@
+// NesT-Small image encoder kernels (BASELINE configs[3]).
+//
+// The reference reaches NesT through ImageEncoder's generic
+// timm.create_model(model, num_classes=0, global_pool="avg", ...)
+// (src/models/pretrain/VisionLanguageModule.py:27-35; timm==1.0.15 nest.py,
+// not installed here).  Besides the GEMMs / LayerNorms shared with the text
+// tower (bert_ops.hip), NesT needs:
+//   * blocked local self-attention: every image block of N = 1024 tokens
+//     (512x512 input) attends within itself, head dim 32 -- flash attention
+//     on MFMA, forward + two backward kernels (dK/dV over key tiles, dQ over
+//     query tiles), log-sum-exp saved by the forward;
+//   * blockify / deblockify (+ the level's positional embedding);
+//   * ConvPool's 3x3/2 max pool (after the channel LayerNorm);
+//   * the patch-embedding im2col (4x4/4, non-overlapping) from the collated
+//     batch (uint8 1-channel upload or the reference's fp32 3-channel tensor);
+//   * DropPath (stochastic depth, timm's default drop_path_rate = 0.5) as a
+//     per-sample scale on each residual branch.
+// Attention layout: q/k/v are the columns [0,C), [C,2C), [2C,3C) of the
+// qkv Linear's output rows, head h at h*32.. (nn.Linear(dim, 3*dim) reshaped
+// (3, heads, 32)); the output is written head-major [row][h*32 + d].  timm
+// NesT's Attention emits channel d*H + h instead (permute(0,2,3,4,1)); the
+// host folds that permutation into the proj weight (vlp_nest_permute_cols).
+#include "common.h"
+#include "gemm.h"
+
+namespace vlp {
+
+// ---------------- fragments (MFMA 16x16x32 bf16 / 16x16x4 f32) ----------------
+// Convention as bert_ops.hip: D[m][n] = sum_k X[m][k] Y[n][k]; lane l = 16g + i
+// holds D[4g + r][i].  kfrag: X rows r0.. of a row-major [row][k] image (k
+// contiguous); tfrag: X rows r0.. (the "mn" index) of a row-major [k][mn]
+// image, i.e. read transposed (ds_read_b64_tr_b16 for bf16).
+template <typename T> struct FA;
+template <> struct FA<bf16> {
+  static constexpr int KS = 32;
+  typedef v8bf F;
+  __device__ static __forceinline__ F kfrag(const bf16* img, int ld, int r0, int k0) {
+    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+    return *reinterpret_cast<const v8bf*>(img + (r0 + i) * ld + k0 + 8 * g);
+  }
+  __device__ static __forceinline__ F tfrag(const bf16* img, int ld, int r0, int k0) {
+    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+    const int q = i >> 2, p = i & 3;
+    const int k1 = k0 + 8 * g + q;
+    v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(img + k1 * ld + r0 + 4 * p));
+    v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(img + (k1 + 4) * ld + r0 + 4 * p));
+    return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+  // a fragment straight from global memory (rows r0.., k contiguous)
+  __device__ static __forceinline__ F gfrag(const bf16* p, size_t ld, int r0, int k0, bool ok) {
+    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+    if (!ok) return F{};
+    return *reinterpret_cast<const v8bf*>(p + (size_t)(r0 + i) * ld + k0 + 8 * g);
+  }
+  __device__ static __forceinline__ void mma(v4f& acc, const F& x, const F& y) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x, y, acc, 0, 0, 0);
+  }
+};
+template <> struct FA<float> {
+  static constexpr int KS = 16;
+  typedef v4f F;
+  __device__ static __forceinline__ F kfrag(const float* img, int ld, int r0, int k0) {
+    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+    return *reinterpret_cast<const v4f*>(img + (r0 + i) * ld + k0 + 4 * g);
+  }
+  __device__ static __forceinline__ F tfrag(const float* img, int ld, int r0, int k0) {
+    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+    F f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f[j] = img[(k0 + 4 * g + j) * ld + r0 + i];
+    return f;
+  }
+  __device__ static __forceinline__ F gfrag(const float* p, size_t ld, int r0, int k0, bool ok) {
+    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
+    if (!ok) return F{0.f, 0.f, 0.f, 0.f};
+    return *reinterpret_cast<const v4f*>(p + (size_t)(r0 + i) * ld + k0 + 4 * g);
+  }
+  __device__ static __forceinline__ void mma(v4f& acc, const F& x, const F& y) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[j], y[j], acc, 0, 0, 0);
+  }
+};
+
+__device__ __forceinline__ float q4max(float v) {
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  return fmaxf(v, __shfl_xor(v, 32, 64));
+}
+__device__ __forceinline__ float q4sum(float v) {
+  v += __shfl_xor(v, 16, 64);
+  return v + __shfl_xor(v, 32, 64);
+}
+
+constexpr int kDh = 32;                 // head dim (every NesT variant: C / heads = 32)
+constexpr int kTile = 64;               // tokens per tile (4 waves x 16)
+
+// four consecutive values of one row -> LDS (8 B bf16 / 16 B fp32)
+template <typename T>
+__device__ __forceinline__ void st4(T* p, float a, float b, float c, float d);
+template <> __device__ __forceinline__ void st4<bf16>(bf16* p, float a, float b, float c, float d) {
+  v4bf v;
+  v[0] = (bf16)a; v[1] = (bf16)b; v[2] = (bf16)c; v[3] = (bf16)d;
+  *reinterpret_cast<v4bf*>(p) = v;
+}
+template <> __device__ __forceinline__ void st4<float>(float* p, float a, float b, float c, float d) {
+  *reinterpret_cast<v4f*>(p) = v4f{a, b, c, d};
+}
+
+// rows [t0, t0+64) x 32 channels (column offset col) of a [rows][ld] tensor ->
+// LDS image [64][LDI]; rows >= N are zero
+template <typename T, int LDI>
+__device__ __forceinline__ void stage_tile(T* img, const T* src, size_t ld, int col, int t0, int N) {
+  constexpr int EPC = 16 / (int)sizeof(T);            // elements per 16-B chunk
+  constexpr int CPR = kDh / EPC;                      // chunks per row
+  for (int q = threadIdx.x; q < kTile * CPR; q += blockDim.x) {
+    const int r = q / CPR, c = q - r * CPR;
+    uint4 v = zero4();
+    if (t0 + r < N) v = ldg16(src + (size_t)(t0 + r) * ld + col + c * EPC);
+    *reinterpret_cast<uint4*>(img + r * LDI + c * EPC) = v;
+  }
+}
+
+// ---------------- forward ----------------
+// grid (ceil(N/64), H, BT); 4 waves, wave w owns queries qt*64 + 16w .. +15.
+// out[bt*N + q][h*32 + d]; lse[(bt*H + h)*N + q] = log2-sum-exp of the scaled
+// (x log2 e) scores.
+template <typename T>
+__global__ void __launch_bounds__(256)
+nest_attn_fwd_kernel(int BT, int H, int N, const T* __restrict__ qkv, T* __restrict__ out,
+                     float* __restrict__ lse, float sl2) {
+  using M = FA<T>;
+  constexpr int PAD = 16 / (int)sizeof(T);
+  constexpr int LDK = kDh + PAD, LDP = kTile + PAD;
+  __shared__ __attribute__((aligned(16))) T sK[kTile * LDK];
+  __shared__ __attribute__((aligned(16))) T sV[kTile * LDK];
+  __shared__ __attribute__((aligned(16))) T sP[4][16 * LDP];
+  const int qt = blockIdx.x, h = blockIdx.y, bt = blockIdx.z;
+  const int C = H * kDh;
+  const size_t ld3 = 3 * (size_t)C;
+  const T* base = qkv + (size_t)bt * N * ld3;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, li = l & 15, lg = l >> 4;
+  const int q0 = qt * kTile + 16 * w;
+  const bool qok = q0 + li < N;
+  typename M::F qf[kDh / M::KS];
+#pragma unroll
+  for (int ks = 0; ks < kDh / M::KS; ++ks) qf[ks] = M::gfrag(base + h * kDh, ld3, q0, ks * M::KS, qok);
+  float mi = -INFINITY, li_sum = 0.f;
+  v4f o[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
+  T* myP = sP[w];
+  const int nt = (N + kTile - 1) / kTile;
+  for (int t = 0; t < nt; ++t) {
+    __syncthreads();   // every wave is done with the previous tile
+    stage_tile<T, LDK>(sK, base, ld3, C + h * kDh, t * kTile, N);
+    stage_tile<T, LDK>(sV, base, ld3, 2 * C + h * kDh, t * kTile, N);
+    __syncthreads();
+    v4f s[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      s[b] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < kDh / M::KS; ++ks) M::mma(s[b], M::kfrag(sK, LDK, 16 * b, ks * M::KS), qf[ks]);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = t * kTile + 16 * b + 4 * lg + r;
+        s[b][r] = key < N ? s[b][r] * sl2 : -INFINITY;
+        mx = fmaxf(mx, s[b][r]);
+      }
+    mx = q4max(mx);
+    const float mn = fmaxf(mi, mx);
+    const float alpha = mi == -INFINITY ? 0.f : exp2f(mi - mn);
+    float sum = 0.f;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s[b][r] = exp2f(s[b][r] - mn);
+        sum += s[b][r];
+      }
+      st4<T>(myP + li * LDP + 16 * b + 4 * lg, s[b][0], s[b][1], s[b][2], s[b][3]);
+    }
+    li_sum = li_sum * alpha + q4sum(sum);
+    mi = mn;
+#pragma unroll
+    for (int db = 0; db < 2; ++db) o[db] *= alpha;
+    // O^T[d][q] += sum_key V^T[d][key] P[q][key]
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int ks = 0; ks < kTile; ks += M::KS)
+        M::mma(o[db], M::tfrag(sV, LDK, 16 * db, ks), M::kfrag(myP, LDP, 0, ks));
+  }
+  if (qok) {
+    const float inv = 1.f / li_sum;
+    T* dst = out + ((size_t)bt * N + q0 + li) * C + h * kDh;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+      st4<T>(dst + 16 * db + 4 * lg, o[db][0] * inv, o[db][1] * inv, o[db][2] * inv, o[db][3] * inv);
+    if (lg == 0) lse[((size_t)bt * H + h) * N + q0 + li] = mi + log2f(li_sum);
+  }
+}
+
+// delta[(bt*H + h)*N + q] = sum_d dout[row][h*32 + d] * out[row][h*32 + d]
+template <typename T>
+__global__ void nest_attn_delta_kernel(int BT, int H, int N, const T* __restrict__ out,
+                                       const T* __restrict__ dout, float* __restrict__ delta) {
+  constexpr int EPC = 16 / (int)sizeof(T);
+  const size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x;   // (row, h)
+  const size_t total = (size_t)BT * N * H;
+  if (idx >= total) return;
+  const size_t row = idx / H;
+  const int h = (int)(idx - row * H);
+  const int C = H * kDh;
+  const T* a = out + row * C + h * kDh;
+  const T* b = dout + row * C + h * kDh;
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < kDh; c += EPC) {
+    float x[EPC], y[EPC];
+    Chunk<T>::unpack(ldg16(a + c), x);
+    Chunk<T>::unpack(ldg16(b + c), y);
+#pragma unroll
+    for (int j = 0; j < EPC; ++j) s += x[j] * y[j];
+  }
+  const size_t bt = row / N, q = row - bt * N;
+  delta[(bt * H + h) * N + q] = s;
+}
+
+// ---------------- backward: dQ over key tiles ----------------
+// grid (ceil(N/64), H, BT); wave w owns queries qt*64 + 16w .. +15.
+//   P = exp2(S*sl2 - lse), dP = dO V^T, dS = P (dP - delta), dQ = scale dS K
+template <typename T>
+__global__ void __launch_bounds__(256)
+nest_attn_bwd_dq_kernel(int BT, int H, int N, const T* __restrict__ qkv, const T* __restrict__ dout,
+                        const float* __restrict__ lse, const float* __restrict__ delta, T* __restrict__ dqkv,
+                        float sl2, float scale) {
+  using M = FA<T>;
+  constexpr int PAD = 16 / (int)sizeof(T);
+  constexpr int LDK = kDh + PAD, LDP = kTile + PAD;
+  __shared__ __attribute__((aligned(16))) T sK[kTile * LDK];
+  __shared__ __attribute__((aligned(16))) T sV[kTile * LDK];
+  __shared__ __attribute__((aligned(16))) T sP[4][16 * LDP];
+  const int qt = blockIdx.x, h = blockIdx.y, bt = blockIdx.z;
+  const int C = H * kDh;
+  const size_t ld3 = 3 * (size_t)C;
+  const T* base = qkv + (size_t)bt * N * ld3;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, li = l & 15, lg = l >> 4;
+  const int q0 = qt * kTile + 16 * w;
+  const bool qok = q0 + li < N;
+  typename M::F qf[kDh / M::KS], df[kDh / M::KS];
+#pragma unroll
+  for (int ks = 0; ks < kDh / M::KS; ++ks) {
+    qf[ks] = M::gfrag(base + h * kDh, ld3, q0, ks * M::KS, qok);
+    df[ks] = M::gfrag(dout + (size_t)bt * N * C + h * kDh, C, q0, ks * M::KS, qok);
+  }
+  const size_t so = ((size_t)bt * H + h) * N + q0 + li;
+  const float lq = qok ? lse[so] : INFINITY;
+  const float dq_ = qok ? delta[so] : 0.f;
+  v4f acc[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
+  T* myP = sP[w];
+  const int nt = (N + kTile - 1) / kTile;
+  for (int t = 0; t < nt; ++t) {
+    __syncthreads();
+    stage_tile<T, LDK>(sK, base, ld3, C + h * kDh, t * kTile, N);
+    stage_tile<T, LDK>(sV, base, ld3, 2 * C + h * kDh, t * kTile, N);
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      v4f s = v4f{0.f, 0.f, 0.f, 0.f}, dp = s;
+#pragma unroll
+      for (int ks = 0; ks < kDh / M::KS; ++ks) {
+        M::mma(s, M::kfrag(sK, LDK, 16 * b, ks * M::KS), qf[ks]);
+        M::mma(dp, M::kfrag(sV, LDK, 16 * b, ks * M::KS), df[ks]);
+      }
+      float ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = t * kTile + 16 * b + 4 * lg + r;
+        const float p = key < N ? exp2f(s[r] * sl2 - lq) : 0.f;
+        ds[r] = p * (dp[r] - dq_);
+      }
+      st4<T>(myP + li * LDP + 16 * b + 4 * lg, ds[0], ds[1], ds[2], ds[3]);
+    }
+    // dQ^T[d][q] += sum_key K^T[d][key] dS[q][key]
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int ks = 0; ks < kTile; ks += M::KS)
+        M::mma(acc[db], M::tfrag(sK, LDK, 16 * db, ks), M::kfrag(myP, LDP, 0, ks));
+  }
+  if (qok) {
+    T* dst = dqkv + ((size_t)bt * N + q0 + li) * ld3 + h * kDh;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+      st4<T>(dst + 16 * db + 4 * lg, acc[db][0] * scale, acc[db][1] * scale, acc[db][2] * scale,
+             acc[db][3] * scale);
+  }
+}
+
+// ---------------- backward: dK, dV over query tiles ----------------
+// grid (ceil(N/64), H, BT); wave w owns keys kt*64 + 16w .. +15.
+//   dV = P^T dO, dK = scale dS^T Q
+template <typename T>
+__global__ void __launch_bounds__(256)
+nest_attn_bwd_dkdv_kernel(int BT, int H, int N, const T* __restrict__ qkv, const T* __restrict__ dout,
+                          const float* __restrict__ lse, const float* __restrict__ delta,
+                          T* __restrict__ dqkv, float sl2, float scale) {
+  using M = FA<T>;
+  constexpr int PAD = 16 / (int)sizeof(T);
+  constexpr int LDK = kDh + PAD, LDQ = 16 + PAD;
+  __shared__ __attribute__((aligned(16))) T sQ[kTile * LDK];
+  __shared__ __attribute__((aligned(16))) T sD[kTile * LDK];
+  __shared__ __attribute__((aligned(16))) T sPt[4][kTile * LDQ];   // P^T as [q][key16]
+  __shared__ __attribute__((aligned(16))) T sSt[4][kTile * LDQ];   // dS^T as [q][key16]
+  __shared__ float sL[kTile], sDl[kTile];
+  const int kt = blockIdx.x, h = blockIdx.y, bt = blockIdx.z;
+  const int C = H * kDh;
+  const size_t ld3 = 3 * (size_t)C;
+  const T* base = qkv + (size_t)bt * N * ld3;
+  const T* dbase = dout + (size_t)bt * N * C;
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63, li = l & 15, lg = l >> 4;
+  const int k0 = kt * kTile + 16 * w;
+  const bool kok = k0 + li < N;
+  typename M::F kf[kDh / M::KS], vf[kDh / M::KS];
+#pragma unroll
+  for (int ks = 0; ks < kDh / M::KS; ++ks) {
+    kf[ks] = M::gfrag(base + C + h * kDh, ld3, k0, ks * M::KS, kok);
+    vf[ks] = M::gfrag(base + 2 * C + h * kDh, ld3, k0, ks * M::KS, kok);
+  }
+  v4f dk[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
+  v4f dv[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
+  T* myP = sPt[w];
+  T* myS = sSt[w];
+  const size_t sb = ((size_t)bt * H + h) * N;
+  const int nt = (N + kTile - 1) / kTile;
+  for (int t = 0; t < nt; ++t) {
+    __syncthreads();
+    stage_tile<T, LDK>(sQ, base, ld3, h * kDh, t * kTile, N);
+    stage_tile<T, LDK>(sD, dbase, C, h * kDh, t * kTile, N);
+    if (threadIdx.x < kTile) {
+      const int q = t * kTile + threadIdx.x;
+      sL[threadIdx.x] = q < N ? lse[sb + q] : INFINITY;
+      sDl[threadIdx.x] = q < N ? delta[sb + q] : 0.f;
+    }
+    __syncthreads();
+    // S^T[key][q] (lane: keys 4lg+r of the wave's 16, query 16b + li)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      v4f s = v4f{0.f, 0.f, 0.f, 0.f}, dp = s;
+#pragma unroll
+      for (int ks = 0; ks < kDh / M::KS; ++ks) {
+        M::mma(s, kf[ks], M::kfrag(sQ, LDK, 16 * b, ks * M::KS));
+        M::mma(dp, vf[ks], M::kfrag(sD, LDK, 16 * b, ks * M::KS));
+      }
+      const int q = 16 * b + li;
+      const float lq = sL[q], dl = sDl[q];
+      float p[4], ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        p[r] = exp2f(s[r] * sl2 - lq);
+        ds[r] = p[r] * (dp[r] - dl);
+      }
+      st4<T>(myP + q * LDQ + 4 * lg, p[0], p[1], p[2], p[3]);
+      st4<T>(myS + q * LDQ + 4 * lg, ds[0], ds[1], ds[2], ds[3]);
+    }
+    // dV^T[d][key] += sum_q dO^T[d][q] P^T[key][q];  dK^T[d][key] += sum_q Q^T[d][q] dS^T[key][q]
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int ks = 0; ks < kTile; ks += M::KS) {
+        M::mma(dv[db], M::tfrag(sD, LDK, 16 * db, ks), M::tfrag(myP, LDQ, 0, ks));
+        M::mma(dk[db], M::tfrag(sQ, LDK, 16 * db, ks), M::tfrag(myS, LDQ, 0, ks));
+      }
+  }
+  if (kok) {
+    T* dst = dqkv + ((size_t)bt * N + k0 + li) * ld3 + h * kDh;
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      st4<T>(dst + C + 16 * db + 4 * lg, dk[db][0] * scale, dk[db][1] * scale, dk[db][2] * scale,
+             dk[db][3] * scale);
+      st4<T>(dst + 2 * C + 16 * db + 4 * lg, dv[db][0], dv[db][1], dv[db][2], dv[db][3]);
+    }
+  }
+}
+
+// ---------------- blockify / deblockify ----------------
+// image x[B][Hg*bs][Wg*bs][C] (NHWC) <-> blocked tokens y[B][Hg*Wg][bs*bs][C]
+// (timm nest blockify: block index gh*Wg + gw, token bh*bs + bw).  Forward adds
+// the level's positional embedding pos[Hg*Wg][bs*bs][C] (fp32) when given.
+template <typename T>
+__global__ void nest_blockify_kernel(int B, int Hg, int Wg, int bs, int C, const T* __restrict__ x,
+                                     const float* __restrict__ pos, T* __restrict__ y, int inverse) {
+  constexpr int EPC = 16 / (int)sizeof(T);
+  const int cpr = C / EPC;
+  const size_t total = (size_t)B * Hg * bs * Wg * bs * cpr;
+  for (size_t q = blockIdx.x * (size_t)blockDim.x + threadIdx.x; q < total; q += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(q % cpr);
+    size_t pix = q / cpr;                       // image pixel index (b, h, w)
+    const int W = Wg * bs, Hh = Hg * bs;
+    const int wq = (int)(pix % W);
+    const size_t r = pix / W;
+    const int hq = (int)(r % Hh);
+    const int b = (int)(r / Hh);
+    const int gh = hq / bs, bh = hq - gh * bs, gw = wq / bs, bw = wq - gw * bs;
+    const size_t blk = (size_t)gh * Wg + gw, tok = (size_t)bh * bs + bw;
+    const size_t trow = ((size_t)b * Hg * Wg + blk) * bs * bs + tok;
+    if (!inverse) {
+      uint4 v = ldg16(x + pix * C + c * EPC);
+      if (pos) {
+        float f[EPC];
+        Chunk<T>::unpack(v, f);
+        const float* pp = pos + (blk * bs * bs + tok) * C + c * EPC;
+#pragma unroll
+        for (int j = 0; j < EPC; ++j) f[j] += pp[j];
+        v = Chunk<T>::pack(f);
+      }
+      stg16(y + trow * C + c * EPC, v);
+    } else {
+      stg16(y + pix * C + c * EPC, ldg16(x + trow * C + c * EPC));
+    }
+  }
+}
+
+// positional-embedding gradient: dpos[t][c] = sum_b dy[b][t][c] (fp32 out)
+template <typename T>
+__global__ void nest_pos_grad_kernel(int B, int TN, int C, const T* __restrict__ dy, float* __restrict__ dpos) {
+  const size_t total = (size_t)TN * C;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += to_f(dy[(size_t)b * total + e]);
+    dpos[e] = s;
+  }
+}
+
+// ---------------- 3x3 / 2 max pool, padding 1 (ConvPool) ----------------
+// x[B][H][W][C] -> y[B][Ho][Wo][C], idx = window tap (0..8) of the maximum
+// (first maximum in row-major tap order, as torch's max_pool2d).
+template <typename T>
+__global__ void nest_maxpool_fwd_kernel(int B, int H, int W, int C, const T* __restrict__ x, T* __restrict__ y,
+                                        uint8_t* __restrict__ idx) {
+  const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+  const size_t total = (size_t)B * Ho * Wo * C;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    size_t r = e / C;
+    const int wo = (int)(r % Wo);
+    r /= Wo;
+    const int ho = (int)(r % Ho);
+    const int b = (int)(r / Ho);
+    float best = 0.f;
+    int bi = -1;
+    for (int kh = 0; kh < 3; ++kh) {
+      const int hi = 2 * ho - 1 + kh;
+      if ((unsigned)hi >= (unsigned)H) continue;
+      for (int kw = 0; kw < 3; ++kw) {
+        const int wi = 2 * wo - 1 + kw;
+        if ((unsigned)wi >= (unsigned)W) continue;
+        const float v = to_f(x[(((size_t)b * H + hi) * W + wi) * C + c]);
+        if (bi < 0 || v > best) { best = v; bi = kh * 3 + kw; }
+      }
+    }
+    y[e] = from_f<T>(best);
+    idx[e] = (uint8_t)bi;
+  }
+}
+// dx[b][h][w][c] = sum of dy over the pooled outputs whose window's maximum is (h, w)
+template <typename T>
+__global__ void nest_maxpool_bwd_kernel(int B, int H, int W, int C, const T* __restrict__ dy,
+                                        const uint8_t* __restrict__ idx, T* __restrict__ dx) {
+  const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+  const size_t total = (size_t)B * H * W * C;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    size_t r = e / C;
+    const int wi = (int)(r % W);
+    r /= W;
+    const int hi = (int)(r % H);
+    const int b = (int)(r / H);
+    float s = 0.f;
+    // the pooled rows whose window 2ho-1 .. 2ho+1 holds hi: (hi+1)/2 and the one above
+    for (int a = 0; a < 2; ++a) {
+      const int ho = (hi + 1) / 2 - a;
+      if (ho < 0 || ho >= Ho || 2 * ho - 1 > hi || 2 * ho + 1 < hi) continue;
+      for (int bb = 0; bb < 2; ++bb) {
+        const int wo = (wi + 1) / 2 - bb;
+        if (wo < 0 || wo >= Wo || 2 * wo - 1 > wi || 2 * wo + 1 < wi) continue;
+        const size_t o = (((size_t)b * Ho + ho) * Wo + wo) * C + c;
+        const int tap = (hi - (2 * ho - 1)) * 3 + (wi - (2 * wo - 1));
+        if (idx[o] == tap) s += to_f(dy[o]);
+      }
+    }
+    dx[e] = from_f<T>(s);
+  }
+}
+
+// ---------------- patch embedding im2col ----------------
+// 4x4 / 4 patches of the normalised image, rows in BLOCKED token order of
+// level 0 (block (gh, gw) of the Hp x Wp patch grid, token (bh, bw)), so the
+// patch GEMM writes level 0's input directly.  K = 48 = (c, kh, kw) as the
+// conv weight [96][3][4][4] flattens; from the uint8 1-channel upload the
+// three channels are the same normalised pixel (PretrainDataModule.py:167-171).
+template <typename T>
+__global__ void nest_patch_prep_kernel(int B, int Himg, int Wimg, int bs, const float* __restrict__ x,
+                                       const uint8_t* __restrict__ xu8, float mean, float inv_std,
+                                       T* __restrict__ out) {
+  const int Hp = Himg / 4, Wp = Wimg / 4;
+  const int Hg = Hp / bs, Wg = Wp / bs;
+  const size_t total = (size_t)B * Hp * Wp * 48;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    const int k = (int)(e % 48);
+    const size_t trow = e / 48;                               // blocked token row
+    const int tok = (int)(trow % ((size_t)bs * bs));
+    size_t r = trow / ((size_t)bs * bs);
+    const int blk = (int)(r % ((size_t)Hg * Wg));
+    const int b = (int)(r / ((size_t)Hg * Wg));
+    const int gh = blk / Wg, gw = blk - gh * Wg, bh = tok / bs, bw = tok - bh * bs;
+    const int ph = gh * bs + bh, pw = gw * bs + bw;           // patch coordinates
+    const int c = k / 16, kh = (k >> 2) & 3, kw = k & 3;
+    const int hi = 4 * ph + kh, wi = 4 * pw + kw;
+    float v;
+    if (xu8) v = ((float)xu8[((size_t)b * Himg + hi) * Wimg + wi] - mean) * inv_std;
+    else v = x[(((size_t)b * 3 + c) * Himg + hi) * Wimg + wi];
+    out[e] = from_f<T>(v);
+  }
+}
+
+// ---------------- small helpers ----------------
+// y[m][n] += bias[n]
+template <typename T>
+__global__ void nest_add_bias_kernel(size_t M, int N, T* __restrict__ y, const float* __restrict__ bias) {
+  const size_t total = M * N;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x)
+    y[e] = from_f<T>(to_f(y[e]) + bias[e % N]);
+}
+// dst[n][d*H + h] <-> dst[n][h*Dh + d]: the proj weight's input columns (fp32
+// master -> compute dtype), or (inverse) its gradient back to timm's order
+template <typename TI, typename TO>
+__global__ void nest_permute_cols_kernel(int Nr, int H, int Dh, const TI* __restrict__ src, TO* __restrict__ dst,
+                                         int inverse) {
+  const int C = H * Dh;
+  const size_t total = (size_t)Nr * C;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    const size_t n = e / C;
+    const int j = (int)(e - n * C);      // head-major column h*Dh + d
+    const int h = j / Dh, d = j - h * Dh;
+    const int t = d * H + h;             // timm column
+    if (!inverse) dst[e] = from_f<TO>(to_f(src[n * C + t]));
+    else dst[n * C + t] = from_f<TO>(to_f(src[e]));
+  }
+}
+// DropPath on a residual branch: x[m][n] += s[m / rows] * y[m][n] (s = 0 or 1/(1-p))
+// mode 1 (backward): y[m][n] = s[m / rows] * x[m][n]
+template <typename T>
+__global__ void nest_rowscale_kernel(size_t M, int N, int rows, const float* __restrict__ s, T* __restrict__ x,
+                                     T* __restrict__ y, int mode) {
+  const size_t total = M * N;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    const float k = s[(e / N) / rows];
+    if (mode == 0) x[e] = from_f<T>(to_f(x[e]) + k * to_f(y[e]));
+    else y[e] = from_f<T>(k * to_f(x[e]));
+  }
+}
+// dy[b*HW + p][c] = dfeat[b][c] * inv (global average pool backward)
+template <typename T>
+__global__ void nest_bcast_kernel(int B, int HW, int C, const float* __restrict__ dfeat, float inv,
+                                  T* __restrict__ dy) {
+  const size_t total = (size_t)B * HW * C;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    const size_t b = e / ((size_t)HW * C);
+    dy[e] = from_f<T>(dfeat[b * C + c] * inv);
+  }
+}
+
+static inline dim3 ew(size_t n) {
+  size_t b = (n + 255) / 256;
+  if (b > 16384) b = 16384;
+  if (b < 1) b = 1;
+  return dim3((unsigned)b);
+}
+
+}  // namespace vlp
+
+using namespace vlp;
+
+#define NEST_DT(dtype, F, ...)                  \
+  do {                                          \
+    if ((dtype) == VLP_BF16) F<bf16>(__VA_ARGS__); \
+    else F<float>(__VA_ARGS__);                 \
+  } while (0)
+
+template <typename T>
+static void attn_fwd_t(int BT, int H, int N, const void* qkv, void* out, float* lse, float scale, hipStream_t st) {
+  hipLaunchKernelGGL(nest_attn_fwd_kernel<T>, dim3((N + kTile - 1) / kTile, H, BT), dim3(256), 0, st, BT, H, N,
+                     (const T*)qkv, (T*)out, lse, scale * 1.4426950408889634f);
+}
+VLP_EXPORT int vlp_nest_attn_fwd(int dtype, int BT, int H, int N, int dh, const void* qkv, void* out, float* lse,
+                                 float scale, void* stream) {
+  if (dh != kDh || BT < 1 || H < 1 || N < 1 || BT > 65535 || H > 65535) return (int)hipErrorInvalidValue;
+  NEST_DT(dtype, attn_fwd_t, BT, H, N, qkv, out, lse, scale, (hipStream_t)stream);
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+static void attn_bwd_t(int BT, int H, int N, const void* qkv, const void* out, const void* dout, const float* lse,
+                       float* delta, void* dqkv, float scale, hipStream_t st) {
+  const size_t rows = (size_t)BT * N * H;
+  hipLaunchKernelGGL(nest_attn_delta_kernel<T>, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, BT, H, N,
+                     (const T*)out, (const T*)dout, delta);
+  const dim3 g((N + kTile - 1) / kTile, H, BT);
+  const float sl2 = scale * 1.4426950408889634f;
+  hipLaunchKernelGGL(nest_attn_bwd_dq_kernel<T>, g, dim3(256), 0, st, BT, H, N, (const T*)qkv, (const T*)dout, lse,
+                     (const float*)delta, (T*)dqkv, sl2, scale);
+  hipLaunchKernelGGL(nest_attn_bwd_dkdv_kernel<T>, g, dim3(256), 0, st, BT, H, N, (const T*)qkv, (const T*)dout, lse,
+                     (const float*)delta, (T*)dqkv, sl2, scale);
+}
+VLP_EXPORT int vlp_nest_attn_bwd(int dtype, int BT, int H, int N, int dh, const void* qkv, const void* out,
+                                 const void* dout, const float* lse, float* delta, void* dqkv, float scale,
+                                 void* stream) {
+  if (dh != kDh || BT < 1 || H < 1 || N < 1 || BT > 65535 || H > 65535) return (int)hipErrorInvalidValue;
+  NEST_DT(dtype, attn_bwd_t, BT, H, N, qkv, out, dout, lse, delta, dqkv, scale, (hipStream_t)stream);
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+static void blockify_t(int B, int Hg, int Wg, int bs, int C, const void* x, const float* pos, void* y, int inv,
+                       hipStream_t st) {
+  const size_t n = (size_t)B * Hg * bs * Wg * bs * (C / (16 / (int)sizeof(T)));
+  hipLaunchKernelGGL(nest_blockify_kernel<T>, ew(n), dim3(256), 0, st, B, Hg, Wg, bs, C, (const T*)x, pos, (T*)y,
+                     inv);
+}
+VLP_EXPORT int vlp_nest_blockify(int dtype, int B, int Hg, int Wg, int bs, int C, const void* x, const float* pos,
+                                 void* y, int inverse, void* stream) {
+  if (C % (dtype == VLP_BF16 ? 8 : 4) || (inverse && pos)) return (int)hipErrorInvalidValue;
+  NEST_DT(dtype, blockify_t, B, Hg, Wg, bs, C, x, pos, y, inverse, (hipStream_t)stream);
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+static void pos_grad_t(int B, int TN, int C, const void* dy, float* dpos, hipStream_t st) {
+  hipLaunchKernelGGL(nest_pos_grad_kernel<T>, ew((size_t)TN * C), dim3(256), 0, st, B, TN, C, (const T*)dy, dpos);
+}
+VLP_EXPORT int vlp_nest_pos_grad(int dtype, int B, int TN, int C, const void* dy, float* dpos, void* stream) {
+  NEST_DT(dtype, pos_grad_t, B, TN, C, dy, dpos, (hipStream_t)stream);
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+static void mp_fwd_t(int B, int H, int W, int C, const void* x, void* y, uint8_t* idx, hipStream_t st) {
+  const size_t n = (size_t)B * ((H + 1) / 2) * ((W + 1) / 2) * C;
+  hipLaunchKernelGGL(nest_maxpool_fwd_kernel<T>, ew(n), dim3(256), 0, st, B, H, W, C, (const T*)x, (T*)y, idx);
+}
+VLP_EXPORT int vlp_nest_maxpool_fwd(int dtype, int B, int H, int W, int C, const void* x, void* y, uint8_t* idx,
+                                    void* stream) {
+  NEST_DT(dtype, mp_fwd_t, B, H, W, C, x, y, idx, (hipStream_t)stream);
+  return (int)hipGetLastError();
+}
+template <typename T>
+static void mp_bwd_t(int B, int H, int W, int C, const void* dy, const uint8_t* idx, void* dx, hipStream_t st) {
+  hipLaunchKernelGGL(nest_maxpool_bwd_kernel<T>, ew((size_t)B * H * W * C), dim3(256), 0, st, B, H, W, C,
+                     (const T*)dy, idx, (T*)dx);
+}
+VLP_EXPORT int vlp_nest_maxpool_bwd(int dtype, int B, int H, int W, int C, const void* dy, const uint8_t* idx,
+                                    void* dx, void* stream) {
+  NEST_DT(dtype, mp_bwd_t, B, H, W, C, dy, idx, dx, (hipStream_t)stream);
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+static void patch_t(int B, int H, int W, int bs, const float* x, const uint8_t* xu8, float mean, float std_,
+                    void* out, hipStream_t st) {
+  hipLaunchKernelGGL(nest_patch_prep_kernel<T>, ew((size_t)B * (H / 4) * (W / 4) * 48), dim3(256), 0, st, B, H, W,
+                     bs, x, xu8, mean, 1.f / std_, (T*)out);
+}
+VLP_EXPORT int vlp_nest_patch_prep(int dtype, int B, int H, int W, int bs, const float* x, const uint8_t* x_u8,
+                                   float mean, float std_, void* out, void* stream) {
+  if (H % 4 || W % 4 || (H / 4) % bs || (W / 4) % bs || (!x) == (!x_u8)) return (int)hipErrorInvalidValue;
+  NEST_DT(dtype, patch_t, B, H, W, bs, x, x_u8, mean, std_, out, (hipStream_t)stream);
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+static void bias_t(long long M, int N, void* y, const float* b, hipStream_t st) {
+  hipLaunchKernelGGL(nest_add_bias_kernel<T>, ew((size_t)M * N), dim3(256), 0, st, (size_t)M, N, (T*)y, b);
+}
+VLP_EXPORT int vlp_nest_add_bias(int dtype, long long M, int N, void* y, const float* bias, void* stream) {
+  NEST_DT(dtype, bias_t, M, N, y, bias, (hipStream_t)stream);
+  return (int)hipGetLastError();
+}
+
+VLP_EXPORT int vlp_nest_permute_cols(int dtype_out, int Nr, int H, int Dh, const float* src, void* dst,
+                                     void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 g = ew((size_t)Nr * H * Dh);
+  if (dtype_out == VLP_BF16)
+    hipLaunchKernelGGL((nest_permute_cols_kernel<float, bf16>), g, dim3(256), 0, st, Nr, H, Dh, src, (bf16*)dst, 0);
+  else
+    hipLaunchKernelGGL((nest_permute_cols_kernel<float, float>), g, dim3(256), 0, st, Nr, H, Dh, src, (float*)dst,
+                       0);
+  return (int)hipGetLastError();
+}
+VLP_EXPORT int vlp_nest_unpermute_cols(int Nr, int H, int Dh, const float* src, float* dst, void* stream) {
+  hipLaunchKernelGGL((nest_permute_cols_kernel<float, float>), ew((size_t)Nr * H * Dh), dim3(256), 0,
+                     (hipStream_t)stream, Nr, H, Dh, src, dst, 1);
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+static void rowscale_t(long long M, int N, int rows, const float* s, void* x, void* y, int mode, hipStream_t st) {
+  hipLaunchKernelGGL(nest_rowscale_kernel<T>, ew((size_t)M * N), dim3(256), 0, st, (size_t)M, N, rows, s, (T*)x,
+                     (T*)y, mode);
+}
+VLP_EXPORT int vlp_nest_rowscale(int dtype, long long M, int N, int rows, const float* s, void* x, void* y, int mode,
+                                 void* stream) {
+  NEST_DT(dtype, rowscale_t, M, N, rows, s, x, y, mode, (hipStream_t)stream);
+  return (int)hipGetLastError();
+}
+
+template <typename T>
+static void bcast_t(int B, int HW, int C, const float* dfeat, float inv, void* dy, hipStream_t st) {
+  hipLaunchKernelGGL(nest_bcast_kernel<T>, ew((size_t)B * HW * C), dim3(256), 0, st, B, HW, C, dfeat, inv, (T*)dy);
+}
+VLP_EXPORT int vlp_nest_bcast(int dtype, int B, int HW, int C, const float* dfeat, float inv, void* dy,
+                              void* stream) {
+  NEST_DT(dtype, bcast_t, B, HW, C, dfeat, inv, dy, (hipStream_t)stream);
+  return (int)hipGetLastError();
+}

@@ -495,3 +495,59 @@ def sim_topk(q, keys, K):
         linear_fwd(q[r0:r0 + r], keys, None, tile, r, N, E, ldy=Np)
         lib().vlp_row_topk(r, N, ptr(tile), Np, K, ptr(vals[r0:r0 + r]), ptr(idx[r0:r0 + r]), _s())
     return vals, idx.long()
+
+
+# ---------------- NesT image encoder ----------------
+def nest_attn_fwd(qkv, out, lse, BT, H, N, scale):
+    tk = ktimer.begin("nest_attn_fwd", 4.0 * BT * H * N * N * 32)
+    lib().vlp_nest_attn_fwd(dcode(qkv), BT, H, N, 32, ptr(qkv), ptr(out), ptr(lse), float(scale), _s())
+    ktimer.end(tk)
+
+
+def nest_attn_bwd(qkv, out, dout, lse, delta, dqkv, BT, H, N, scale):
+    tk = ktimer.begin("nest_attn_bwd", 10.0 * BT * H * N * N * 32)
+    lib().vlp_nest_attn_bwd(dcode(qkv), BT, H, N, 32, ptr(qkv), ptr(out), ptr(dout), ptr(lse), ptr(delta),
+                            ptr(dqkv), float(scale), _s())
+    ktimer.end(tk)
+
+
+def nest_blockify(x, y, B, Hg, Wg, bs, C, pos=None, inverse=False):
+    lib().vlp_nest_blockify(dcode(x), B, Hg, Wg, bs, C, ptr(x), ptr(pos), ptr(y), int(inverse), _s())
+
+
+def nest_pos_grad(dy, dpos, B, TN, C):
+    lib().vlp_nest_pos_grad(dcode(dy), B, TN, C, ptr(dy), ptr(dpos), _s())
+
+
+def nest_maxpool_fwd(x, y, idx):
+    B, H, W, C = x.shape
+    lib().vlp_nest_maxpool_fwd(dcode(x), B, H, W, C, ptr(x), ptr(y), ptr(idx), _s())
+
+
+def nest_maxpool_bwd(dy, idx, dx):
+    B, H, W, C = dx.shape
+    lib().vlp_nest_maxpool_bwd(dcode(dy), B, H, W, C, ptr(dy), ptr(idx), ptr(dx), _s())
+
+
+def nest_patch_prep(out, B, H, W, bs, x=None, x_u8=None, mean=0.0, std=1.0):
+    lib().vlp_nest_patch_prep(dcode(out), B, H, W, bs, ptr(x), ptr(x_u8), float(mean), float(std), ptr(out), _s())
+
+
+def nest_add_bias(y, bias, M, N):
+    lib().vlp_nest_add_bias(dcode(y), M, N, ptr(y), ptr(bias), _s())
+
+
+def nest_permute_cols(src, dst, Nr, H, Dh):
+    lib().vlp_nest_permute_cols(dcode(dst), Nr, H, Dh, ptr(src), ptr(dst), _s())
+
+
+def nest_unpermute_cols(src, dst, Nr, H, Dh):
+    lib().vlp_nest_unpermute_cols(Nr, H, Dh, ptr(src), ptr(dst), _s())
+
+
+def nest_rowscale(x, y, s, M, N, rows, mode):
+    lib().vlp_nest_rowscale(dcode(x), M, N, rows, ptr(s), ptr(x), ptr(y), int(mode), _s())
+
+
+def nest_bcast(dfeat, dy, B, HW, C, inv):
+    lib().vlp_nest_bcast(dcode(dy), B, HW, C, ptr(dfeat), float(inv), ptr(dy), _s())
