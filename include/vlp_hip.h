@@ -225,6 +225,10 @@ int vlp_layernorm_bwd(int dtype, int M, int D, const void* dy, float p_out,
                       unsigned long long seed_out, const void* x, const float* mean,
                       const float* rstd, const float* gamma, void* dx, void* dxd, float p_in,
                       unsigned long long seed_in, float* dgamma, float* dbeta, void* stream);
+/* dx = LayerNorm backward + addend (pre-norm residual: NesT's x + attn(norm1(x))) */
+int vlp_layernorm_bwd_add(int dtype, int M, int D, const void* dy, const void* x, const float* mean,
+                          const float* rstd, const float* gamma, const void* addend, void* dx,
+                          float* dgamma, float* dbeta, void* stream);
 int vlp_attn_fwd(int dtype, int B, int T, int H, int dh, const void* qkv, const long long* amask,
                  void* ctx, float* P, float scale, float p, unsigned long long seed, void* stream);
 int vlp_attn_bwd(int dtype, int B, int T, int H, int dh, const void* qkv, const float* P,

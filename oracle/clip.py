@@ -77,9 +77,14 @@ def recall_at_k(image_embeddings, text_embeddings, ks):
 
 
 class _ImageEncoder(nn.Module):           # :27-35
-    def __init__(self, drop_rate=0.0):
+    def __init__(self, drop_rate=0.0, model="resnet34", img_size=224):
         super().__init__()
-        self.model = ResNet34(drop_rate=drop_rate)
+        if model == "resnet34":
+            self.model = ResNet34(drop_rate=drop_rate)
+        else:                                 # timm nest_small restated (oracle/nest.py)
+            from oracle.nest import nest_small
+            assert model == "nest_small", model
+            self.model = nest_small(img_size=img_size, drop_rate=drop_rate)
 
     def forward(self, x):
         return self.model(x)
@@ -100,12 +105,14 @@ class OracleVLP(nn.Module):
     (image_encoder.model.*, text_encoder.model.*, image_projection,
     text_projection, logit_scale; :98-111)."""
 
-    def __init__(self, embedding_dim=128, text_dropout=0.1, image_dropout=0.0):
+    def __init__(self, embedding_dim=128, text_dropout=0.1, image_dropout=0.0, image_model="resnet34",
+                 img_size=224):
         super().__init__()
-        self.image_encoder = _ImageEncoder(image_dropout)
+        self.image_encoder = _ImageEncoder(image_dropout, image_model, img_size)
         self.text_encoder = _TextEncoder(text_dropout)
-        self.image_projection = nn.Parameter(torch.empty(512, embedding_dim))
-        nn.init.normal_(self.image_projection, std=512 ** -0.5)
+        di = self.image_encoder.model.num_features
+        self.image_projection = nn.Parameter(torch.empty(di, embedding_dim))
+        nn.init.normal_(self.image_projection, std=di ** -0.5)
         self.text_projection = nn.Parameter(torch.empty(312, embedding_dim))
         nn.init.normal_(self.text_projection, std=312 ** -0.5)
         # float64, as in the reference: torch.tensor([np.log(1/0.07)]) (:111) is fp64, which

@@ -1,0 +1,143 @@
+"""NesT image tower (vlp_amd/nest.py) and the NesT + TinyBERT contrastive step
+against the plain-torch restatement of timm nest_small (oracle/nest.py; timm
+itself is absent, so NesT parity is UNPINNED against timm -- these tests pin the
+HIP path to the restatement, whose layout/keys match timm's).
+
+Shapes: img 64 (patch grid 16: 16 blocks of 4x4 tokens, 4 blocks at level 1, 1
+at level 2), img 96 (blocks of 6x6 = 36 tokens: partial attention tiles) and
+img 128 (8x8 = 64-token blocks: one full tile).  Weights: the tower's own timm
+initialisation, copied into the oracle.  DropPath (timm default rate 0.5) is
+exercised in train mode by replaying the tower's per-sample masks in the oracle.
+
+Tolerances: fp32 features rel-L2 <= 1e-4 against the fp64 oracle and every
+parameter gradient rel-L2 <= 1e-3 (GELU / softmax / LayerNorm are smooth; only
+a max-pool tie could move a gradient discontinuously); bf16 features <= 5e-2 (24 layers of bf16 activations; measured 3.2e-2),
+gradients <= 0.1 per tensor with >= 90 % of tensors <= 5e-2.
+"""
+import functools
+
+import pytest
+import torch
+
+from tests.golden.synth import synth_batch
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def make_pair(img, dtype, seed=0):
+    import oracle.nest as on
+    from vlp_amd.nest import NestTower
+    torch.manual_seed(seed)
+    t = NestTower("nest_small", img_size=img, compute_dtype=dtype, device="cuda")
+    o = on.nest_small(img_size=img).double()
+    o.load_state_dict({k: v.detach().double().cpu() for k, v in t.state_dict().items()})
+    return t, o
+
+
+def replay_masks(tower, oracle_model):
+    """Feed the tower's last DropPath masks to the oracle's layers."""
+    masks = tower.last_drop_masks
+    for i, lvl in enumerate(oracle_model.levels):
+        for j, layer in enumerate(lvl.transformer_encoder):
+            m = masks[i][j] if masks is not None else None
+            layer.masks = None if m is None else (m[0].double(), m[1].double())
+
+
+@pytest.mark.parametrize("img", [64, 96, 128])
+def test_tower_fp32_vs_oracle(img):
+    t, o = make_pair(img, "fp32", seed=img)
+    g = torch.Generator().manual_seed(img)
+    x = torch.randn(2, 3, img, img, generator=g)
+    # eval features (the linear-probe embedding)
+    t.eval(); o.eval()
+    with torch.no_grad():
+        f = t(x.cuda())
+        fo = o(x.double())
+    assert rel(f, fo) < 1e-4, rel(f, fo)
+    # train step with DropPath: features and every parameter gradient
+    t.train(); o.train()
+    w = torch.randn(2, 384, generator=g)
+    f = t(x.cuda())
+    (f * w.cuda()).sum().backward()
+    replay_masks(t, o)
+    fo = o(x.double())
+    (fo * w.double()).sum().backward()
+    assert rel(f.detach(), fo.detach()) < 1e-4
+    og = dict(o.named_parameters())
+    worst = max((rel(p.grad, og[k].grad), k) for k, p in t.named_parameters() if og[k].grad is not None
+                and og[k].grad.norm() > 0)
+    assert worst[0] < 1e-3, worst
+
+
+def test_tower_bf16_vs_oracle():
+    t, o = make_pair(128, "bf16", seed=5)
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 3, 128, 128, generator=g)
+    t.train(); o.train()
+    w = torch.randn(2, 384, generator=g)
+    f = t(x.cuda())
+    (f * w.cuda()).sum().backward()
+    replay_masks(t, o)
+    fo = o(x.double())
+    (fo * w.double()).sum().backward()
+    ef = rel(f.detach(), fo.detach())
+    assert ef < 5e-2, ef
+    og = dict(o.named_parameters())
+    errs = sorted((rel(p.grad, og[k].grad), k) for k, p in t.named_parameters() if og[k].grad is not None
+                  and og[k].grad.norm() > 0)
+    assert errs[-1][0] < 0.1, errs[-3:]
+    assert sum(e <= 5e-2 for e, _ in errs) >= 0.9 * len(errs), errs[-5:]
+
+
+def test_uint8_input_matches_float():
+    t, _ = make_pair(64, "fp32", seed=2)
+    t.eval()
+    g = torch.Generator().manual_seed(2)
+    xu = torch.randint(0, 256, (2, 1, 64, 64), generator=g, dtype=torch.uint8)
+    xf = ((xu.float() - 127.5) / 73.9).expand(2, 3, 64, 64).contiguous()
+    with torch.no_grad():
+        a = t(xu.cuda())
+        b = t(xf.cuda())
+    assert rel(a, b) < 1e-6
+
+
+def test_clip_step_nest_tinybert_vs_oracle():
+    """The VisionLanguageModule step with image_model="nest_small" (BASELINE
+    configs[3]: NesT-Small + TinyBERT) in fp32 against the oracle's step: loss
+    and every gradient (eval-mode BN-free tower: DropPath off via drop_path_rate=0,
+    text dropout off)."""
+    from oracle.clip import OracleVLP, compute_loss
+    from src.models.pretrain.VisionLanguageModule import VisionLanguageModule
+    torch.manual_seed(0)
+    m = VisionLanguageModule("nest_small", "tinybert", functools.partial(torch.optim.AdamW, lr=5e-5), False,
+                             False, 384, 312, 128, compute_dtype="fp32", text_dropout=0.0, image_size=64,
+                             drop_path_rate=0.0)
+    m.train()
+    o = OracleVLP(128, text_dropout=0.0, image_model="nest_small", img_size=64).double()
+    sd = {k: v.detach().double().cpu() for k, v in m.state_dict().items()}
+    missing = o.load_state_dict(sd, strict=False)
+    assert not missing.unexpected_keys, missing.unexpected_keys
+    o.train()
+    for lvl in o.image_encoder.model.levels:
+        for layer in lvl.transformer_encoder:
+            layer.drop_path = 0.0
+    b = synth_batch(6, 64, 12, 11)
+    loss, li, lt, ie, te = m.training_step_outputs(b)
+    loss.backward()
+    bo = {"x-ray": b["x-ray"].double(), "caption_tokenized": b["caption_tokenized"]}
+    logits, _, _ = o(bo)
+    lo, _, _ = compute_loss(logits)
+    lo.backward()
+    assert abs(loss.item() - lo.item()) < 1e-5, (loss.item(), lo.item())
+    og = dict(o.named_parameters())
+    # attention.self.key.bias: adding a constant to every key of a query leaves the
+    # softmax unchanged, so its true gradient is 0 and both sides hold rounding noise
+    worst = max((rel(p.grad, og[k].grad), k) for k, p in m.named_parameters()
+                if p.grad is not None and og[k].grad is not None and og[k].grad.norm() > 0
+                and not k.endswith("attention.self.key.bias"))
+    assert worst[0] < 2e-3, worst

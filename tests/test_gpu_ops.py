@@ -57,6 +57,8 @@ CONV_CASES = [
     (2, 12, 12, 256, 256, 3, 3, 1, 1),  # M, N >= 256: 256x256 large-tile kernel (bf16)
     (4, 7, 7, 512, 512, 3, 3, 1, 1),    # layer 4 at 224 px, B = 4
     (4, 14, 14, 256, 512, 3, 3, 2, 1),  # layer-4 stride-2 block at 224 px
+    (2, 16, 16, 96, 192, 3, 3, 1, 1),   # NesT ConvPool (C = 96: K-steps straddle filter taps)
+    (2, 8, 8, 192, 384, 3, 3, 1, 1),    # NesT ConvPool, level 2
 ]
 
 

@@ -127,7 +127,7 @@ layernorm_bwd_kernel(int M, int D, const T* __restrict__ dy, float p_out, uint64
                      const T* __restrict__ x, const float* __restrict__ mean,
                      const float* __restrict__ rstd, const float* __restrict__ gamma,
                      T* __restrict__ dx, T* __restrict__ dxd, float p_in, uint64_t seed_in,
-                     float* dgamma, float* dbeta) {
+                     float* dgamma, float* dbeta, const T* __restrict__ addend) {
   // one wave per row; lane l owns columns l + 64j (j < kLnCols, D <= 512),
   // so the gamma/beta gradient partials live in registers across the wave's
   // rows and meet once per block (LDS) before one atomic per column
@@ -169,7 +169,9 @@ layernorm_bwd_kernel(int M, int D, const T* __restrict__ dy, float p_out, uint64
       const int c = l + 64 * j;
       if (c < D) {
         const float d = rs * (g[j] * gm[j] - a - xh[j] * b);
-        dx[(size_t)row * D + c] = from_f<T>(d);
+        // (the addend -- a pre-norm residual branch's gradient -- joins dx only;
+        // dxd stays the LN part)
+        dx[(size_t)row * D + c] = from_f<T>(addend ? d + to_f(addend[(size_t)row * D + c]) : d);
         if (dxd) {
           const float dd = p_in > 0.f ? d * drop_scale(seed_in, (uint64_t)row * D + c, p_in) : d;
           dxd[(size_t)row * D + c] = from_f<T>(dd);
@@ -722,11 +724,11 @@ VLP_EXPORT int vlp_layernorm_fwd(int dtype, int M, int D, const void* x, const f
   return (int)hipGetLastError();
 }
 
-VLP_EXPORT int vlp_layernorm_bwd(int dtype, int M, int D, const void* dy, float p_out,
-                                 unsigned long long seed_out, const void* x, const float* mean,
-                                 const float* rstd, const float* gamma, void* dx, void* dxd,
-                                 float p_in, unsigned long long seed_in, float* dgamma, float* dbeta,
-                                 void* stream) {
+static int layernorm_bwd_launch(int dtype, int M, int D, const void* dy, float p_out,
+                                unsigned long long seed_out, const void* x, const float* mean,
+                                const float* rstd, const float* gamma, void* dx, void* dxd,
+                                float p_in, unsigned long long seed_in, float* dgamma, float* dbeta,
+                                const void* addend, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (D > 512) return (int)hipErrorInvalidValue;
   int blocks = (M + 15) / 16;   // 4 rows per wave
@@ -735,12 +737,27 @@ VLP_EXPORT int vlp_layernorm_bwd(int dtype, int M, int D, const void* dy, float 
   if (dtype == VLP_BF16)
     hipLaunchKernelGGL(layernorm_bwd_kernel<bf16>, dim3(blocks), dim3(256), lds, st, M, D,
                        (const bf16*)dy, p_out, seed_out, (const bf16*)x, mean, rstd, gamma, (bf16*)dx,
-                       (bf16*)dxd, p_in, seed_in, dgamma, dbeta);
+                       (bf16*)dxd, p_in, seed_in, dgamma, dbeta, (const bf16*)addend);
   else
     hipLaunchKernelGGL(layernorm_bwd_kernel<float>, dim3(blocks), dim3(256), lds, st, M, D,
                        (const float*)dy, p_out, seed_out, (const float*)x, mean, rstd, gamma,
-                       (float*)dx, (float*)dxd, p_in, seed_in, dgamma, dbeta);
+                       (float*)dx, (float*)dxd, p_in, seed_in, dgamma, dbeta, (const float*)addend);
   return (int)hipGetLastError();
+}
+VLP_EXPORT int vlp_layernorm_bwd(int dtype, int M, int D, const void* dy, float p_out,
+                                 unsigned long long seed_out, const void* x, const float* mean,
+                                 const float* rstd, const float* gamma, void* dx, void* dxd,
+                                 float p_in, unsigned long long seed_in, float* dgamma, float* dbeta,
+                                 void* stream) {
+  return layernorm_bwd_launch(dtype, M, D, dy, p_out, seed_out, x, mean, rstd, gamma, dx, dxd, p_in, seed_in,
+                              dgamma, dbeta, nullptr, stream);
+}
+// pre-norm residual form: dx = LN backward + addend (NesT: x + attn(norm1(x)))
+VLP_EXPORT int vlp_layernorm_bwd_add(int dtype, int M, int D, const void* dy, const void* x, const float* mean,
+                                     const float* rstd, const float* gamma, const void* addend, void* dx,
+                                     float* dgamma, float* dbeta, void* stream) {
+  return layernorm_bwd_launch(dtype, M, D, dy, 0.f, 0, x, mean, rstd, gamma, dx, nullptr, 0.f, 0, dgamma, dbeta,
+                              addend, stream);
 }
 
 template <typename T, int TB>

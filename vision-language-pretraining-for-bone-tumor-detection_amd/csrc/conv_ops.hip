@@ -1371,10 +1371,14 @@ static int conv_fwd_t(const void* x, const void* wp, void* y, ConvGeom g, const 
     ConvFwdA<T, true> la{g, (const T*)x, sc, sh};
     return gemm_auto<T>(g.M, g.Co, g.K, 1, la, lb, ep, st);
   }
+  ConvFwdA<T, false> la{g, (const T*)x, nullptr, nullptr};
   if constexpr (std::is_same<T, bf16>::value) {
     if (rows_c64_ok(g)) return launch_rows_c64(g, x, wp, 0, ep, st);
+    // the LDS-DMA loaders take ONE filter tap per 64-deep K-step; a channel
+    // count that is not a multiple of 64 (NesT's 96-channel ConvPool input)
+    // takes the register-staged engine, which resolves the tap per 16-B chunk
+    if (g.C % 64) return launch_gemm<T, 128, 128, 2>(g.M, g.Co, g.K, 1, la, lb, ep, st);
   }
-  ConvFwdA<T, false> la{g, (const T*)x, nullptr, nullptr};
   return gemm_auto<T>(g.M, g.Co, g.K, 1, la, lb, ep, st);
 }
 
@@ -1384,6 +1388,7 @@ static int conv_dgrad_t(const void* dy, const void* wt, void* dx, ConvGeom g, co
                         const float* invstd, double* s1, double* s2, int rep, hipStream_t st) {
   g.M = g.N * g.H * g.W;
   g.K = g.KH * g.KW * g.Co;
+  if (std::is_same<T, bf16>::value && g.Co % 64) return (int)hipErrorInvalidValue;   // one tap per K-step
   if (g.S == 2) {
     // four parity classes, each a dense GEMM over its valid taps only
     for (int ph = 0; ph < 2; ++ph)

@@ -37,6 +37,7 @@ if _PKG not in sys.path:
 from vlp_amd import ops  # noqa: E402
 from vlp_amd.clip_model import ClipHead, ClipStepFn, _project_normalize  # noqa: E402
 from vlp_amd.optim import FusedAdamW  # noqa: E402
+from vlp_amd.nest import NEST_CFGS, NestTower  # noqa: E402
 from vlp_amd.resnet34 import ResNet34Tower  # noqa: E402
 from vlp_amd.tinybert import TinyBertConfig, TinyBertTower  # noqa: E402
 
@@ -89,10 +90,19 @@ class ImageEncoder(nn.Module):
 
     def __init__(self, model, compute_dtype="bf16", device=None, **kwargs):
         super().__init__()
-        if model != "resnet34":
-            raise ValueError(f"ImageEncoder: model {model} is not built for MI355X (supported: resnet34)")
-        self.model = ResNet34Tower(drop_rate=kwargs.get("drop_rate", 0.0), compute_dtype=compute_dtype,
+        if model == "resnet34":
+            self.model = ResNet34Tower(drop_rate=kwargs.get("drop_rate", 0.0), compute_dtype=compute_dtype,
+                                       device=device)
+        elif model in NEST_CFGS:
+            # timm nest defaults: img_size 224, drop_path_rate 0.5 (SURVEY §8(f) row 2:
+            # 512 x 512 inputs need img_size=512, passed through the module's image_size)
+            self.model = NestTower(model, img_size=kwargs.get("img_size", 224),
+                                   drop_rate=kwargs.get("drop_rate", 0.0),
+                                   drop_path_rate=kwargs.get("drop_path_rate", 0.5), compute_dtype=compute_dtype,
                                    device=device)
+        else:
+            raise ValueError(f"ImageEncoder: model {model} is not built for MI355X "
+                             f"(supported: resnet34, {', '.join(NEST_CFGS)})")
 
     def forward(self, x):
         return self.model(x)
@@ -253,10 +263,16 @@ class VisionLanguageModule(_Base):
         else:
             self.save_hyperparameters(hp, logger=False)
         dev = _default_device(device)
-        if image_embedding_dim != 512 or text_embedding_dim != 312:
-            raise ValueError("MI355X build: resnet34 (512) + tinybert (312) feature dims")
-        self.image_encoder = ImageEncoder(image_model, compute_dtype=compute_dtype, device=dev,
-                                          drop_rate=image_encoder_droupout)        # :98
+        enc_kw = {"drop_rate": image_encoder_droupout}                                # :98
+        if "image_size" in kwargs:          # timm img_size (NesT needs it for 512 x 512 inputs)
+            enc_kw["img_size"] = kwargs["image_size"]
+        if "drop_path_rate" in kwargs:
+            enc_kw["drop_path_rate"] = kwargs["drop_path_rate"]
+        self.image_encoder = ImageEncoder(image_model, compute_dtype=compute_dtype, device=dev, **enc_kw)
+        feat_dim = self.image_encoder.model.num_features if image_model != "resnet34" else 512
+        if image_embedding_dim != feat_dim or text_embedding_dim != 312:
+            raise ValueError(f"MI355X build: {image_model} ({feat_dim}) + tinybert (312) feature dims, got "
+                             f"image_embedding_dim={image_embedding_dim}, text_embedding_dim={text_embedding_dim}")
         self.text_encoder = TextEncoder(text_encoder_model, compute_dtype=compute_dtype, device=dev,
                                         dropout=text_dropout)                        # :99
         # projections + logit scale (:102-111) live in one arena; registered here so

@@ -134,7 +134,8 @@ class ClipStepFn(torch.autograd.Function):
         B, Tn = input_ids.shape
         D, E = txt_t.cfg.hidden, head.embedding_dim
         wT = head.wcopy()
-        ie, inorm = _project_normalize(head, wT, feat_img, 512, 512, "image_projection", E)
+        Di = head.image_dim
+        ie, inorm = _project_normalize(head, wT, feat_img, Di, Di, "image_projection", E)
         te, tnorm = _project_normalize(head, wT, h_last, D, D, "text_projection", E)
         rank, world = vdist.world()
         ie_all = vdist.all_gather_rows(ie)
@@ -170,7 +171,8 @@ class ClipStepFn(torch.autograd.Function):
         gs = dloss.reshape(1).float().contiguous()
         head.arena.grad.zero_()
         ops.scale(small[2:3], gs, head.arena.gview("logit_scale"))
-        dfeat_img = _project_backward(head, wT, feat_img, 512, 512, "image_projection", E, ie, inorm,
+        Di = head.image_dim
+        dfeat_img = _project_backward(head, wT, feat_img, Di, Di, "image_projection", E, ie, inorm,
                                       g_img, gs)
         dcls = _project_backward(head, wT, h_last, D, D, "text_projection", E, te, tnorm,
                                  g_txt, gs)

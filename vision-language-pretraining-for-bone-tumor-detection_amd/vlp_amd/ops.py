@@ -551,3 +551,8 @@ def nest_rowscale(x, y, s, M, N, rows, mode):
 
 def nest_bcast(dfeat, dy, B, HW, C, inv):
     lib().vlp_nest_bcast(dcode(dy), B, HW, C, ptr(dfeat), float(inv), ptr(dy), _s())
+
+
+def layernorm_bwd_add(dy, x, mean, rstd, gamma, addend, dx, dgamma, dbeta, M, D):
+    lib().vlp_layernorm_bwd_add(dcode(dy), M, D, ptr(dy), ptr(x), ptr(mean), ptr(rstd), ptr(gamma), ptr(addend),
+                                ptr(dx), ptr(dgamma), ptr(dbeta), _s())
