@@ -49,7 +49,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--image-model", default="resnet34", choices=["resnet34", "nest_small"],
+                    help="image tower: resnet34 (BASELINE configs[1]) or nest_small (configs[3], bs=128)")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 256; 128 for nest_small)")
     ap.add_argument("--image-size", type=int, default=512)
     ap.add_argument("--seq-len", type=int, default=40)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
@@ -59,13 +61,30 @@ def parse():
                          "the reference's fp32 3-channel batch")
     ap.add_argument("--no-loss-check", dest="loss_check", action="store_false",
                     help="skip the bf16-vs-fp32-oracle loss comparison on the bench batch")
-    ap.add_argument("--cpu-sample-batch", type=int, default=32)
+    ap.add_argument("--cpu-sample-batch", type=int, default=None,
+                    help="CPU-baseline sample batch (default 32; 4 for nest_small)")
     ap.add_argument("--cpu-sample-steps", type=int, default=3)
     ap.add_argument("--roofline-kernel", default="auto")
     ap.add_argument("--kernel-report", default="")
     ap.add_argument("--pcie-steps", type=int, default=5,
                     help="steps timed with the batch copied from pinned host memory (0: skip)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    nest = a.image_model != "resnet34"
+    if a.batch is None:
+        a.batch = 128 if nest else 256
+    if a.cpu_sample_batch is None:
+        a.cpu_sample_batch = 4 if nest else 32
+    return a
+
+
+def flop_per_pair(args):
+    """ResNet34 113.60 + TinyBERT 1.117 + head GFLOP per pair at 512^2
+    (FlopCounterMode); NesT: vlp_amd.nest.nest_flops_per_image (GEMMs, convs and
+    attention, backward = 2x forward) + TinyBERT."""
+    if args.image_model == "resnet34":
+        return FLOP_PER_PAIR_512 * (args.image_size / 512) ** 2
+    from vlp_amd.nest import nest_flops_per_image
+    return nest_flops_per_image(args.image_model, args.image_size) + 1.117e9
 
 
 def setup_dist(args):
@@ -112,13 +131,17 @@ def loss_delta_vs_fp32(args, model, host):
     saved = (cfg.hidden_dropout, cfg.attention_dropout)
     cfg.hidden_dropout = cfg.attention_dropout = 0.0
     sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    nest = args.image_model != "resnet34"
+    if nest:   # no BatchNorm: eval mode keeps DropPath's random masks out of the comparison
+        model.eval()
     with torch.no_grad():
         loss, li, lt, ie, te = model.training_step_outputs(host)
         loss, ie, te = loss.item(), ie.float().cpu(), te.float().cpu()
+    model.train()
     cfg.hidden_dropout, cfg.attention_dropout = saved
-    o = OracleVLP(128, text_dropout=0.0)
-    o.load_state_dict(sd)
-    o.train()
+    o = OracleVLP(128, text_dropout=0.0, image_model=args.image_model, img_size=args.image_size)
+    o.load_state_dict(sd, strict=False)
+    o.train(not nest)
     x = host["x-ray"] if "x-ray" in host else normalize_u8(host["x-ray-u8"])
     t0 = time.perf_counter()
     with torch.no_grad():
@@ -139,8 +162,9 @@ def cpu_baseline(args):
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     torch.set_num_threads(threads)
     B, H, T = args.cpu_sample_batch, args.image_size, args.seq_len
-    model = OracleVLP(128, text_dropout=0.1)
-    W.apply_recipe(model, 0)
+    model = OracleVLP(128, text_dropout=0.1, image_model=args.image_model, img_size=H)
+    if args.image_model == "resnet34":
+        W.apply_recipe(model, 0)
     model.train()
     opt = torch.optim.AdamW(model.param_groups(), lr=5e-5)
     batch = synth_batch(B, H, T, 0)
@@ -264,8 +288,13 @@ def main():
 
     dev = torch.device("cuda", local)
     torch.manual_seed(1234 + rank)
-    model = VisionLanguageModule("resnet34", "tinybert", functools.partial(torch.optim.AdamW, lr=5e-5),
-                                 False, False, 512, 312, 128, compute_dtype=args.dtype, device=dev)
+    if args.image_model == "resnet34":
+        model = VisionLanguageModule("resnet34", "tinybert", functools.partial(torch.optim.AdamW, lr=5e-5),
+                                     False, False, 512, 312, 128, compute_dtype=args.dtype, device=dev)
+    else:   # BASELINE configs[3]: timm nest_small at img_size = the batch resolution
+        model = VisionLanguageModule(args.image_model, "tinybert", functools.partial(torch.optim.AdamW, lr=5e-5),
+                                     False, False, 384, 312, 128, compute_dtype=args.dtype, device=dev,
+                                     image_size=args.image_size)
     model.train()
     opt = model.configure_optimizers()["optimizer"]
     batch = make_batch(args.batch, args.image_size, args.seq_len, dev, seed=rank, form=args.input)
@@ -360,12 +389,12 @@ def main():
                         if args.input == "u8" else "the reference's normalised 3-ch fp32 tensor")
                      + ", uploaded per step by the side-stream DevicePrefetcher inside the timed region; "
                        "seeded token ids; random-init weights)"),
-            "config": {"workload": "ResNet34+TinyBERT CLIP pretrain step (fwd+bwd+global-batch InfoNCE+AdamW)",
+            "config": {"workload": ("ResNet34" if args.image_model == "resnet34" else "NesT-Small")
+                       + "+TinyBERT CLIP pretrain step (fwd+bwd+global-batch InfoNCE+AdamW)",
                        "global_batch": world * args.batch, "per_gpu_batch": args.batch,
                        "image_size": args.image_size, "seq_len": args.seq_len,
                        "parallelism": f"dp{world}"},
-            "model_flops_frac": round(value * FLOP_PER_PAIR_512 * (args.image_size / 512) ** 2 / (world * peak * 1e12), 4)
-            if args.image_size == 512 else None,
+            "model_flops_frac": round(value * flop_per_pair(args) / (world * peak * 1e12), 4),
             "roofline": {"bound": "mfma", "kernel": tk, "achieved": round(achieved, 2), "peak": peak,
                          "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                          "avg_launch_us": round(ms_k * 1e3 / max(nl, 1), 2), "launches": nl,
