@@ -141,6 +141,13 @@ struct ConvFwdA {
     return ((s.mask >> st.tap) & 1u) ? s.base + st.delta : kOOB;
   }
 };
+// the same operand through register staging only (per-chunk filter tap): for
+// channel counts the one-tap-per-K-step LDS-DMA / direct loaders cannot take
+template <typename T>
+struct ConvFwdAReg : ConvFwdA<T, false> {
+  static constexpr bool kDirect = false;
+  static constexpr bool kBuf = false;
+};
 
 // ---- data-gradient A operand (stride 1): output-gradient "patches", K-contiguous ----
 template <typename T>
@@ -1377,7 +1384,10 @@ static int conv_fwd_t(const void* x, const void* wp, void* y, ConvGeom g, const 
     // the LDS-DMA loaders take ONE filter tap per 64-deep K-step; a channel
     // count that is not a multiple of 64 (NesT's 96-channel ConvPool input)
     // takes the register-staged engine, which resolves the tap per 16-B chunk
-    if (g.C % 64) return launch_gemm<T, 128, 128, 2>(g.M, g.Co, g.K, 1, la, lb, ep, st);
+    if (g.C % 64) {
+      ConvFwdAReg<T> lr{la};
+      return launch_gemm<T, 128, 128, 2>(g.M, g.Co, g.K, 1, lr, lb, ep, st);
+    }
   }
   return gemm_auto<T>(g.M, g.Co, g.K, 1, la, lb, ep, st);
 }
