@@ -373,7 +373,8 @@ def main():
         peak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
         achieved = (flop_k / (ms_k / 1e3)) / 1e12 if ms_k > 0 else 0.0
         res = {
-            "metric": "image-text pairs/sec (fwd+bwd) at bs=256/GPU, 1/2/4/8 MI355X",
+            # BASELINE.json's metric is quoted at bs=256 (ResNet34); other batches name theirs
+            "metric": f"image-text pairs/sec (fwd+bwd) at bs={args.batch}/GPU, 1/2/4/8 MI355X",
             "value": round(value, 2),
             "unit": "image-text pairs/s",
             "n_gpus": world,

@@ -25,26 +25,63 @@
 
 namespace vlp {
 
+constexpr int kDh = 32;                 // head dim (every NesT variant: C / heads = 32)
+constexpr int kTileRows = 64;           // key / query tokens per staged tile
+constexpr int kQBlock = 128;            // queries per forward / dQ workgroup (4 waves x 32)
+
 // ---------------- fragments (MFMA 16x16x32 bf16 / 16x16x4 f32) ----------------
 // Convention as bert_ops.hip: D[m][n] = sum_k X[m][k] Y[n][k]; lane l = 16g + i
-// holds D[4g + r][i].  kfrag: X rows r0.. of a row-major [row][k] image (k
-// contiguous); tfrag: X rows r0.. (the "mn" index) of a row-major [k][mn]
-// image, i.e. read transposed (ds_read_b64_tr_b16 for bf16).
+// holds D[4g + r][i].
+//
+// Tiles of 64 tokens x 32 channels are staged in LDS as [token][channel]
+// images.  bf16 images are unpadded 64-B rows whose four 16-B chunks are
+// XOR-swizzled by sw(row) = ((row>>2)&1)<<1 | ((row>>3)&1): the ds_read_b128
+// row read (16 consecutive rows, one chunk) and the ds_read_b64_tr_b16
+// transposed read (rows 4g + q of two groups, two adjacent chunks) are both
+// bank-conflict free on it.  fp32 images are padded rows of 36 floats.
+//
+// Score tiles never pass through LDS: an accumulator v4f s[b] (b = 0..3) holds
+// S[key 16b + 4g + r][i] (or S[q 16b + 4g + r][key i] in dK/dV), and the MFMA's
+// k-slot order is free as long as both operands agree, so pfrag() hands the
+// accumulators (as bf16) straight to the next product as the operand whose
+// k-slot j of lane group g is token 16(2h + j/4) + 4g + j%4; vtfrag() reads the
+// other operand (a [token][channel] image, channel on the lane) in that order.
 template <typename T> struct FA;
 template <> struct FA<bf16> {
-  static constexpr int KS = 32;
+  static constexpr int KS = 32, IMG = kTileRows * 32;
   typedef v8bf F;
-  __device__ static __forceinline__ F kfrag(const bf16* img, int ld, int r0, int k0) {
-    const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-    return *reinterpret_cast<const v8bf*>(img + (r0 + i) * ld + k0 + 8 * g);
+  __device__ static __forceinline__ int sw(int row) { return (((row >> 2) & 1) << 1) | ((row >> 3) & 1); }
+  __device__ static __forceinline__ int at(int row, int col) {
+    return row * 32 + ((((col >> 3) ^ sw(row)) << 3) | (col & 7));
   }
-  __device__ static __forceinline__ F tfrag(const bf16* img, int ld, int r0, int k0) {
+  // rows r0 + i, k = k0 + 8g .. +7 of an image (k0 = 0: one k-step spans the 32 channels)
+  __device__ static __forceinline__ F kfrag(const bf16* img, int r0, int k0) {
     const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-    const int q = i >> 2, p = i & 3;
-    const int k1 = k0 + 8 * g + q;
-    v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(img + k1 * ld + r0 + 4 * p));
-    v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(img + (k1 + 4) * ld + r0 + 4 * p));
+    return *reinterpret_cast<const v8bf*>(img + at(r0 + i, k0 + 8 * g));
+  }
+  // channels c0 + i (lane row), k-slots = tokens t0 + 16(j/4) + 4g + j%4
+  __device__ static __forceinline__ F vtfrag(const bf16* img, int t0, int c0) {
+    const int l = threadIdx.x & 63, g = l >> 4, q = (l >> 2) & 3, p = l & 3;
+    const int r = t0 + 4 * g + q, c = c0 + 4 * p;
+    v4bf lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(img + at(r, c)));
+    v4bf hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_v4bf*)(img + at(r + 16, c)));
     return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+  // accumulators s[2h], s[2h+1] as the operand of k-step h
+  __device__ static __forceinline__ F pfrag(const v4f* s, int h) {
+    F f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      f[r] = (bf16)s[2 * h][r];
+      f[4 + r] = (bf16)s[2 * h + 1][r];
+    }
+    return f;
+  }
+  __device__ static __forceinline__ F ones() {
+    F f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = (bf16)1.f;
+    return f;
   }
   // a fragment straight from global memory (rows r0.., k contiguous)
   __device__ static __forceinline__ F gfrag(const bf16* p, size_t ld, int r0, int k0, bool ok) {
@@ -57,19 +94,23 @@ template <> struct FA<bf16> {
   }
 };
 template <> struct FA<float> {
-  static constexpr int KS = 16;
+  static constexpr int KS = 16, LD = 36, IMG = kTileRows * LD;
   typedef v4f F;
-  __device__ static __forceinline__ F kfrag(const float* img, int ld, int r0, int k0) {
+  __device__ static __forceinline__ int at(int row, int col) { return row * LD + col; }
+  __device__ static __forceinline__ F kfrag(const float* img, int r0, int k0) {
     const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
-    return *reinterpret_cast<const v4f*>(img + (r0 + i) * ld + k0 + 4 * g);
+    return *reinterpret_cast<const v4f*>(img + at(r0 + i, k0 + 4 * g));
   }
-  __device__ static __forceinline__ F tfrag(const float* img, int ld, int r0, int k0) {
+  // element j of lane (g, i): image[t0 + 4g + j][c0 + i]  (mma j: k-slot g)
+  __device__ static __forceinline__ F vtfrag(const float* img, int t0, int c0) {
     const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
     F f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) f[j] = img[(k0 + 4 * g + j) * ld + r0 + i];
+    for (int j = 0; j < 4; ++j) f[j] = img[at(t0 + 4 * g + j, c0 + i)];
     return f;
   }
+  __device__ static __forceinline__ F pfrag(const v4f* s, int h) { return s[h]; }
+  __device__ static __forceinline__ F ones() { return F{1.f, 1.f, 1.f, 1.f}; }
   __device__ static __forceinline__ F gfrag(const float* p, size_t ld, int r0, int k0, bool ok) {
     const int l = threadIdx.x & 63, i = l & 15, g = l >> 4;
     if (!ok) return F{0.f, 0.f, 0.f, 0.f};
@@ -81,19 +122,42 @@ template <> struct FA<float> {
   }
 };
 
+// single-instruction maxima (fmaxf on MFMA results otherwise gets a
+// canonicalising v_max per operand)
+__device__ __forceinline__ float max2_(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float max3_(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+// maximum of the 16 scores a lane holds
+__device__ __forceinline__ float max16(const v4f* s) {
+  float m = max3_(s[0][0], s[0][1], s[0][2]);
+  m = max3_(m, s[0][3], s[1][0]);
+  m = max3_(m, s[1][1], s[1][2]);
+  m = max3_(m, s[1][3], s[2][0]);
+  m = max3_(m, s[2][1], s[2][2]);
+  m = max3_(m, s[2][3], s[3][0]);
+  m = max3_(m, s[3][1], s[3][2]);
+  return max2_(m, s[3][3]);
+}
 __device__ __forceinline__ float q4max(float v) {
-  v = fmaxf(v, __shfl_xor(v, 16, 64));
-  return fmaxf(v, __shfl_xor(v, 32, 64));
+  v = max2_(v, __shfl_xor(v, 16, 64));
+  return max2_(v, __shfl_xor(v, 32, 64));
 }
 __device__ __forceinline__ float q4sum(float v) {
   v += __shfl_xor(v, 16, 64);
   return v + __shfl_xor(v, 32, 64);
 }
+// v_exp_f32: 2^x without OCML's denormal-range fix-up (results below 2^-126
+// flush to 0, far below what a bf16/fp32 softmax weight resolves)
+__device__ __forceinline__ float exp2_hw(float x) { return __builtin_amdgcn_exp2f(x); }
 
-constexpr int kDh = 32;                 // head dim (every NesT variant: C / heads = 32)
-constexpr int kTile = 64;               // tokens per tile (4 waves x 16)
-
-// four consecutive values of one row -> LDS (8 B bf16 / 16 B fp32)
+// four consecutive values of one row -> memory (8 B bf16 / 16 B fp32)
 template <typename T>
 __device__ __forceinline__ void st4(T* p, float a, float b, float c, float d);
 template <> __device__ __forceinline__ void st4<bf16>(bf16* p, float a, float b, float c, float d) {
@@ -105,100 +169,140 @@ template <> __device__ __forceinline__ void st4<float>(float* p, float a, float 
   *reinterpret_cast<v4f*>(p) = v4f{a, b, c, d};
 }
 
-// rows [t0, t0+64) x 32 channels (column offset col) of a [rows][ld] tensor ->
-// LDS image [64][LDI]; rows >= N are zero
-template <typename T, int LDI>
-__device__ __forceinline__ void stage_tile(T* img, const T* src, size_t ld, int col, int t0, int N) {
-  constexpr int EPC = 16 / (int)sizeof(T);            // elements per 16-B chunk
-  constexpr int CPR = kDh / EPC;                      // chunks per row
-  for (int q = threadIdx.x; q < kTile * CPR; q += blockDim.x) {
-    const int r = q / CPR, c = q - r * CPR;
-    uint4 v = zero4();
-    if (t0 + r < N) v = ldg16(src + (size_t)(t0 + r) * ld + col + c * EPC);
-    *reinterpret_cast<uint4*>(img + r * LDI + c * EPC) = v;
+// Register-staged tile copy (issue the global loads early, write the LDS
+// image after the barrier): rows [t0, t0+64) x 32 channels at column `col` of a
+// [rows][ld] tensor; rows >= N are zero in the image.  The loads are
+// unconditional (row index clamped to N-1) so nothing waits on them before the
+// store; the store applies the row mask.  256 threads.
+template <typename T>
+struct TileStage {
+  static constexpr int EPC = 16 / (int)sizeof(T), CPR = kDh / EPC, CPT = kTileRows * CPR / 256;
+  uint4 v[CPT];
+  __device__ __forceinline__ void load(const T* src, size_t ld, int col, int t0, int N) {
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const int q = threadIdx.x + 256 * c, r = q / CPR, ch = q % CPR;
+      v[c] = ldg16(src + (size_t)min(t0 + r, N - 1) * ld + col + ch * EPC);
+    }
   }
-}
+  __device__ __forceinline__ void store(T* img, int t0, int N) const {
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      const int q = threadIdx.x + 256 * c, r = q / CPR, ch = q % CPR;
+      *reinterpret_cast<uint4*>(img + FA<T>::at(r, ch * EPC)) = t0 + r < N ? v[c] : zero4();
+    }
+  }
+};
 
 // ---------------- forward ----------------
-// grid (ceil(N/64), H, BT); 4 waves, wave w owns queries qt*64 + 16w .. +15.
+// grid (ceil(N/128), H, BT); 4 waves, wave w owns queries qt*128 + 32w .. +31
+// as two 16-query subtiles that share every K / V fragment read.
 // out[bt*N + q][h*32 + d]; lse[(bt*H + h)*N + q] = log2-sum-exp of the scaled
-// (x log2 e) scores.
+// (x log2 e) scores.  Per key tile: S^T = K Q^T, the online softmax in
+// registers (lane = query, 16 keys per lane), O^T += V^T P^T with P fed from
+// the accumulators; the row sums come out of the same product with a ones
+// operand (1^T P^T), i.e. they sum exactly the weights O accumulates.
 template <typename T>
 __global__ void __launch_bounds__(256)
 nest_attn_fwd_kernel(int BT, int H, int N, const T* __restrict__ qkv, T* __restrict__ out,
                      float* __restrict__ lse, float sl2) {
   using M = FA<T>;
-  constexpr int PAD = 16 / (int)sizeof(T);
-  constexpr int LDK = kDh + PAD, LDP = kTile + PAD;
-  __shared__ __attribute__((aligned(16))) T sK[kTile * LDK];
-  __shared__ __attribute__((aligned(16))) T sV[kTile * LDK];
-  __shared__ __attribute__((aligned(16))) T sP[4][16 * LDP];
+  constexpr int QW = 2, KSN = kDh / M::KS;
+  __shared__ __attribute__((aligned(16))) T sK[M::IMG];
+  __shared__ __attribute__((aligned(16))) T sV[M::IMG];
   const int qt = blockIdx.x, h = blockIdx.y, bt = blockIdx.z;
   const int C = H * kDh;
   const size_t ld3 = 3 * (size_t)C;
   const T* base = qkv + (size_t)bt * N * ld3;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, li = l & 15, lg = l >> 4;
-  const int q0 = qt * kTile + 16 * w;
-  const bool qok = q0 + li < N;
-  typename M::F qf[kDh / M::KS];
+  const int q0 = qt * kQBlock + 32 * w;
+  typename M::F qf[QW][KSN];
 #pragma unroll
-  for (int ks = 0; ks < kDh / M::KS; ++ks) qf[ks] = M::gfrag(base + h * kDh, ld3, q0, ks * M::KS, qok);
-  float mi = -INFINITY, li_sum = 0.f;
-  v4f o[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
-  T* myP = sP[w];
-  const int nt = (N + kTile - 1) / kTile;
+  for (int u = 0; u < QW; ++u)
+#pragma unroll
+    for (int ks = 0; ks < KSN; ++ks)
+      qf[u][ks] = M::gfrag(base + h * kDh, ld3, q0 + 16 * u, ks * M::KS, q0 + 16 * u + li < N);
+  const typename M::F one = M::ones();
+  float mi[QW];
+  v4f o[QW][2], lsum[QW];
+#pragma unroll
+  for (int u = 0; u < QW; ++u) {
+    mi[u] = -INFINITY;
+    lsum[u] = o[u][0] = o[u][1] = v4f{0.f, 0.f, 0.f, 0.f};
+  }
+  const int nt = (N + kTileRows - 1) / kTileRows;
+  TileStage<T> stk, stv;
+  stk.load(base, ld3, C + h * kDh, 0, N);
+  stv.load(base, ld3, 2 * C + h * kDh, 0, N);
   for (int t = 0; t < nt; ++t) {
     __syncthreads();   // every wave is done with the previous tile
-    stage_tile<T, LDK>(sK, base, ld3, C + h * kDh, t * kTile, N);
-    stage_tile<T, LDK>(sV, base, ld3, 2 * C + h * kDh, t * kTile, N);
+    stk.store(sK, t * kTileRows, N);
+    stv.store(sV, t * kTileRows, N);
     __syncthreads();
-    v4f s[4];
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      s[b] = v4f{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < kDh / M::KS; ++ks) M::mma(s[b], M::kfrag(sK, LDK, 16 * b, ks * M::KS), qf[ks]);
-    }
-    float mx = -INFINITY;
-#pragma unroll
-    for (int b = 0; b < 4; ++b)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = t * kTile + 16 * b + 4 * lg + r;
-        s[b][r] = key < N ? s[b][r] * sl2 : -INFINITY;
-        mx = fmaxf(mx, s[b][r]);
-      }
-    mx = q4max(mx);
-    const float mn = fmaxf(mi, mx);
-    const float alpha = mi == -INFINITY ? 0.f : exp2f(mi - mn);
-    float sum = 0.f;
+    // next tile's loads fly under this tile's MFMAs (unconditional: past the
+    // end they re-read row N-1, which keeps the loaded registers phi-free so
+    // nothing waits on them before the next store)
+    stk.load(base, ld3, C + h * kDh, (t + 1) * kTileRows, N);
+    stv.load(base, ld3, 2 * C + h * kDh, (t + 1) * kTileRows, N);
+    v4f s[QW][4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        s[b][r] = exp2f(s[b][r] - mn);
-        sum += s[b][r];
+      for (int u = 0; u < QW; ++u) s[u][b] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KSN; ++ks) {
+        const typename M::F kf = M::kfrag(sK, 16 * b, ks * M::KS);
+#pragma unroll
+        for (int u = 0; u < QW; ++u) M::mma(s[u][b], kf, qf[u][ks]);
       }
-      st4<T>(myP + li * LDP + 16 * b + 4 * lg, s[b][0], s[b][1], s[b][2], s[b][3]);
     }
-    li_sum = li_sum * alpha + q4sum(sum);
-    mi = mn;
+    if (t * kTileRows + kTileRows > N) {   // partial last tile: keys >= N take no weight
 #pragma unroll
-    for (int db = 0; db < 2; ++db) o[db] *= alpha;
-    // O^T[d][q] += sum_key V^T[d][key] P[q][key]
+      for (int b = 0; b < 4; ++b)
 #pragma unroll
-    for (int db = 0; db < 2; ++db)
+        for (int r = 0; r < 4; ++r)
+          if (t * kTileRows + 16 * b + 4 * lg + r >= N)
 #pragma unroll
-      for (int ks = 0; ks < kTile; ks += M::KS)
-        M::mma(o[db], M::tfrag(sV, LDK, 16 * db, ks), M::kfrag(myP, LDP, 0, ks));
+            for (int u = 0; u < QW; ++u) s[u][b][r] = -INFINITY;
+    }
+#pragma unroll
+    for (int u = 0; u < QW; ++u) {
+      const float mn = max2_(mi[u], q4max(max16(s[u])) * sl2);   // running max of the scaled scores
+      const float alpha = exp2_hw(mi[u] - mn);                   // 0 on the first tile (mi = -inf)
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[u][b][r] = exp2_hw(fmaf(s[u][b][r], sl2, -mn));
+      mi[u] = mn;
+      o[u][0] *= alpha;
+      o[u][1] *= alpha;
+      lsum[u] *= alpha;
+    }
+    // O^T[d][q] += sum_key V^T[d][key] P[q][key];  l[q] += sum_key P[q][key]
+#pragma unroll
+    for (int hs = 0; hs < kTileRows / M::KS; ++hs) {
+      const typename M::F v0 = M::vtfrag(sV, hs * M::KS, 0), v1 = M::vtfrag(sV, hs * M::KS, 16);
+#pragma unroll
+      for (int u = 0; u < QW; ++u) {
+        const typename M::F pf = M::pfrag(s[u], hs);
+        M::mma(o[u][0], v0, pf);
+        M::mma(o[u][1], v1, pf);
+        M::mma(lsum[u], one, pf);
+      }
+    }
   }
-  if (qok) {
-    const float inv = 1.f / li_sum;
-    T* dst = out + ((size_t)bt * N + q0 + li) * C + h * kDh;
 #pragma unroll
-    for (int db = 0; db < 2; ++db)
-      st4<T>(dst + 16 * db + 4 * lg, o[db][0] * inv, o[db][1] * inv, o[db][2] * inv, o[db][3] * inv);
-    if (lg == 0) lse[((size_t)bt * H + h) * N + q0 + li] = mi + log2f(li_sum);
+  for (int u = 0; u < QW; ++u) {
+    const int q = q0 + 16 * u + li;
+    if (q < N) {
+      const float inv = 1.f / lsum[u][0];
+      T* dst = out + ((size_t)bt * N + q) * C + h * kDh;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+        st4<T>(dst + 16 * db + 4 * lg, o[u][db][0] * inv, o[u][db][1] * inv, o[u][db][2] * inv,
+               o[u][db][3] * inv);
+      if (lg == 0) lse[((size_t)bt * H + h) * N + q] = mi[u] + log2f(lsum[u][0]);
+    }
   }
 }
 
@@ -229,158 +333,222 @@ __global__ void nest_attn_delta_kernel(int BT, int H, int N, const T* __restrict
 }
 
 // ---------------- backward: dQ over key tiles ----------------
-// grid (ceil(N/64), H, BT); wave w owns queries qt*64 + 16w .. +15.
-//   P = exp2(S*sl2 - lse), dP = dO V^T, dS = P (dP - delta), dQ = scale dS K
+// grid (ceil(N/128), H, BT); wave w owns queries qt*128 + 32w .. +31 as two
+// 16-query subtiles (lane = query) sharing the K / V fragment reads.
+//   P = exp2(S*sl2 - lse), dP' = dO V^T - delta (the accumulator starts at
+//   -delta), dS = P dP', dQ^T += K^T dS^T with dS fed from the accumulators.
 template <typename T>
 __global__ void __launch_bounds__(256)
 nest_attn_bwd_dq_kernel(int BT, int H, int N, const T* __restrict__ qkv, const T* __restrict__ dout,
                         const float* __restrict__ lse, const float* __restrict__ delta, T* __restrict__ dqkv,
                         float sl2, float scale) {
   using M = FA<T>;
-  constexpr int PAD = 16 / (int)sizeof(T);
-  constexpr int LDK = kDh + PAD, LDP = kTile + PAD;
-  __shared__ __attribute__((aligned(16))) T sK[kTile * LDK];
-  __shared__ __attribute__((aligned(16))) T sV[kTile * LDK];
-  __shared__ __attribute__((aligned(16))) T sP[4][16 * LDP];
+  constexpr int QW = 2, KSN = kDh / M::KS;
+  __shared__ __attribute__((aligned(16))) T sK[M::IMG];
+  __shared__ __attribute__((aligned(16))) T sV[M::IMG];
   const int qt = blockIdx.x, h = blockIdx.y, bt = blockIdx.z;
   const int C = H * kDh;
   const size_t ld3 = 3 * (size_t)C;
   const T* base = qkv + (size_t)bt * N * ld3;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, li = l & 15, lg = l >> 4;
-  const int q0 = qt * kTile + 16 * w;
-  const bool qok = q0 + li < N;
-  typename M::F qf[kDh / M::KS], df[kDh / M::KS];
+  const int q0 = qt * kQBlock + 32 * w;
+  typename M::F qf[QW][KSN], df[QW][KSN];
+  float lq[QW], ndl[QW];
 #pragma unroll
-  for (int ks = 0; ks < kDh / M::KS; ++ks) {
-    qf[ks] = M::gfrag(base + h * kDh, ld3, q0, ks * M::KS, qok);
-    df[ks] = M::gfrag(dout + (size_t)bt * N * C + h * kDh, C, q0, ks * M::KS, qok);
+  for (int u = 0; u < QW; ++u) {
+    const int q = q0 + 16 * u;
+    const bool ok = q + li < N;
+#pragma unroll
+    for (int ks = 0; ks < KSN; ++ks) {
+      qf[u][ks] = M::gfrag(base + h * kDh, ld3, q, ks * M::KS, ok);
+      df[u][ks] = M::gfrag(dout + (size_t)bt * N * C + h * kDh, C, q, ks * M::KS, ok);
+    }
+    const size_t so = ((size_t)bt * H + h) * N + q + li;
+    lq[u] = ok ? lse[so] : INFINITY;
+    ndl[u] = ok ? -delta[so] : 0.f;
   }
-  const size_t so = ((size_t)bt * H + h) * N + q0 + li;
-  const float lq = qok ? lse[so] : INFINITY;
-  const float dq_ = qok ? delta[so] : 0.f;
-  v4f acc[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
-  T* myP = sP[w];
-  const int nt = (N + kTile - 1) / kTile;
+  v4f acc[QW][2];
+#pragma unroll
+  for (int u = 0; u < QW; ++u) acc[u][0] = acc[u][1] = v4f{0.f, 0.f, 0.f, 0.f};
+  const int nt = (N + kTileRows - 1) / kTileRows;
+  TileStage<T> stk, stv;
+  stk.load(base, ld3, C + h * kDh, 0, N);
+  stv.load(base, ld3, 2 * C + h * kDh, 0, N);
   for (int t = 0; t < nt; ++t) {
     __syncthreads();
-    stage_tile<T, LDK>(sK, base, ld3, C + h * kDh, t * kTile, N);
-    stage_tile<T, LDK>(sV, base, ld3, 2 * C + h * kDh, t * kTile, N);
+    stk.store(sK, t * kTileRows, N);
+    stv.store(sV, t * kTileRows, N);
     __syncthreads();
+    stk.load(base, ld3, C + h * kDh, (t + 1) * kTileRows, N);
+    stv.load(base, ld3, 2 * C + h * kDh, (t + 1) * kTileRows, N);
+    v4f ds[QW][4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
-      v4f s = v4f{0.f, 0.f, 0.f, 0.f}, dp = s;
+      v4f sc[QW], dp[QW];
 #pragma unroll
-      for (int ks = 0; ks < kDh / M::KS; ++ks) {
-        M::mma(s, M::kfrag(sK, LDK, 16 * b, ks * M::KS), qf[ks]);
-        M::mma(dp, M::kfrag(sV, LDK, 16 * b, ks * M::KS), df[ks]);
+      for (int u = 0; u < QW; ++u) {
+        sc[u] = v4f{0.f, 0.f, 0.f, 0.f};
+        dp[u] = v4f{ndl[u], ndl[u], ndl[u], ndl[u]};
       }
-      float ds[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = t * kTile + 16 * b + 4 * lg + r;
-        const float p = key < N ? exp2f(s[r] * sl2 - lq) : 0.f;
-        ds[r] = p * (dp[r] - dq_);
+      for (int ks = 0; ks < KSN; ++ks) {
+        const typename M::F kf = M::kfrag(sK, 16 * b, ks * M::KS), vf = M::kfrag(sV, 16 * b, ks * M::KS);
+#pragma unroll
+        for (int u = 0; u < QW; ++u) {
+          M::mma(sc[u], kf, qf[u][ks]);
+          M::mma(dp[u], vf, df[u][ks]);
+        }
       }
-      st4<T>(myP + li * LDP + 16 * b + 4 * lg, ds[0], ds[1], ds[2], ds[3]);
+#pragma unroll
+      for (int u = 0; u < QW; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ds[u][b][r] = exp2_hw(fmaf(sc[u][r], sl2, -lq[u])) * dp[u][r];
+    }
+    if (t * kTileRows + kTileRows > N) {   // keys >= N (zero rows) carry no probability
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (t * kTileRows + 16 * b + 4 * lg + r >= N)
+#pragma unroll
+            for (int u = 0; u < QW; ++u) ds[u][b][r] = 0.f;
     }
     // dQ^T[d][q] += sum_key K^T[d][key] dS[q][key]
 #pragma unroll
-    for (int db = 0; db < 2; ++db)
+    for (int hs = 0; hs < kTileRows / M::KS; ++hs) {
+      const typename M::F k0 = M::vtfrag(sK, hs * M::KS, 0), k1 = M::vtfrag(sK, hs * M::KS, 16);
 #pragma unroll
-      for (int ks = 0; ks < kTile; ks += M::KS)
-        M::mma(acc[db], M::tfrag(sK, LDK, 16 * db, ks), M::kfrag(myP, LDP, 0, ks));
+      for (int u = 0; u < QW; ++u) {
+        const typename M::F pf = M::pfrag(ds[u], hs);
+        M::mma(acc[u][0], k0, pf);
+        M::mma(acc[u][1], k1, pf);
+      }
+    }
   }
-  if (qok) {
-    T* dst = dqkv + ((size_t)bt * N + q0 + li) * ld3 + h * kDh;
 #pragma unroll
-    for (int db = 0; db < 2; ++db)
-      st4<T>(dst + 16 * db + 4 * lg, acc[db][0] * scale, acc[db][1] * scale, acc[db][2] * scale,
-             acc[db][3] * scale);
+  for (int u = 0; u < QW; ++u) {
+    const int q = q0 + 16 * u + li;
+    if (q < N) {
+      T* dst = dqkv + ((size_t)bt * N + q) * ld3 + h * kDh;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+        st4<T>(dst + 16 * db + 4 * lg, acc[u][db][0] * scale, acc[u][db][1] * scale, acc[u][db][2] * scale,
+               acc[u][db][3] * scale);
+    }
   }
 }
 
 // ---------------- backward: dK, dV over query tiles ----------------
-// grid (ceil(N/64), H, BT); wave w owns keys kt*64 + 16w .. +15.
-//   dV = P^T dO, dK = scale dS^T Q
+// grid (ceil(N/64), H, BT); wave w owns keys kt*64 + 16w .. +15 (lane = key;
+// two key subtiles per wave measured slower: 188 VGPRs halve the occupancy).
+//   S[q][key] = Q K^T and dP[q][key] - delta[q] as accumulators (row q =
+//   16b + 4g + r), P and dS from them, then dV^T += dO^T P and dK^T += Q^T dS
+//   with P / dS fed from the accumulators.  Query rows >= N are zero in the
+//   images with lse = +inf, so they carry no probability.
 template <typename T>
 __global__ void __launch_bounds__(256)
 nest_attn_bwd_dkdv_kernel(int BT, int H, int N, const T* __restrict__ qkv, const T* __restrict__ dout,
                           const float* __restrict__ lse, const float* __restrict__ delta,
                           T* __restrict__ dqkv, float sl2, float scale) {
   using M = FA<T>;
-  constexpr int PAD = 16 / (int)sizeof(T);
-  constexpr int LDK = kDh + PAD, LDQ = 16 + PAD;
-  __shared__ __attribute__((aligned(16))) T sQ[kTile * LDK];
-  __shared__ __attribute__((aligned(16))) T sD[kTile * LDK];
-  __shared__ __attribute__((aligned(16))) T sPt[4][kTile * LDQ];   // P^T as [q][key16]
-  __shared__ __attribute__((aligned(16))) T sSt[4][kTile * LDQ];   // dS^T as [q][key16]
-  __shared__ float sL[kTile], sDl[kTile];
+  constexpr int KW = 1, KSN = kDh / M::KS;
+  __shared__ __attribute__((aligned(16))) T sQ[M::IMG];
+  __shared__ __attribute__((aligned(16))) T sD[M::IMG];
+  __shared__ __attribute__((aligned(16))) float sL[kTileRows], sDl[kTileRows];
   const int kt = blockIdx.x, h = blockIdx.y, bt = blockIdx.z;
   const int C = H * kDh;
   const size_t ld3 = 3 * (size_t)C;
   const T* base = qkv + (size_t)bt * N * ld3;
   const T* dbase = dout + (size_t)bt * N * C;
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63, li = l & 15, lg = l >> 4;
-  const int k0 = kt * kTile + 16 * w;
-  const bool kok = k0 + li < N;
-  typename M::F kf[kDh / M::KS], vf[kDh / M::KS];
+  const int k0 = kt * 64 * KW + 16 * KW * w;
+  typename M::F kf[KW][KSN], vf[KW][KSN];
 #pragma unroll
-  for (int ks = 0; ks < kDh / M::KS; ++ks) {
-    kf[ks] = M::gfrag(base + C + h * kDh, ld3, k0, ks * M::KS, kok);
-    vf[ks] = M::gfrag(base + 2 * C + h * kDh, ld3, k0, ks * M::KS, kok);
-  }
-  v4f dk[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
-  v4f dv[2] = {v4f{0.f, 0.f, 0.f, 0.f}, v4f{0.f, 0.f, 0.f, 0.f}};
-  T* myP = sPt[w];
-  T* myS = sSt[w];
+  for (int u = 0; u < KW; ++u)
+#pragma unroll
+    for (int ks = 0; ks < KSN; ++ks) {
+      const bool ok = k0 + 16 * u + li < N;
+      kf[u][ks] = M::gfrag(base + C + h * kDh, ld3, k0 + 16 * u, ks * M::KS, ok);
+      vf[u][ks] = M::gfrag(base + 2 * C + h * kDh, ld3, k0 + 16 * u, ks * M::KS, ok);
+    }
+  v4f dk[KW][2], dv[KW][2];
+#pragma unroll
+  for (int u = 0; u < KW; ++u) dk[u][0] = dk[u][1] = dv[u][0] = dv[u][1] = v4f{0.f, 0.f, 0.f, 0.f};
   const size_t sb = ((size_t)bt * H + h) * N;
-  const int nt = (N + kTile - 1) / kTile;
+  const int nt = (N + kTileRows - 1) / kTileRows;
+  TileStage<T> stq, std_;
+  float pl = 0.f, pd = 0.f;
+  auto load_rows = [&](int t0) {
+    stq.load(base, ld3, h * kDh, t0, N);
+    std_.load(dbase, C, h * kDh, t0, N);
+    const int q = min(t0 + (int)(threadIdx.x & (kTileRows - 1)), N - 1);   // every thread: no phi
+    pl = lse[sb + q];
+    pd = delta[sb + q];
+  };
+  load_rows(0);
   for (int t = 0; t < nt; ++t) {
     __syncthreads();
-    stage_tile<T, LDK>(sQ, base, ld3, h * kDh, t * kTile, N);
-    stage_tile<T, LDK>(sD, dbase, C, h * kDh, t * kTile, N);
-    if (threadIdx.x < kTile) {
-      const int q = t * kTile + threadIdx.x;
-      sL[threadIdx.x] = q < N ? lse[sb + q] : INFINITY;
-      sDl[threadIdx.x] = q < N ? delta[sb + q] : 0.f;
+    stq.store(sQ, t * kTileRows, N);
+    std_.store(sD, t * kTileRows, N);
+    if (threadIdx.x < kTileRows) {
+      const bool ok = t * kTileRows + (int)threadIdx.x < N;
+      sL[threadIdx.x] = ok ? pl : INFINITY;
+      sDl[threadIdx.x] = ok ? -pd : 0.f;
     }
     __syncthreads();
-    // S^T[key][q] (lane: keys 4lg+r of the wave's 16, query 16b + li)
+    load_rows((t + 1) * kTileRows);
+    v4f p[KW][4], ds[KW][4];
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
-      v4f s = v4f{0.f, 0.f, 0.f, 0.f}, dp = s;
+      const v4f lq = *reinterpret_cast<const v4f*>(sL + 16 * b + 4 * lg);
+      const v4f ndl = *reinterpret_cast<const v4f*>(sDl + 16 * b + 4 * lg);
+      v4f sc[KW], dp[KW];
 #pragma unroll
-      for (int ks = 0; ks < kDh / M::KS; ++ks) {
-        M::mma(s, kf[ks], M::kfrag(sQ, LDK, 16 * b, ks * M::KS));
-        M::mma(dp, vf[ks], M::kfrag(sD, LDK, 16 * b, ks * M::KS));
+      for (int u = 0; u < KW; ++u) {
+        sc[u] = v4f{0.f, 0.f, 0.f, 0.f};
+        dp[u] = ndl;
       }
-      const int q = 16 * b + li;
-      const float lq = sL[q], dl = sDl[q];
-      float p[4], ds[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        p[r] = exp2f(s[r] * sl2 - lq);
-        ds[r] = p[r] * (dp[r] - dl);
+      for (int ks = 0; ks < KSN; ++ks) {
+        const typename M::F qa = M::kfrag(sQ, 16 * b, ks * M::KS), da = M::kfrag(sD, 16 * b, ks * M::KS);
+#pragma unroll
+        for (int u = 0; u < KW; ++u) {
+          M::mma(sc[u], qa, kf[u][ks]);
+          M::mma(dp[u], da, vf[u][ks]);
+        }
       }
-      st4<T>(myP + q * LDQ + 4 * lg, p[0], p[1], p[2], p[3]);
-      st4<T>(myS + q * LDQ + 4 * lg, ds[0], ds[1], ds[2], ds[3]);
+#pragma unroll
+      for (int u = 0; u < KW; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          p[u][b][r] = exp2_hw(fmaf(sc[u][r], sl2, -lq[r]));
+          ds[u][b][r] = p[u][b][r] * dp[u][r];
+        }
     }
-    // dV^T[d][key] += sum_q dO^T[d][q] P^T[key][q];  dK^T[d][key] += sum_q Q^T[d][q] dS^T[key][q]
+    // dV^T[d][key] += sum_q dO^T[d][q] P[q][key];  dK^T[d][key] += sum_q Q^T[d][q] dS[q][key]
 #pragma unroll
-    for (int db = 0; db < 2; ++db)
+    for (int hs = 0; hs < kTileRows / M::KS; ++hs)
 #pragma unroll
-      for (int ks = 0; ks < kTile; ks += M::KS) {
-        M::mma(dv[db], M::tfrag(sD, LDK, 16 * db, ks), M::tfrag(myP, LDQ, 0, ks));
-        M::mma(dk[db], M::tfrag(sQ, LDK, 16 * db, ks), M::tfrag(myS, LDQ, 0, ks));
+      for (int db = 0; db < 2; ++db) {
+        const typename M::F dt = M::vtfrag(sD, hs * M::KS, 16 * db), qt_ = M::vtfrag(sQ, hs * M::KS, 16 * db);
+#pragma unroll
+        for (int u = 0; u < KW; ++u) {
+          M::mma(dv[u][db], dt, M::pfrag(p[u], hs));
+          M::mma(dk[u][db], qt_, M::pfrag(ds[u], hs));
+        }
       }
   }
-  if (kok) {
-    T* dst = dqkv + ((size_t)bt * N + k0 + li) * ld3 + h * kDh;
 #pragma unroll
-    for (int db = 0; db < 2; ++db) {
-      st4<T>(dst + C + 16 * db + 4 * lg, dk[db][0] * scale, dk[db][1] * scale, dk[db][2] * scale,
-             dk[db][3] * scale);
-      st4<T>(dst + 2 * C + 16 * db + 4 * lg, dv[db][0], dv[db][1], dv[db][2], dv[db][3]);
+  for (int u = 0; u < KW; ++u) {
+    const int key = k0 + 16 * u + li;
+    if (key < N) {
+      T* dst = dqkv + ((size_t)bt * N + key) * ld3 + h * kDh;
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        st4<T>(dst + C + 16 * db + 4 * lg, dk[u][db][0] * scale, dk[u][db][1] * scale, dk[u][db][2] * scale,
+               dk[u][db][3] * scale);
+        st4<T>(dst + 2 * C + 16 * db + 4 * lg, dv[u][db][0], dv[u][db][1], dv[u][db][2], dv[u][db][3]);
+      }
     }
   }
 }
@@ -593,7 +761,7 @@ using namespace vlp;
 
 template <typename T>
 static void attn_fwd_t(int BT, int H, int N, const void* qkv, void* out, float* lse, float scale, hipStream_t st) {
-  hipLaunchKernelGGL(nest_attn_fwd_kernel<T>, dim3((N + kTile - 1) / kTile, H, BT), dim3(256), 0, st, BT, H, N,
+  hipLaunchKernelGGL(nest_attn_fwd_kernel<T>, dim3((N + kQBlock - 1) / kQBlock, H, BT), dim3(256), 0, st, BT, H, N,
                      (const T*)qkv, (T*)out, lse, scale * 1.4426950408889634f);
 }
 VLP_EXPORT int vlp_nest_attn_fwd(int dtype, int BT, int H, int N, int dh, const void* qkv, void* out, float* lse,
@@ -609,11 +777,11 @@ static void attn_bwd_t(int BT, int H, int N, const void* qkv, const void* out, c
   const size_t rows = (size_t)BT * N * H;
   hipLaunchKernelGGL(nest_attn_delta_kernel<T>, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, BT, H, N,
                      (const T*)out, (const T*)dout, delta);
-  const dim3 g((N + kTile - 1) / kTile, H, BT);
+  const dim3 gq((N + kQBlock - 1) / kQBlock, H, BT), gk((N + 63) / 64, H, BT);
   const float sl2 = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(nest_attn_bwd_dq_kernel<T>, g, dim3(256), 0, st, BT, H, N, (const T*)qkv, (const T*)dout, lse,
+  hipLaunchKernelGGL(nest_attn_bwd_dq_kernel<T>, gq, dim3(256), 0, st, BT, H, N, (const T*)qkv, (const T*)dout, lse,
                      (const float*)delta, (T*)dqkv, sl2, scale);
-  hipLaunchKernelGGL(nest_attn_bwd_dkdv_kernel<T>, g, dim3(256), 0, st, BT, H, N, (const T*)qkv, (const T*)dout, lse,
+  hipLaunchKernelGGL(nest_attn_bwd_dkdv_kernel<T>, gk, dim3(256), 0, st, BT, H, N, (const T*)qkv, (const T*)dout, lse,
                      (const float*)delta, (T*)dqkv, sl2, scale);
 }
 VLP_EXPORT int vlp_nest_attn_bwd(int dtype, int BT, int H, int N, int dh, const void* qkv, const void* out,
