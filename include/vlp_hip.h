@@ -205,6 +205,11 @@ int vlp_avgpool_fwd(int dtype, int N, int HW, int C, const void* x, void* feat, 
 int vlp_linear_fwd(int dtype, int M, int N, int K, const void* x, int ldx, const void* w,
                    const float* bias, void* y, int ldy, int mode, void* aux, const void* res,
                    int ldr, float p, unsigned long long seed, void* stream);
+/* y = res + rscale[row / rps] * (x W^T + bias): a residual branch under DropPath (NesT
+ * TransformerLayer, timm nest.py: x + drop_path(attn(norm1(x))); per-sample scale 0 or 1/(1-p)) */
+int vlp_linear_fwd_rs(int dtype, int M, int N, int K, const void* x, int ldx, const void* w,
+                      const float* bias, void* y, int ldy, const void* res, int ldr, const float* rscale,
+                      int rps, void* stream);
 /* dx = dy W; mode 1: dx *= gelu'(aux); mode 0: dx += addend (if non-NULL) */
 int vlp_linear_dgrad(int dtype, int M, int Kin, int Nout, const void* dy, int lddy, const void* w,
                      void* dx, int lddx, int mode, const void* aux, int ldaux, const void* addend,
@@ -229,6 +234,11 @@ int vlp_layernorm_bwd(int dtype, int M, int D, const void* dy, float p_out,
 int vlp_layernorm_bwd_add(int dtype, int M, int D, const void* dy, const void* x, const float* mean,
                           const float* rstd, const float* gamma, const void* addend, void* dx,
                           float* dgamma, float* dbeta, void* stream);
+/* the same, also writing dxs = rscale[row / rps] * dx: the DropPath-scaled gradient of the
+ * residual branch that produced x (NesT; saves a separate scaling pass) */
+int vlp_layernorm_bwd_add_rs(int dtype, int M, int D, const void* dy, const void* x, const float* mean,
+                             const float* rstd, const float* gamma, const void* addend, void* dx, void* dxs,
+                             const float* rscale, int rps, float* dgamma, float* dbeta, void* stream);
 int vlp_attn_fwd(int dtype, int B, int T, int H, int dh, const void* qkv, const long long* amask,
                  void* ctx, float* P, float scale, float p, unsigned long long seed, void* stream);
 int vlp_attn_bwd(int dtype, int B, int T, int H, int dh, const void* qkv, const float* P,

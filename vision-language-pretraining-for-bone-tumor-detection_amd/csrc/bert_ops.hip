@@ -32,6 +32,7 @@ struct EpiLinear {
   double* stat1 = nullptr; double* stat2 = nullptr;
   T* out; int ldo; const float* bias; int mode;
   T* aux; const T* res; int ldr; float p; uint64_t seed; int N;
+  const float* rscale = nullptr; int rps = 1;   // mode 2: out = rscale[row / rps] * v + res (DropPath)
   __device__ void operator()(int row, int col, v4f v, v4f&, v4f&) const {
     if (bias) v += *reinterpret_cast<const v4f*>(bias + col);
     if (mode == 1) {
@@ -43,6 +44,7 @@ struct EpiLinear {
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] *= drop_scale(seed, (uint64_t)row * N + col + j, p);
       }
+      if (rscale) v *= rscale[row / rps];
       v += load4(res + (size_t)row * ldr + col);
     }
     store4(out + (size_t)row * ldo + col, v);
@@ -91,99 +93,178 @@ static int gemm_lin(int M, int N, int K, int ksplit, const LA& la, const LB& lb,
 }
 
 // ---------------- LayerNorm over rows of D ----------------
-// one wave per row; fp32 statistics; saves mean/rstd.
-template <typename T>
-__global__ void layernorm_fwd_kernel(int M, int D, const T* __restrict__ x, const float* __restrict__ gamma,
-                                     const float* __restrict__ beta, float eps, T* __restrict__ y,
-                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                     float p, uint64_t seed) {
-  int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  int l = threadIdx.x & 63;
+// 16 lanes per row, 16-B chunks: lane j of a row owns chunks j, j+16, ...
+// (NCH of them, D = 8 * chunks for bf16 / 4 * chunks for fp32, D <= 512), so
+// a row is read once into registers and reduced with four 16-lane shuffles.
+// fp32 statistics; mean / rstd saved per row.
+// sum over a 16-lane row, result in every lane (DPP row_ror 8 / 4, then two
+// quad permutations: VALU only)
+__device__ __forceinline__ float row16_allsum(float x) {
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x128, 0xf, 0xf, false));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x124, 0xf, 0xf, false));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0xB1, 0xf, 0xf, false));
+  x += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x4E, 0xf, 0xf, false));
+  return x;
+}
+
+template <typename T, int NCH>
+__global__ void __launch_bounds__(256)
+layernorm_fwd_kernel(int M, int D, const T* __restrict__ x, const float* __restrict__ gamma,
+                     const float* __restrict__ beta, float eps, T* __restrict__ y,
+                     float* __restrict__ mean_out, float* __restrict__ rstd_out, float p, uint64_t seed) {
+  constexpr int E = Chunk<T>::N;
+  const int row = blockIdx.x * 16 + (threadIdx.x >> 4), j = threadIdx.x & 15;
   if (row >= M) return;
+  const int nch = D / E;
   const T* xr = x + (size_t)row * D;
+  float v[NCH][E];
   float s = 0.f;
-  for (int c = l; c < D; c += 64) s += to_f(xr[c]);
-  float mean = warp_sum(s) / D;
-  float v = 0.f;
-  for (int c = l; c < D; c += 64) { float d = to_f(xr[c]) - mean; v += d * d; }
-  float rstd = rsqrtf(warp_sum(v) / D + eps);
-  T* yr = y + (size_t)row * D;
-  for (int c = l; c < D; c += 64) {
-    float o = (to_f(xr[c]) - mean) * rstd * gamma[c] + beta[c];
-    if (p > 0.f) o *= drop_scale(seed, (uint64_t)row * D + c, p);
-    yr[c] = from_f<T>(o);
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = j + 16 * k;
+    if (c < nch) {
+      Chunk<T>::unpack(ldg16(xr + c * E), v[k]);
+#pragma unroll
+      for (int e = 0; e < E; ++e) s += v[k][e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < E; ++e) v[k][e] = 0.f;
+    }
   }
-  if (l == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+  const float mean = row16_allsum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k)
+    if (j + 16 * k < nch)
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const float d = v[k][e] - mean;
+        q += d * d;
+      }
+  const float rstd = rsqrtf(row16_allsum(q) / D + eps);
+  T* yr = y + (size_t)row * D;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = j + 16 * k;
+    if (c < nch) {
+      const v4f* g4 = reinterpret_cast<const v4f*>(gamma + c * E);
+      const v4f* b4 = reinterpret_cast<const v4f*>(beta + c * E);
+      float o[E];
+#pragma unroll
+      for (int h = 0; h < E / 4; ++h) {
+        const v4f g = g4[h], b = b4[h];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[4 * h + e] = (v[k][4 * h + e] - mean) * rstd * g[e] + b[e];
+      }
+      if (p > 0.f) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) o[e] *= drop_scale(seed, (uint64_t)row * D + c * E + e, p);
+      }
+      stg16(yr + c * E, Chunk<T>::pack(o));
+    }
+  }
+  if (j == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
 }
 
 // LN backward.  dy is the gradient of the LN output (before the output dropout
-// when p > 0: the dropout mask is re-generated from the seed).  Writes
-//   dx  = LN input gradient (+ addend, e.g. a residual branch)
-//   dxd = dx * dropout-mask (gradient of the dropped dense output), optional
-// and accumulates dgamma/dbeta.
-template <typename T>
+// when p_out > 0: the dropout mask is re-generated from the seed).  Writes
+//   dx  = LN input gradient (+ addend, e.g. a pre-norm residual's gradient)
+//   dxd = optional second output: with rscale, rscale[row / rps] * dx (the
+//         DropPath-scaled gradient of the residual branch that produced the
+//         LN input, NesT); otherwise the LN part times the input dropout mask
+// and accumulates dgamma/dbeta.  Same lane layout as the forward; rows are
+// strided over a capped grid so the gamma/beta partials stay in registers,
+// meet across the wave's four rows by shuffles and across the block in LDS,
+// then one atomic per column and block.
+template <typename T, int NCH>
 __global__ void __launch_bounds__(256)
 layernorm_bwd_kernel(int M, int D, const T* __restrict__ dy, float p_out, uint64_t seed_out,
                      const T* __restrict__ x, const float* __restrict__ mean,
                      const float* __restrict__ rstd, const float* __restrict__ gamma,
                      T* __restrict__ dx, T* __restrict__ dxd, float p_in, uint64_t seed_in,
-                     float* dgamma, float* dbeta, const T* __restrict__ addend) {
-  // one wave per row; lane l owns columns l + 64j (j < kLnCols, D <= 512),
-  // so the gamma/beta gradient partials live in registers across the wave's
-  // rows and meet once per block (LDS) before one atomic per column
-  constexpr int NJ = 8;
-  __shared__ float part[4][2][NJ * 64];
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float pg[NJ], pb[NJ], gm[NJ];
+                     float* dgamma, float* dbeta, const T* __restrict__ addend,
+                     const float* __restrict__ rscale, int rps) {
+  constexpr int E = Chunk<T>::N;
+  __shared__ float part[4][2][512];
+  const int j = threadIdx.x & 15, w = threadIdx.x >> 6;
+  const int nch = D / E;
+  float pg[NCH][E], pb[NCH][E], gm[NCH][E];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    pg[j] = pb[j] = 0.f;
-    const int c = l + 64 * j;
-    gm[j] = c < D ? gamma[c] : 0.f;
+  for (int k = 0; k < NCH; ++k) {
+    const int c = j + 16 * k;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      pg[k][e] = pb[k][e] = 0.f;
+      gm[k][e] = c < nch ? gamma[c * E + e] : 0.f;
+    }
   }
-  for (int row = blockIdx.x * 4 + w; row < M; row += gridDim.x * 4) {
+  for (int row = blockIdx.x * 16 + (threadIdx.x >> 4); row < M; row += gridDim.x * 16) {
     const T* xr = x + (size_t)row * D;
     const T* dyr = dy + (size_t)row * D;
     const float mu = mean[row], rs = rstd[row];
-    float g[NJ], xh[NJ];
+    float g[NCH][E], xh[NCH][E];
     float a = 0.f, b = 0.f;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int c = l + 64 * j;
-      g[j] = 0.f; xh[j] = 0.f;
-      if (c < D) {
-        g[j] = to_f(dyr[c]);
-        if (p_out > 0.f) g[j] *= drop_scale(seed_out, (uint64_t)row * D + c, p_out);
-        xh[j] = (to_f(xr[c]) - mu) * rs;
-      }
-      const float gg = g[j] * gm[j];
-      a += gg;
-      b += gg * xh[j];
-      pg[j] += g[j] * xh[j];
-      pb[j] += g[j];
-    }
-    a = warp_sum(a) / D;
-    b = warp_sum(b) / D;
+    for (int k = 0; k < NCH; ++k) {
+      const int c = j + 16 * k;
+      if (c < nch) {
+        Chunk<T>::unpack(ldg16(dyr + c * E), g[k]);
+        Chunk<T>::unpack(ldg16(xr + c * E), xh[k]);
+      } else {
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int c = l + 64 * j;
-      if (c < D) {
-        const float d = rs * (g[j] * gm[j] - a - xh[j] * b);
-        // (the addend -- a pre-norm residual branch's gradient -- joins dx only;
-        // dxd stays the LN part)
-        dx[(size_t)row * D + c] = from_f<T>(addend ? d + to_f(addend[(size_t)row * D + c]) : d);
+        for (int e = 0; e < E; ++e) g[k][e] = xh[k][e] = 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        if (p_out > 0.f && c < nch) g[k][e] *= drop_scale(seed_out, (uint64_t)row * D + c * E + e, p_out);
+        xh[k][e] = c < nch ? (xh[k][e] - mu) * rs : 0.f;
+        const float gg = g[k][e] * gm[k][e];
+        a += gg;
+        b += gg * xh[k][e];
+        pg[k][e] += g[k][e] * xh[k][e];
+        pb[k][e] += g[k][e];
+      }
+    }
+    a = row16_allsum(a) / D;
+    b = row16_allsum(b) / D;
+    const float rsc = rscale ? rscale[row / rps] : 0.f;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int c = j + 16 * k;
+      if (c < nch) {
+        float d[E], ad[E];
+        if (addend) Chunk<T>::unpack(ldg16(addend + (size_t)row * D + c * E), ad);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          d[e] = rs * (g[k][e] * gm[k][e] - a - xh[k][e] * b);
+          if (addend) ad[e] += d[e];   // (the addend joins dx; without rscale dxd stays the LN part)
+        }
+        stg16(dx + (size_t)row * D + c * E, Chunk<T>::pack(addend ? ad : d));
         if (dxd) {
-          const float dd = p_in > 0.f ? d * drop_scale(seed_in, (uint64_t)row * D + c, p_in) : d;
-          dxd[(size_t)row * D + c] = from_f<T>(dd);
+          float dd[E];
+#pragma unroll
+          for (int e = 0; e < E; ++e)
+            dd[e] = rscale ? rsc * (addend ? ad[e] : d[e])
+                           : (p_in > 0.f ? d[e] * drop_scale(seed_in, (uint64_t)row * D + c * E + e, p_in) : d[e]);
+          stg16(dxd + (size_t)row * D + c * E, Chunk<T>::pack(dd));
         }
       }
     }
   }
+  // the wave's four rows hold the same columns: fold lanes 16 apart, then waves in LDS
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    part[w][0][l + 64 * j] = pg[j];
-    part[w][1][l + 64 * j] = pb[j];
-  }
+  for (int k = 0; k < NCH; ++k)
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      float u = pg[k][e], t = pb[k][e];
+      u += __shfl_xor(u, 16, 64); u += __shfl_xor(u, 32, 64);
+      t += __shfl_xor(t, 16, 64); t += __shfl_xor(t, 32, 64);
+      const int c = j + 16 * k;
+      if ((threadIdx.x & 63) < 16 && c < nch) {
+        part[w][0][c * E + e] = u;
+        part[w][1][c * E + e] = t;
+      }
+    }
   __syncthreads();
   for (int c = threadIdx.x; c < D; c += blockDim.x) {
     atomicAdd(dgamma + c, part[0][0][c] + part[1][0][c] + part[2][0][c] + part[3][0][c]);
@@ -625,6 +706,25 @@ VLP_EXPORT int vlp_linear_fwd(int dtype, int M, int N, int K, const void* x, int
   return gemm_lin<float>(M, N, K, 1, la, lb, ep, st);
 }
 
+// residual + DropPath: y = res + rscale[row / rps] * (x W^T + bias)  (NesT
+// TransformerLayer: x + drop_path(branch), one per-sample scale 0 or 1/(1-p))
+VLP_EXPORT int vlp_linear_fwd_rs(int dtype, int M, int N, int K, const void* x, int ldx, const void* w,
+                                 const float* bias, void* y, int ldy, const void* res, int ldr,
+                                 const float* rscale, int rps, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (!rscale || rps < 1) return (int)hipErrorInvalidValue;
+  if (dtype == VLP_BF16) {
+    KMat<bf16> la{(const bf16*)x, ldx, M, K};
+    KMat<bf16> lb{(const bf16*)w, K, N, K};
+    EpiLinear<bf16> ep{nullptr, nullptr, (bf16*)y, ldy, bias, 2, nullptr, (const bf16*)res, ldr, 0.f, 0, N, rscale, rps};
+    return gemm_lin<bf16>(M, N, K, 1, la, lb, ep, st);
+  }
+  KMat<float> la{(const float*)x, ldx, M, K};
+  KMat<float> lb{(const float*)w, K, N, K};
+  EpiLinear<float> ep{nullptr, nullptr, (float*)y, ldy, bias, 2, nullptr, (const float*)res, ldr, 0.f, 0, N, rscale, rps};
+  return gemm_lin<float>(M, N, K, 1, la, lb, ep, st);
+}
+
 // dx[M][Kin] = dy[M][Nout] W[Nout][Kin]   (mode 1: * gelu'(aux))
 VLP_EXPORT int vlp_linear_dgrad(int dtype, int M, int Kin, int Nout, const void* dy, int lddy,
                                 const void* w, void* dx, int lddx, int mode, const void* aux,
@@ -710,38 +810,70 @@ VLP_EXPORT int vlp_colsum(int dtype, int M, int N, const void* x, int ld, float*
   return (int)hipGetLastError();
 }
 
+template <typename T, int NCH>
+static void ln_fwd_t(int M, int D, const void* x, const float* gamma, const float* beta, float eps, void* y,
+                     float* mean, float* rstd, float p, unsigned long long seed, hipStream_t st) {
+  hipLaunchKernelGGL((layernorm_fwd_kernel<T, NCH>), dim3((M + 15) / 16), dim3(256), 0, st, M, D, (const T*)x, gamma,
+                     beta, eps, (T*)y, mean, rstd, p, (uint64_t)seed);
+}
+// chunks per lane: ceil(D / (16 elements-per-chunk... x 16 lanes))
+static int ln_nch(int dtype, int D) {
+  const int e = dtype == VLP_BF16 ? 8 : 4;
+  if (D < 1 || D > 512 || D % e) return -1;
+  return (D / e + 15) / 16;
+}
+#define LN_DISPATCH(F, dtype, nch, ...)                                                          \
+  do {                                                                                         \
+    if ((dtype) == VLP_BF16) {                                                                 \
+      switch (nch) {                                                                           \
+        case 1: F<bf16, 1>(__VA_ARGS__); break;                                                \
+        case 2: F<bf16, 2>(__VA_ARGS__); break;                                                \
+        case 3: F<bf16, 3>(__VA_ARGS__); break;                                                \
+        default: F<bf16, 4>(__VA_ARGS__); break;                                               \
+      }                                                                                        \
+    } else {                                                                                   \
+      switch (nch) {                                                                           \
+        case 1: F<float, 1>(__VA_ARGS__); break;                                               \
+        case 2: F<float, 2>(__VA_ARGS__); break;                                               \
+        case 3: F<float, 3>(__VA_ARGS__); break;                                               \
+        case 4: F<float, 4>(__VA_ARGS__); break;                                               \
+        case 5: case 6: F<float, 6>(__VA_ARGS__); break;                                       \
+        default: F<float, 8>(__VA_ARGS__); break;                                              \
+      }                                                                                        \
+    }                                                                                          \
+  } while (0)
+
 VLP_EXPORT int vlp_layernorm_fwd(int dtype, int M, int D, const void* x, const float* gamma,
                                  const float* beta, float eps, void* y, float* mean, float* rstd,
                                  float p, unsigned long long seed, void* stream) {
-  hipStream_t st = (hipStream_t)stream;
-  dim3 grid((M + 3) / 4);
-  if (dtype == VLP_BF16)
-    hipLaunchKernelGGL(layernorm_fwd_kernel<bf16>, grid, dim3(256), 0, st, M, D, (const bf16*)x, gamma,
-                       beta, eps, (bf16*)y, mean, rstd, p, seed);
-  else
-    hipLaunchKernelGGL(layernorm_fwd_kernel<float>, grid, dim3(256), 0, st, M, D, (const float*)x,
-                       gamma, beta, eps, (float*)y, mean, rstd, p, seed);
+  const int nch = ln_nch(dtype, D);
+  if (nch < 0) return (int)hipErrorInvalidValue;
+  if (M < 1) return 0;
+  LN_DISPATCH(ln_fwd_t, dtype, nch, M, D, x, gamma, beta, eps, y, mean, rstd, p, seed, (hipStream_t)stream);
   return (int)hipGetLastError();
 }
 
+template <typename T, int NCH>
+static void ln_bwd_t(int M, int D, const void* dy, float p_out, unsigned long long seed_out, const void* x,
+                     const float* mean, const float* rstd, const float* gamma, void* dx, void* dxd, float p_in,
+                     unsigned long long seed_in, float* dgamma, float* dbeta, const void* addend,
+                     const float* rscale, int rps, hipStream_t st) {
+  int blocks = (M + 15) / 16;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL((layernorm_bwd_kernel<T, NCH>), dim3(blocks), dim3(256), 0, st, M, D, (const T*)dy, p_out,
+                     (uint64_t)seed_out, (const T*)x, mean, rstd, gamma, (T*)dx, (T*)dxd, p_in, (uint64_t)seed_in,
+                     dgamma, dbeta, (const T*)addend, rscale, rps);
+}
 static int layernorm_bwd_launch(int dtype, int M, int D, const void* dy, float p_out,
                                 unsigned long long seed_out, const void* x, const float* mean,
                                 const float* rstd, const float* gamma, void* dx, void* dxd,
                                 float p_in, unsigned long long seed_in, float* dgamma, float* dbeta,
-                                const void* addend, void* stream) {
-  hipStream_t st = (hipStream_t)stream;
-  if (D > 512) return (int)hipErrorInvalidValue;
-  int blocks = (M + 15) / 16;   // 4 rows per wave
-  if (blocks > 1024) blocks = 1024;
-  size_t lds = 0;
-  if (dtype == VLP_BF16)
-    hipLaunchKernelGGL(layernorm_bwd_kernel<bf16>, dim3(blocks), dim3(256), lds, st, M, D,
-                       (const bf16*)dy, p_out, seed_out, (const bf16*)x, mean, rstd, gamma, (bf16*)dx,
-                       (bf16*)dxd, p_in, seed_in, dgamma, dbeta, (const bf16*)addend);
-  else
-    hipLaunchKernelGGL(layernorm_bwd_kernel<float>, dim3(blocks), dim3(256), lds, st, M, D,
-                       (const float*)dy, p_out, seed_out, (const float*)x, mean, rstd, gamma,
-                       (float*)dx, (float*)dxd, p_in, seed_in, dgamma, dbeta, (const float*)addend);
+                                const void* addend, const float* rscale, int rps, void* stream) {
+  const int nch = ln_nch(dtype, D);
+  if (nch < 0 || (rscale && rps < 1)) return (int)hipErrorInvalidValue;
+  if (M < 1) return 0;
+  LN_DISPATCH(ln_bwd_t, dtype, nch, M, D, dy, p_out, seed_out, x, mean, rstd, gamma, dx, dxd, p_in, seed_in, dgamma,
+              dbeta, addend, rscale, rps, (hipStream_t)stream);
   return (int)hipGetLastError();
 }
 VLP_EXPORT int vlp_layernorm_bwd(int dtype, int M, int D, const void* dy, float p_out,
@@ -750,14 +882,24 @@ VLP_EXPORT int vlp_layernorm_bwd(int dtype, int M, int D, const void* dy, float 
                                  float p_in, unsigned long long seed_in, float* dgamma, float* dbeta,
                                  void* stream) {
   return layernorm_bwd_launch(dtype, M, D, dy, p_out, seed_out, x, mean, rstd, gamma, dx, dxd, p_in, seed_in,
-                              dgamma, dbeta, nullptr, stream);
+                              dgamma, dbeta, nullptr, nullptr, 1, stream);
 }
-// pre-norm residual form: dx = LN backward + addend (NesT: x + attn(norm1(x)))
+// pre-norm residual form: dx = LN backward + addend (NesT: x + attn(norm1(x)));
+// dxs (optional) = rscale[row / rps] * dx, the DropPath-scaled gradient of the
+// residual branch that produced x (nullptr rscale: dxs unused)
 VLP_EXPORT int vlp_layernorm_bwd_add(int dtype, int M, int D, const void* dy, const void* x, const float* mean,
                                      const float* rstd, const float* gamma, const void* addend, void* dx,
                                      float* dgamma, float* dbeta, void* stream) {
   return layernorm_bwd_launch(dtype, M, D, dy, 0.f, 0, x, mean, rstd, gamma, dx, nullptr, 0.f, 0, dgamma, dbeta,
-                              addend, stream);
+                              addend, nullptr, 1, stream);
+}
+VLP_EXPORT int vlp_layernorm_bwd_add_rs(int dtype, int M, int D, const void* dy, const void* x, const float* mean,
+                                        const float* rstd, const float* gamma, const void* addend, void* dx,
+                                        void* dxs, const float* rscale, int rps, float* dgamma, float* dbeta,
+                                        void* stream) {
+  if (!rscale || !dxs) return (int)hipErrorInvalidValue;
+  return layernorm_bwd_launch(dtype, M, D, dy, 0.f, 0, x, mean, rstd, gamma, dx, dxs, 0.f, 0, dgamma, dbeta,
+                              addend, rscale, rps, stream);
 }
 
 template <typename T, int TB>

@@ -294,10 +294,8 @@ class NestTower(ArenaModule):
         if scale is None:
             ops.linear_fwd(a, w, bias, out, M, N, K, mode=2, res=x)
             return out
-        ops.linear_fwd(a, w, bias, out, M, N, K)
-        res = x.clone()
-        ops.nest_rowscale(res, out, scale, M, N, M // B, 0)
-        return res
+        ops.linear_fwd_rs(a, w, bias, out, x, scale, M // B, M, N, K)
+        return out
 
     # ---------------- backward ----------------
     def run_backward(self, sv, dfeat, on_stage_done=None):
@@ -324,12 +322,14 @@ class NestTower(ArenaModule):
             M = B * grid * grid
             H, F = self.heads[i], self.mlp[i]
             BT = B * self.num_blocks[i]
+            dh_s = None
             for j in range(self.depths[i] - 1, -1, -1):
                 q = f"levels.{i}.transformer_encoder.{j}."
                 L = lv["layers"][j]
                 dm = dpm[i][j] if dpm is not None else None
-                # MLP branch
-                db = self._branch_grad(dh, dm[1] if dm is not None else None, M, C, B)
+                # MLP branch (its DropPath-scaled gradient came out of the LN backward that
+                # produced dh, except at a level's top layer)
+                db = dh_s if dh_s is not None else self._branch_grad(dh, dm[1] if dm is not None else None, M, C, B)
                 ops.colsum(db, G.gview(q + "mlp.fc2.bias"), M, C)
                 ops.linear_wgrad(db, L["act"], G.gview(q + "mlp.fc2.weight"), M, C, F)
                 dpre = torch.empty(M, F, dtype=T, device=dev)
@@ -339,10 +339,12 @@ class NestTower(ArenaModule):
                 dy2 = torch.empty(M, C, dtype=T, device=dev)
                 ops.linear_dgrad(dpre, self._w(wT, q + "mlp.fc1.weight"), dy2, M, C, F)
                 dx2 = torch.empty(M, C, dtype=T, device=dev)
+                da = torch.empty(M, C, dtype=T, device=dev) if dm is not None else dx2
                 ops.layernorm_bwd_add(dy2, L["x2"], L["mu2"], L["rs2"], self.arena.view(q + "norm2.weight"), dh, dx2,
-                                      G.gview(q + "norm2.weight"), G.gview(q + "norm2.bias"), M, C)
+                                      G.gview(q + "norm2.weight"), G.gview(q + "norm2.bias"), M, C,
+                                      dxs=da if dm is not None else None, rscale=dm[0] if dm is not None else None,
+                                      rps=M // B)
                 # attention branch
-                da = self._branch_grad(dx2, dm[0] if dm is not None else None, M, C, B)
                 ops.colsum(da, G.gview(q + "attn.proj.bias"), M, C)
                 dwp = self._proj_grad_ws(C)
                 ops.linear_wgrad(da, L["o"], dwp, M, C, C)
@@ -357,8 +359,12 @@ class NestTower(ArenaModule):
                 dy1 = torch.empty(M, C, dtype=T, device=dev)
                 ops.linear_dgrad(dqkv, self._w(wT, q + "attn.qkv.weight"), dy1, M, C, 3 * C)
                 dx = torch.empty(M, C, dtype=T, device=dev)
+                # the layer below's MLP-branch scale, applied in the same pass
+                nm = dpm[i][j - 1] if (dpm is not None and j > 0) else None
+                dh_s = torch.empty(M, C, dtype=T, device=dev) if nm is not None else None
                 ops.layernorm_bwd_add(dy1, L["x"], L["mu1"], L["rs1"], self.arena.view(q + "norm1.weight"), dx2, dx,
-                                      G.gview(q + "norm1.weight"), G.gview(q + "norm1.bias"), M, C)
+                                      G.gview(q + "norm1.weight"), G.gview(q + "norm1.bias"), M, C,
+                                      dxs=dh_s, rscale=nm[1] if nm is not None else None, rps=M // B)
                 dh = dx
             # positional embedding: sum over the batch of the level-input gradient
             TN = self.num_blocks[i] * self.seq

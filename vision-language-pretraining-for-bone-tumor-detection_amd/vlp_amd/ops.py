@@ -306,6 +306,14 @@ def linear_fwd(x, w, bias, y, M, N, K, ldx=None, ldy=None, mode=0, aux=None, res
     ktimer.end(tk)
 
 
+def linear_fwd_rs(x, w, bias, y, res, rscale, rps, M, N, K):
+    """y = res + rscale[row // rps] * (x W^T + bias)  (residual branch under DropPath)."""
+    tk = ktimer.begin(f"linear_fwd{_tile_lin(M, N)}", 2.0 * M * N * K)
+    lib().vlp_linear_fwd_rs(dcode(x), M, N, K, ptr(x), K, ptr(w), ptr(bias), ptr(y), N, ptr(res), N, ptr(rscale),
+                            int(rps), _s())
+    ktimer.end(tk)
+
+
 def linear_dgrad(dy, w, dx, M, Kin, Nout, lddy=None, lddx=None, mode=0, aux=None, ldaux=None,
                  addend=None, ldad=None):
     tk = ktimer.begin(f"linear_dgrad{_tile_lin(M, Kin)}", 2.0 * M * Kin * Nout)
@@ -553,6 +561,12 @@ def nest_bcast(dfeat, dy, B, HW, C, inv):
     lib().vlp_nest_bcast(dcode(dy), B, HW, C, ptr(dfeat), float(inv), ptr(dy), _s())
 
 
-def layernorm_bwd_add(dy, x, mean, rstd, gamma, addend, dx, dgamma, dbeta, M, D):
-    lib().vlp_layernorm_bwd_add(dcode(dy), M, D, ptr(dy), ptr(x), ptr(mean), ptr(rstd), ptr(gamma), ptr(addend),
-                                ptr(dx), ptr(dgamma), ptr(dbeta), _s())
+def layernorm_bwd_add(dy, x, mean, rstd, gamma, addend, dx, dgamma, dbeta, M, D, dxs=None, rscale=None, rps=1):
+    """dx = LN backward + addend; with rscale also dxs = rscale[row // rps] * dx."""
+    if rscale is None:
+        lib().vlp_layernorm_bwd_add(dcode(dy), M, D, ptr(dy), ptr(x), ptr(mean), ptr(rstd), ptr(gamma),
+                                    ptr(addend), ptr(dx), ptr(dgamma), ptr(dbeta), _s())
+    else:
+        lib().vlp_layernorm_bwd_add_rs(dcode(dy), M, D, ptr(dy), ptr(x), ptr(mean), ptr(rstd), ptr(gamma),
+                                       ptr(addend), ptr(dx), ptr(dxs), ptr(rscale), int(rps), ptr(dgamma),
+                                       ptr(dbeta), _s())
