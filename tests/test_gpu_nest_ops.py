@@ -45,11 +45,16 @@ def ref_attention(qkv, BT, N, H):
 
 
 @pytest.mark.parametrize("dt", DT)
-@pytest.mark.parametrize("BT,H,N", [(3, 2, 64), (2, 3, 200), (2, 3, 1024), (1, 1, 16)])
-def test_attention_fwd_bwd(ops, dt, BT, H, N):
+@pytest.mark.parametrize("BT,H,N,amp", [(3, 2, 64, 1.0), (2, 3, 200, 1.0), (2, 3, 1024, 1.0), (1, 1, 16, 1.0),
+                                         (2, 2, 36, 1.0), (2, 2, 130, 1.0), (2, 1, 300, 3.0)])
+def test_attention_fwd_bwd(ops, dt, BT, H, N, amp):
+    """amp scales q and k: amp 3 makes peaked rows whose running maximum moves
+    between key tiles (the online-softmax rescale path)."""
     g = torch.Generator().manual_seed(N + H)
     C = 32 * H
-    qkv = torch.randn(BT * N, 3 * C, generator=g).to(dt).float()
+    qkv = torch.randn(BT * N, 3 * C, generator=g)
+    qkv[:, :2 * C] *= amp
+    qkv = qkv.to(dt).float()
     do = torch.randn(BT * N, C, generator=g).to(dt).float()
     x = qkv.double().requires_grad_()
     o_ref = ref_attention(x, BT, N, H)
@@ -183,3 +188,57 @@ def test_permute_rowscale_bcast(ops):
     assert torch.allclose(x2, ref, atol=1e-6)
     assert torch.allclose(y2, s.repeat_interleave(rows)[:, None] * x, atol=1e-6)
     assert torch.allclose(dy.view(2, 5, 8), (dfeat * 0.2)[:, None, :].expand(2, 5, 8), atol=1e-7)
+
+
+@pytest.mark.parametrize("dt", DT)
+def test_linear_fwd_rowscale(ops, dt):
+    """vlp_linear_fwd_rs: res + s[row // rps] * (x W^T + b) (DropPath residual)."""
+    g = torch.Generator().manual_seed(7)
+    B, rps, N, K = 3, 40, 96, 192
+    M = B * rps
+    x = torch.randn(M, K, generator=g).to(dt).float()
+    w = torch.randn(N, K, generator=g).mul(0.1).to(dt).float()
+    b = torch.randn(N, generator=g)
+    res = torch.randn(M, N, generator=g).to(dt).float()
+    s = torch.tensor([0.0, 2.0, 1.25])
+    ref = res.double() + s.double().repeat_interleave(rps)[:, None] * (x.double() @ w.double().T + b.double())
+    y = torch.empty(M, N, dtype=dt, device="cuda")
+    ops.linear_fwd_rs(x.to(dt).cuda(), w.to(dt).cuda(), b.cuda(), y, res.to(dt).cuda(), s.cuda(), rps, M, N, K)
+    torch.cuda.synchronize()
+    assert rel(y.float(), ref) < (1e-5 if dt == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("D", [96, 192, 384, 312])
+def test_layernorm_fwd_bwd_add_rowscale(ops, dt, D):
+    """Vectorized LayerNorm forward (eps 1e-6) and the pre-norm backward with
+    addend and the DropPath-scaled second output, vs torch autograd (fp64)."""
+    g = torch.Generator().manual_seed(D)
+    B, rps = 2, 37
+    M = B * rps
+    x = torch.randn(M, D, generator=g).mul(2).add(0.5).to(dt).float()
+    gam = torch.randn(D, generator=g)
+    bet = torch.randn(D, generator=g)
+    dy = torch.randn(M, D, generator=g).to(dt).float()
+    add = torch.randn(M, D, generator=g).to(dt).float()
+    s = torch.tensor([2.0, 0.0])
+    xd = x.double().requires_grad_()
+    gd, bd = gam.double().requires_grad_(), bet.double().requires_grad_()
+    yref = F.layer_norm(xd, (D,), gd, bd, 1e-6)
+    yref.backward(dy.double())
+    dxref = xd.grad + add.double()
+    y = torch.empty(M, D, dtype=dt, device="cuda")
+    mu, rs = torch.empty(M, device="cuda"), torch.empty(M, device="cuda")
+    xc = x.to(dt).cuda()
+    ops.layernorm_fwd(xc, gam.cuda(), bet.cuda(), 1e-6, y, mu, rs, M, D)
+    dx = torch.empty(M, D, dtype=dt, device="cuda")
+    dxs = torch.empty(M, D, dtype=dt, device="cuda")
+    dg, db = torch.zeros(D, device="cuda"), torch.zeros(D, device="cuda")
+    ops.layernorm_bwd_add(dy.to(dt).cuda(), xc, mu, rs, gam.cuda(), add.to(dt).cuda(), dx, dg, db, M, D,
+                          dxs=dxs, rscale=s.cuda(), rps=rps)
+    torch.cuda.synchronize()
+    tol = 1e-5 if dt == torch.float32 else 1e-2
+    assert rel(y.float(), yref.detach()) < tol
+    assert rel(dx.float(), dxref) < tol
+    assert rel(dxs.float(), s.double().repeat_interleave(rps)[:, None] * dxref) < tol
+    assert rel(dg, gd.grad) < 1e-5 and rel(db, bd.grad) < 1e-5
