@@ -341,6 +341,25 @@ int vlp_pack_stem(int dtype, const float* w, void* wp, void* stream);
 int vlp_unpack_conv_grad(int Co, int C, int KH, int KW, const float* ws, float* g, void* stream);
 int vlp_unpack_stem_grad(const float* ws, float* g, void* stream);
 
+/* ---------------- radiograph preprocessing / augmentation ----------------
+ * Replace the reference's CPU DataLoader transforms (src/data/PretrainDataModule.py:157-198).
+ * vlp_prep_images: n grayscale images of any size packed back to back in src (uint8 when
+ * src_u8, else fp32; element offsets off[n] and sizes hw[n][2] in DEVICE memory) ->
+ * HistogramNormalized (MONAI, 256 bins) -> CropLargerDimension(0.05) ->
+ * PadToSquaredEdgeAverage -> Resized(S, area) -> (x - mean) / std, written to out fp32
+ * [n][C][S][S] (channels identical, as the reference's 3-channel repeat).
+ * work: n * 1544 bytes of device scratch. */
+int vlp_prep_images(int n, const void* src, int src_u8, const long long* off, const int* hw, int S,
+                    float mean, float std_, int C, float* out, void* work, void* stream);
+/* One resample per sample for RandAffined + RandRotated + RandFlipd + RandZoomd, then
+ * RandGaussianNoised: out[b][c] = bilinear(in[b][ci]) at source (row, col) =
+ * M_b (p - centre) + centre + t_b (border clamp) + N(0, noise_std[b]);
+ * maps[b] = {m00, m01, t0, m10, m11, t1} drawn on the host.  in: fp32 [B][Cin][H][W]
+ * (Cin 1 or C), or uint8 [B][1][H][W] normalised on load with (v - mean) / std. */
+int vlp_aug_warp(int B, int Cin, int C, int H, int W, const void* in, int in_u8, float mean, float std_,
+                 const float* maps, const float* noise_std, unsigned long long seed, float* out,
+                 void* stream);
+
 #ifdef __cplusplus
 }
 #endif

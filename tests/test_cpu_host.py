@@ -195,3 +195,14 @@ def test_fused_adamw_span_grouping():
     assert len(opt._spans(txt)) <= 2
     with pytest.raises(ValueError):
         FusedAdamW([torch.nn.Parameter(torch.zeros(3))], arenas=[])
+
+
+def test_augment_maps_match_oracle():
+    """Host half of the device augmentation: the composed output->source maps
+    equal the oracle's per-transform composition (oracle/prep.py)."""
+    import torch
+    import oracle.prep as op
+    from vlp_amd.augment import Augmenter
+    a = Augmenter(seed=3)
+    prm = a.draw(64)
+    assert torch.allclose(a.maps(prm), op.source_maps(prm), atol=1e-12)

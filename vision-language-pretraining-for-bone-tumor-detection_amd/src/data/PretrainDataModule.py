@@ -24,9 +24,14 @@ MI355X-first changes:
     is off the step's critical path.
   * image_size (default 224, the reference's) and the synthetic dataset.
 
-The MURA/LERA readers, MONAI augmentation pipeline and caption sampler need
-datasets and packages that are not in this image; with
-synthetic=False the module raises NotImplementedError.  Synthetic samples
+  * the training augmentations run on the device (device_augment ->
+    vlp_amd.augment, csrc/prep_ops.hip), called by the trainer on each training
+    batch after the upload; vlp_amd.augment.preprocess is the device form of the
+    pre-normalisation chain (histogram equalisation, crop, pad, area resize) for
+    decoded radiographs of any size.
+
+The MURA/LERA readers and caption sampler need datasets that are not in this
+image; with synthetic=False the module raises NotImplementedError.  Synthetic samples
 follow SURVEY §8(d): uint8 pixels ~ U{0..255} (histogram-equalised), captions
 CLS + U{8..20} tokens in [1000, 30000) + SEP, zero padding.
 """
@@ -232,8 +237,33 @@ class PretrainDataModule:
         # caches them per fold, :217-267, for NormalizeIntensityd)
         self.image_mean, self.image_std = self._intensity_stats(self.train_dataset)
         self.collate = PairCollator(upload, num_channels, self.image_mean, self.image_std)
-        if not disable_augmentations:
-            logger.warning("PretrainDataModule: augmentations are not applied in the MI355X build")
+        self._augmenter = None
+        if disable_augmentations:
+            logger.warning("PretrainDataModule: No augmentations are applied.")
+
+    def device_augment(self, batch: dict) -> dict:
+        """The reference's training augmentations (RandAffined, RandRotated, RandFlipd,
+        RandZoomd, RandGaussianNoised; PretrainDataModule.py:186-198) on a device batch
+        in one pass (vlp_amd.augment.Augmenter -> vlp_aug_warp): the uint8 upload is
+        normalised on load and comes back as the fp32 "x-ray" tensor.  Identity when
+        augmentations are disabled or the batch is on the CPU."""
+        if self.disable_augmentations:
+            return batch
+        x = batch.get("x-ray-u8", batch.get("x-ray"))
+        if x is None or x.device.type != "cuda":
+            return batch
+        if self._augmenter is None:
+            from vlp_amd.augment import Augmenter
+            rank = torch.distributed.get_rank() if torch.distributed.is_initialized() else 0
+            self._augmenter = Augmenter(seed=self.seed * 1_000_003 + 17 * rank + 1)
+        out = dict(batch)
+        if "x-ray-u8" in batch:
+            out["x-ray"] = self._augmenter(x, channels=self.num_channels, mean=self.image_mean, std=self.image_std)
+            del out["x-ray-u8"]
+            out.pop("x-ray-u8-norm", None)
+        else:
+            out["x-ray"] = self._augmenter(x, channels=self.num_channels)
+        return out
 
     @staticmethod
     def _intensity_stats(ds, n: int = 64):

@@ -287,6 +287,9 @@ class Trainer:
         world = self._dp_world()
         reduce_grads = world > 1 and not getattr(model, "handles_dp_collectives", False)
         stop = False
+        # training-batch augmentation on the device (the reference's MONAI chain runs
+        # in its DataLoader workers, PretrainDataModule.py:186-198)
+        augment = getattr(datamodule, "device_augment", None) if datamodule is not None else None
         t_fit = time.perf_counter()
         for epoch in range(self.max_epochs):
             self.current_epoch = epoch
@@ -297,6 +300,8 @@ class Trainer:
                 if self.limit_train_batches is not None and i >= self.limit_train_batches:
                     break
                 t0 = time.perf_counter()
+                if augment is not None:
+                    batch = augment(batch)
                 optimizer.zero_grad(set_to_none=False)
                 loss = model.training_step(batch, i)
                 loss.backward()

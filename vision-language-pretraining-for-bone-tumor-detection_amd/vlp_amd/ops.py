@@ -570,3 +570,21 @@ def layernorm_bwd_add(dy, x, mean, rstd, gamma, addend, dx, dgamma, dbeta, M, D,
         lib().vlp_layernorm_bwd_add_rs(dcode(dy), M, D, ptr(dy), ptr(x), ptr(mean), ptr(rstd), ptr(gamma),
                                        ptr(addend), ptr(dx), ptr(dxs), ptr(rscale), int(rps), ptr(dgamma),
                                        ptr(dbeta), _s())
+
+
+# ---------------- radiograph preprocessing / augmentation (csrc/prep_ops.hip) ----------------
+PREP_WORK_BYTES_PER_IMAGE = (64 * 2 + 256 + 2) * 4
+
+
+def prep_images(src, src_u8, off, hw, n, size, mean, std, channels, out, work):
+    """src: packed pixels (device, uint8 or fp32); off [n] int64 / hw [n, 2] int32 (device)."""
+    lib().vlp_prep_images(n, ptr(src), int(bool(src_u8)), ptr(off), ptr(hw), int(size), float(mean), float(std),
+                          int(channels), ptr(out), ptr(work), _s())
+
+
+def aug_warp(x, out, maps, noise_std, seed, mean=0.0, std=1.0):
+    """x: fp32 [B, Cin, H, W] or uint8 [B, 1, H, W]; out fp32 [B, C, H, W]; maps [B, 6] fp32."""
+    B, Cin, H, W = x.shape
+    C = out.shape[1]
+    lib().vlp_aug_warp(B, Cin, C, H, W, ptr(x), int(x.dtype == torch.uint8), float(mean), float(std), ptr(maps),
+                       ptr(noise_std), int(seed) & ((1 << 64) - 1), ptr(out), _s())
