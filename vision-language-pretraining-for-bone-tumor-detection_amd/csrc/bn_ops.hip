@@ -176,7 +176,19 @@ bn_grad_rep_kernel(int rep, int C, double* sum_g, double* sum_gx, double* sum_gx
 }
 
 // ---- out = relu(sc*y + sh + identity), identity = idt or (scd*idt + shd) ----
-template <typename T, bool HAS_IDT>
+// U chunks per thread per iteration with every load issued before the first
+// store (more bytes in flight per wave); NT: non-temporal stores (streamed
+// outputs are not re-read by this pass)
+template <int U, bool NT>
+__device__ __forceinline__ void ew_st16(void* p, const uint4& v) {
+  if constexpr (NT) {
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    const v4u w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<v4u*>(p));
+  }
+  else stg16(p, v);
+}
+template <typename T, bool HAS_IDT, int U = 1, bool NT = false>
 __global__ void __launch_bounds__(256)
 bn_add_relu_kernel(unsigned nchunks, int cpr, const T* __restrict__ y, const float* __restrict__ sc,
                    const float* __restrict__ sh, const T* __restrict__ idt,
@@ -194,11 +206,11 @@ bn_add_relu_kernel(unsigned nchunks, int cpr, const T* __restrict__ y, const flo
     d[j] = scd ? shd[c0 + j] : 0.f;
     b[j] += d[j];
   }
-  for (unsigned i = tid; i < nchunks; i += stride) {
+  auto one = [&](unsigned i, const uint4& yv, const uint4& iv) __attribute__((always_inline)) {
     float u[E], v[E];
-    Chunk<T>::unpack(ldg16(y + (size_t)i * E), u);
+    Chunk<T>::unpack(yv, u);
     if constexpr (HAS_IDT) {
-      Chunk<T>::unpack(ldg16(idt + (size_t)i * E), v);
+      Chunk<T>::unpack(iv, v);
 #pragma unroll
       for (int j = 0; j < E; ++j) u[j] = fmaxf(fmaf(u[j], a[j], fmaf(v[j], c[j], b[j])), 0.f);
     } else {
@@ -206,10 +218,28 @@ bn_add_relu_kernel(unsigned nchunks, int cpr, const T* __restrict__ y, const flo
       for (int j = 0; j < E; ++j) u[j] = fmaxf(fmaf(u[j], a[j], b[j]), 0.f);
     }
     const uint4 pk = Chunk<T>::pack(u);
-    stg16(out + (size_t)i * E, pk);
+    ew_st16<U, NT>(out + (size_t)i * E, pk);
     if constexpr (E == 8) {
       if (rmask) rmask[i] = relu_bits8(pk);
     }
+  };
+  unsigned i = tid;
+  if constexpr (U > 1) {
+    for (; i + (U - 1) * stride < nchunks; i += U * stride) {
+      uint4 yv[U], iv[U];
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        yv[k] = ldg16(y + (size_t)(i + k * stride) * E);
+        if constexpr (HAS_IDT) iv[k] = ldg16(idt + (size_t)(i + k * stride) * E);
+      }
+#pragma unroll
+      for (int k = 0; k < U; ++k) one(i + k * stride, yv[k], HAS_IDT ? iv[k] : yv[k]);
+    }
+  }
+  for (; i < nchunks; i += stride) {
+    const uint4 yv = ldg16(y + (size_t)i * E);
+    const uint4 iv = HAS_IDT ? ldg16(idt + (size_t)i * E) : yv;
+    one(i, yv, iv);
   }
 }
 
@@ -286,7 +316,7 @@ struct BnBwdSide {
   const void* y; const float* mean; const float* istd; const float* gamma;
   const double* sum_g; const double* sum_gx; void* dy;
 };
-template <typename T, bool HAS_B>
+template <typename T, bool HAS_B, int U = 1, bool NT = false>
 __global__ void __launch_bounds__(256)
 bn_bwd_apply_kernel(unsigned nchunks, int cpr, double count, const T* __restrict__ dout,
                     const float* __restrict__ dbc, int HW, const T* __restrict__ mask, BnBwdSide A,
@@ -310,6 +340,39 @@ bn_bwd_apply_kernel(unsigned nchunks, int cpr, double count, const T* __restrict
       float k2 = B.gamma[c] * B.istd[c];
       float mg2 = (float)B.sum_g[c] * inv_count, mgx2 = (float)B.sum_gx[c] * inv_count;
       kb[j] = k2; bb[j] = -k2 * B.istd[c] * mgx2; cb[j] = -k2 * mg2 + k2 * B.istd[c] * mgx2 * B.mean[c];
+    }
+  }
+  // the plain form (no broadcast gradient, no mask, no g_out, one side) runs
+  // U chunks per iteration with both loads of every chunk issued first
+  if constexpr (U > 1 && !HAS_B) {
+    if (!dbc && !mask && !g_out) {
+      unsigned i = tid;
+      for (; i + (U - 1) * stride < nchunks; i += U * stride) {
+        uint4 gv[U], yv[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+          gv[k] = ldg16(dout + (size_t)(i + k * stride) * E);
+          yv[k] = ldg16((const T*)A.y + (size_t)(i + k * stride) * E);
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+          float g[E], y[E], d[E];
+          Chunk<T>::unpack(gv[k], g);
+          Chunk<T>::unpack(yv[k], y);
+#pragma unroll
+          for (int j = 0; j < E; ++j) d[j] = fmaf(ka[j], g[j], fmaf(ba[j], y[j], ca[j]));
+          ew_st16<U, NT>((T*)A.dy + (size_t)(i + k * stride) * E, Chunk<T>::pack(d));
+        }
+      }
+      for (; i < nchunks; i += stride) {
+        float g[E], y[E], d[E];
+        Chunk<T>::unpack(ldg16(dout + (size_t)i * E), g);
+        Chunk<T>::unpack(ldg16((const T*)A.y + (size_t)i * E), y);
+#pragma unroll
+        for (int j = 0; j < E; ++j) d[j] = fmaf(ka[j], g[j], fmaf(ba[j], y[j], ca[j]));
+        ew_st16<U, NT>((T*)A.dy + (size_t)i * E, Chunk<T>::pack(d));
+      }
+      return;
     }
   }
   for (unsigned i = tid; i < nchunks; i += stride) {
@@ -852,6 +915,22 @@ __global__ void avgpool_fwd_kernel(int N, int HW, int C, const T* __restrict__ x
 
 // grid whose total thread count is a multiple of cpr (256 % cpr == 0)
 static inline int ew_grid(size_t nchunks) { return ew_blocks(nchunks, 256, 4096); }
+// streaming-pass variants (A/B switches VLP_EW for bn_add_relu, VLP_EWB for
+// bn_bwd_apply): 0 one chunk per iteration, 1 / 2 two / four chunks per
+// iteration, 3 four + non-temporal stores, 4 non-temporal stores.  Measured
+// (tools/ew_bench.py, bs = 256): unrolling loses at every size; non-temporal
+// stores take bn_add_relu from 4.8-4.9 to 5.2-6.3 TB/s at layers 1-2 and do
+// not help bn_bwd_apply, so the defaults are 4 and 0.
+static inline int ew_variant() {
+  static int v = -1;
+  if (v < 0) v = getenv("VLP_EW") ? atoi(getenv("VLP_EW")) : 4;
+  return v;
+}
+static inline int ewb_variant() {
+  static int v = -1;
+  if (v < 0) v = getenv("VLP_EWB") ? atoi(getenv("VLP_EWB")) : 0;
+  return v;
+}
 
 }  // namespace vlp
 
@@ -912,12 +991,22 @@ VLP_EXPORT int vlp_bn_add_relu(int dtype, long long M, int C, const void* y, con
   if (256 % cpr) return (int)hipErrorInvalidValue;
   dim3 g(ew_grid(n));
   if (dtype == VLP_BF16) {
-    if (idt)
-      hipLaunchKernelGGL((bn_add_relu_kernel<bf16, true>), g, dim3(256), 0, st, n, cpr, (const bf16*)y, sc,
-                         sh, (const bf16*)idt, scd, shd, (bf16*)out, relu_mask);
-    else
-      hipLaunchKernelGGL((bn_add_relu_kernel<bf16, false>), g, dim3(256), 0, st, n, cpr, (const bf16*)y,
-                         sc, sh, (const bf16*)idt, scd, shd, (bf16*)out, relu_mask);
+    switch (ew_variant()) {
+#define VLP_ADD_RELU(U, NT)                                                                                    \
+  if (idt)                                                                                                     \
+    hipLaunchKernelGGL((bn_add_relu_kernel<bf16, true, U, NT>), g, dim3(256), 0, st, n, cpr, (const bf16*)y,  \
+                       sc, sh, (const bf16*)idt, scd, shd, (bf16*)out, relu_mask);                             \
+  else                                                                                                         \
+    hipLaunchKernelGGL((bn_add_relu_kernel<bf16, false, U, NT>), g, dim3(256), 0, st, n, cpr, (const bf16*)y, \
+                       sc, sh, (const bf16*)idt, scd, shd, (bf16*)out, relu_mask);                             \
+  break;
+      case 1: VLP_ADD_RELU(2, false)
+      case 2: VLP_ADD_RELU(4, false)
+      case 3: VLP_ADD_RELU(4, true)
+      case 4: VLP_ADD_RELU(1, true)
+      default: VLP_ADD_RELU(1, false)
+#undef VLP_ADD_RELU
+    }
   } else {
     if (idt)
       hipLaunchKernelGGL((bn_add_relu_kernel<float, true>), g, dim3(256), 0, st, n, cpr, (const float*)y,
@@ -984,9 +1073,20 @@ VLP_EXPORT int vlp_bn_bwd_apply(int dtype, long long M, int C, const void* dout,
     if (hb)
       hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16, true>), g, dim3(256), 0, st, n, cpr, (double)M,
                          (const bf16*)dout, dbc, HW, (const bf16*)mask, A, B, (bf16*)g_out);
-    else
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16, false>), g, dim3(256), 0, st, n, cpr, (double)M,
-                         (const bf16*)dout, dbc, HW, (const bf16*)mask, A, B, (bf16*)g_out);
+    else {
+      switch (ewb_variant()) {
+#define VLP_BWD_APPLY(U, NT)                                                                            \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16, false, U, NT>), g, dim3(256), 0, st, n, cpr, (double)M, \
+                     (const bf16*)dout, dbc, HW, (const bf16*)mask, A, B, (bf16*)g_out);               \
+  break;
+        case 1: VLP_BWD_APPLY(2, false)
+        case 2: VLP_BWD_APPLY(4, false)
+        case 3: VLP_BWD_APPLY(4, true)
+        case 4: VLP_BWD_APPLY(1, true)
+        default: VLP_BWD_APPLY(1, false)
+#undef VLP_BWD_APPLY
+      }
+    }
   } else {
     if (hb)
       hipLaunchKernelGGL((bn_bwd_apply_kernel<float, true>), g, dim3(256), 0, st, n, cpr, (double)M,

@@ -1107,8 +1107,8 @@ gemm_bk_kernel(GemmShape sh, LA la, LB lb, EP ep) {
 //     MFMAs of k-substep 1
 // so each fetch has ~two iterations of MFMA work to land in, and the
 // operand traffic per FLOP halves against 128x128 (256x256: 128 FLOP/B).
-template <int BM, int BN, int WGM, int WGN, class LA, class LB, class EP>
-__global__ void __launch_bounds__(WGM * WGN * 64) __attribute__((amdgpu_waves_per_eu(VLP_WAVES_PER_EU)))
+template <int BM, int BN, int WGM, int WGN, class LA, class LB, class EP, int WPE = VLP_WAVES_PER_EU>
+__global__ void __launch_bounds__(WGM * WGN * 64) __attribute__((amdgpu_waves_per_eu(WPE)))
 gemm_big_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   constexpr int NT = WGM * WGN * 64;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
@@ -1273,6 +1273,228 @@ gemm_big_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   }
 }
 
+// ---------------- ping-pong large-tile kernel (bf16, K-contig operands) ----------------
+// The two wave groups of a 2 x WGN workgroup (M halves; one wave of each per
+// SIMD) run one barrier interval apart, so that on every SIMD one wave issues
+// its MFMAs while its partner issues the next phase's fragment reads and
+// LDS-DMA pieces (MI355X_MICROARCH "two waves per SIMD"; the 256x256
+// 8-phase schedule of cdna_hip_programming.md §5).  The ring holds four
+// 32-deep half-tiles ([rows][64 B] images, 16-B chunk c of row r at
+// c ^ (bit3(r) << 1): conflict-free ds_read_b128 fragment reads); the loaders
+// still step 64-deep (half h = the chunks 4h..4h+3 of a step, +64 B).
+// Phase q (half-tile q in slot q % 4), per wave:
+//   L_q: fragment reads of half-tile q; group 0 fetches A of half-tile q+2,
+//        group 1 B of half-tile q+3 (then waits until B of q+1 has landed);
+//        barrier
+//   M_q: lgkmcnt(0); MFMAs; group 0 waits until A of q+1 has landed; barrier
+// Group 1 enters one barrier late, so its L_q shares an interval with group
+// 0's M_q.  A slot is refetched only after both groups' reads of its previous
+// half-tile retired behind a barrier (q+2 / q+3 land in slots last read in
+// phases q-2 / q-1), and half-tile q+1 is read only after both issuers'
+// counted waits and a barrier.
+__device__ __forceinline__ int pp_chunk(int r, int c) { return c ^ (((r >> 3) & 1) << 1); }
+template <int BM, class L, int NTG, bool KC = L::kKContig>
+struct HStager;
+// K-contig operand: [BM rows][64 B] half image, 16 rows per wave-wide piece
+template <int BM, class L, int NTG>
+struct HStager<BM, L, NTG, true> {
+  static constexpr int P = BM * 4 / NTG;   // 16-B pieces per thread per half-tile
+  static_assert(P >= 1 && (BM * 4) % NTG == 0, "tile / thread geometry");
+  typename L::BState st[P];
+  __device__ __forceinline__ void init(const L& ld, int row0, int kb, int wg) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+      const int q = (wg * P + i) * 64 + lane;
+      const int r = q >> 2;
+      st[i] = ld.bstart(row0 + r, pp_chunk(r, q & 3) * 8, kb);
+    }
+  }
+  template <int H>
+  __device__ __forceinline__ void issue(const L& ld, rsrc_t rs, int k0, char* lds, int wg) {
+    const auto stp = ld.bstep(k0);
+#pragma unroll
+    for (int i = 0; i < P; ++i) dma16(rs, ld.boff(st[i], stp) + (unsigned)H * 64u, lds + (wg * P + i) * 1024);
+  }
+};
+// MN-contig operand: the blocked image (mn8_off) of 32 k-rows; each wave owns
+// one 8-row k-group, so a thread keeps one pixel-row walk per half
+template <int BM, class L, int NTG>
+struct HStager<BM, L, NTG, false> {
+  static constexpr int CPB = BM / 64;
+  static constexpr int P = BM * 4 / NTG;
+  static_assert(P == CPB && NTG == 256, "one k-group per wave");
+  typename L::BRow rs[2];
+  typename L::BCol cs[P];
+  __device__ __forceinline__ void init(const L& ld, int row0, int kb, int wg) {
+    const int lane = threadIdx.x & 63;
+    const int k = 8 * wg + (lane >> 3);
+#pragma unroll
+    for (int i = 0; i < P; ++i) cs[i] = ld.bcstart(row0 + (8 * i + ((lane & 7) ^ mn8_h(k))) * 8);
+    rs[0] = ld.brstart(k, kb);
+    rs[1] = ld.brstart(k + 32, kb);
+  }
+  template <int H>
+  __device__ __forceinline__ void issue(const L& ld, rsrc_t r, int, char* lds, int wg) {
+#pragma unroll
+    for (int i = 0; i < P; ++i) dma16(r, ld.boff(rs[H], cs[i]), lds + (wg * P + i) * 1024);
+    ld.bradvance(rs[H]);
+  }
+};
+
+template <int BM, int BN, int WGM, int WGN, class LA, class LB, class EP>
+__global__ void __launch_bounds__(WGM * WGN * 64) __attribute__((amdgpu_waves_per_eu(2)))
+gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
+  static_assert(WGM == 2, "two M-half wave groups");
+  constexpr int NT = WGM * WGN * 64, NTG = NT / 2;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int MB = WTM / 16, NB = WTN / 16;
+  constexpr int BK = 64;
+  constexpr int HA = BM * 64, SLOT = (BM + BN) * 64;
+  using SA = HStager<BM, LA, NTG>;
+  using SB = HStager<BN, LB, NTG>;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int nwg = sh.tiles_m * sh.tiles_n;
+  const int ntot = nwg * sh.nsplit;
+  const int bid = blockIdx.x;
+  int g = bid;
+  if (ntot >= 16) {
+    const int xcd = bid & 7, idx = bid >> 3, q = ntot >> 3, rr = ntot & 7;
+    g = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
+  }
+  const int split = g / nwg;
+  const int wid = g - split * nwg;
+  const int tm = wid / sh.tiles_n, tn = wid - tm * sh.tiles_n;
+  const int row0 = tm * BM, col0 = tn * BN;
+  const int kb = split * sh.kchunk;
+  int ke = kb + sh.kchunk;
+  if (ke > sh.K) ke = sh.K;
+  const int nk = (ke - kb + BK - 1) / BK;
+  const int nh = 2 * (nk > 0 ? nk : 0);
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int wm = wv / WGN, wn = wv - wm * WGN;
+  const int grp = wm, wg = wn;
+
+  SA sa;
+  SB sb;
+  if (grp == 0) sa.init(la, row0, kb, wg);
+  else sb.init(lb, col0, kb, wg);
+  const rsrc_t ra = la.rsrc(), rb = lb.rsrc();
+  const rsrc_t rz = null_rsrc(zero_page());
+  v4f acc[MB][NB];
+#pragma unroll
+  for (int a = 0; a < MB; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[a][b] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  // half-tile u sits in slot (u + off) % 4 (off even, so u and its slot share
+  // parity = the half of its 64-deep step); nh % 4 == 2 starts at slot 2 so
+  // the 4-phase unrolled loop ends on slot 3
+  const int off = nh & 2;
+  auto fetchA = [&](auto hc, int u, char* slot) __attribute__((always_inline)) {
+    sa.template issue<decltype(hc)::value>(la, u < nh ? ra : rz, kb + (u >> 1) * BK, slot, wg);
+  };
+  auto fetchB = [&](auto hc, int u, char* slot) __attribute__((always_inline)) {
+    sb.template issue<decltype(hc)::value>(lb, u < nh ? rb : rz, kb + (u >> 1) * BK, slot + HA, wg);
+  };
+  using H0 = std::integral_constant<int, 0>;
+  using H1 = std::integral_constant<int, 1>;
+  if (grp == 0) {
+    fetchA(H0{}, 0, smem + off * SLOT);
+    fetchA(H1{}, 1, smem + ((off + 1) & 3) * SLOT);
+    wait_vmcnt<SA::P>();
+  } else {
+    fetchB(H0{}, 0, smem + off * SLOT);
+    fetchB(H1{}, 1, smem + ((off + 1) & 3) * SLOT);
+    fetchB(H0{}, 2, smem + ((off + 2) & 3) * SLOT);
+    wait_vmcnt<2 * SB::P>();
+  }
+  raw_barrier();
+  if (grp == 1) raw_barrier();   // the stagger
+  __builtin_amdgcn_sched_barrier(0);
+
+  const int lane = threadIdx.x & 63;
+  const int fi = lane & 15, fg = lane >> 4;
+  const char* fbase = smem + fi * 64 + (pp_chunk(fi, fg) << 4);
+  // MN-contig operands: one transposing-read address per (slot pair, fragment column)
+  constexpr int QA = MB < 4 ? MB : 4, QB = NB < 4 ? NB : 4;
+  unsigned abase[2][LA::kKContig ? 1 : QA], bbase[2][LB::kKContig ? 1 : QB];
+  if constexpr (!LA::kKContig) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int a = 0; a < QA; ++a) abase[p][a] = mn_frag_base<BM * 2>(smem + 2 * p * SLOT, wm * WTM + a * 16);
+  }
+  if constexpr (!LB::kKContig) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int b = 0; b < QB; ++b) bbase[p][b] = mn_frag_base<BN * 2>(smem + 2 * p * SLOT + HA, wn * WTN + b * 16);
+  }
+
+  auto phase = [&](auto slc, int q) __attribute__((always_inline)) {
+    constexpr int SL = decltype(slc)::value;
+    constexpr int SO = (SL & 1) * SLOT;   // offset inside the slot pair
+    v8bf fa[MB], fb[NB];
+    static_for<0, MB>([&](auto ac) {
+      constexpr int a = decltype(ac)::value;
+      if constexpr (LA::kKContig)
+        fa[a] = *reinterpret_cast<const v8bf*>(fbase + SL * SLOT + (wm * WTM + a * 16) * 64);
+      else
+        fa[a] = frag_tr_at<SO + (a >> 2) * 1024>(abase[SL >> 1][a & 3]);
+    });
+    static_for<0, NB>([&](auto bc) {
+      constexpr int b = decltype(bc)::value;
+      if constexpr (LB::kKContig)
+        fb[b] = *reinterpret_cast<const v8bf*>(fbase + SL * SLOT + HA + (wn * WTN + b * 16) * 64);
+      else
+        fb[b] = frag_tr_at<SO + (b >> 2) * 1024>(bbase[SL >> 1][b & 3]);
+    });
+    if (grp == 0) {
+      fetchA(std::integral_constant<int, SL & 1>{}, q + 2, smem + ((SL + 2) & 3) * SLOT);
+    } else {
+      fetchB(std::integral_constant<int, 1 - (SL & 1)>{}, q + 3, smem + ((SL + 3) & 3) * SLOT);
+      wait_vmcnt<2 * SB::P>();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    raw_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int a = 0; a < MB; ++a)
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], acc[a][b], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    if (grp == 0) wait_vmcnt<SA::P>();
+    __builtin_amdgcn_sched_barrier(0);
+    raw_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  int q = 0;
+  if (off) {
+    phase(std::integral_constant<int, 2>{}, 0);
+    phase(std::integral_constant<int, 3>{}, 1);
+    q = 2;
+  }
+  for (; q < nh; q += 4) {
+    phase(std::integral_constant<int, 0>{}, q);
+    phase(std::integral_constant<int, 1>{}, q + 1);
+    phase(std::integral_constant<int, 2>{}, q + 2);
+    phase(std::integral_constant<int, 3>{}, q + 3);
+  }
+  if (grp == 0) raw_barrier();   // matches group 1's stagger barrier
+  __syncthreads();   // ring drained (incl. the null-resource tail fetches) before LDS is reused
+  if constexpr (SplitTrait<EP>::value) {
+    ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep.at_split(split), acc, row0, col0, wid, wm, wn, smem);
+  } else {
+    ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep, acc, row0, col0, wid, wm, wn, smem);
+  }
+}
+
 template <int BM, int BN, class EP>
 constexpr int big_lds_bytes() {
   constexpr int ring = 2 * (BM + BN) * 128;
@@ -1429,7 +1651,7 @@ inline int launch_gemm_bk(int M, int N, int K, int ksplit, const LA& la, const L
   return (int)hipGetLastError();
 }
 
-template <int BM, int BN, int WGM, int WGN, class LA, class LB, class EP>
+template <int BM, int BN, int WGM, int WGN, class LA, class LB, class EP, int WPE = VLP_WAVES_PER_EU>
 inline int launch_gemm_big(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
                           hipStream_t stream) {
   constexpr int BK = 64;
@@ -1447,10 +1669,10 @@ inline int launch_gemm_big(int M, int N, int K, int ksplit, const LA& la, const 
     if (!occ) {
       constexpr int lds_b = big_lds_bytes<BM, BN, EP>();
       if (lds_b > 65536)
-        (void)hipFuncSetAttribute((const void*)&gemm_big_kernel<BM, BN, WGM, WGN, LA, LB, EP>,
+        (void)hipFuncSetAttribute((const void*)&gemm_big_kernel<BM, BN, WGM, WGN, LA, LB, EP, WPE>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds_b);
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-              &occ, (const void*)&gemm_big_kernel<BM, BN, WGM, WGN, LA, LB, EP>, WGM * WGN * 64,
+              &occ, (const void*)&gemm_big_kernel<BM, BN, WGM, WGN, LA, LB, EP, WPE>, WGM * WGN * 64,
               lds_b) != hipSuccess || occ <= 0)
         occ = 1;
     }
@@ -1474,13 +1696,62 @@ inline int launch_gemm_big(int M, int N, int K, int ksplit, const LA& la, const 
   if constexpr (lds > 65536) {
     static bool attr_set = false;
     if (!attr_set) {
-      (void)hipFuncSetAttribute((const void*)&gemm_big_kernel<BM, BN, WGM, WGN, LA, LB, EP>,
+      (void)hipFuncSetAttribute((const void*)&gemm_big_kernel<BM, BN, WGM, WGN, LA, LB, EP, WPE>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
       attr_set = true;
     }
   }
-  hipLaunchKernelGGL((gemm_big_kernel<BM, BN, WGM, WGN, LA, LB, EP>), grid, dim3(WGM * WGN * 64), lds,
+  hipLaunchKernelGGL((gemm_big_kernel<BM, BN, WGM, WGN, LA, LB, EP, WPE>), grid, dim3(WGM * WGN * 64), lds,
                      stream, sh, la, lb, ep);
+  return (int)hipGetLastError();
+}
+
+template <int BM, int BN, int WGM, int WGN, class LA, class LB, class EP>
+inline int launch_gemm_pp(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
+                          hipStream_t stream) {
+  constexpr int BK = 64;
+  if (M <= 0 || N <= 0) return 0;
+  GemmShape sh;
+  sh.xsplit = 0;
+  sh.dbg = 0;
+  sh.M = M; sh.N = N; sh.K = K;
+  sh.tiles_m = (M + BM - 1) / BM;
+  sh.tiles_n = (N + BN - 1) / BN;
+  constexpr int lds = big_lds_bytes<BM, BN, EP>();
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  if (ksplit <= 0) {   // auto: fill whole rounds of resident workgroups (one per CU)
+    static int occ = 0;
+    if (!occ) {
+      if (lds > 65536)
+        (void)hipFuncSetAttribute((const void*)&gemm_pp_kernel<BM, BN, WGM, WGN, LA, LB, EP>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+              &occ, (const void*)&gemm_pp_kernel<BM, BN, WGM, WGN, LA, LB, EP>, WGM * WGN * 64, lds) != hipSuccess ||
+          occ <= 0)
+        occ = 1;
+    }
+    ksplit = balanced_ksplit(sh.tiles_m * sh.tiles_n, K, occ * device_cus(), -ksplit > 0 ? -ksplit : 2048);
+  }
+  if (ksplit < 1) ksplit = 1;
+  int kc = (K + ksplit - 1) / ksplit;
+  kc = ((kc + BK - 1) / BK) * BK;
+  if (kc < BK) kc = BK;
+  ksplit = (K + kc - 1) / kc;
+  if (ksplit < 1) ksplit = 1;
+  sh.kchunk = kc;
+  sh.nsplit = ksplit;
+  last_ksplit() = ksplit;
+  dim3 grid(sh.tiles_m * sh.tiles_n * ksplit, 1, 1);
+  if constexpr (lds > 65536) {
+    static bool attr_set = false;
+    if (!attr_set) {
+      (void)hipFuncSetAttribute((const void*)&gemm_pp_kernel<BM, BN, WGM, WGN, LA, LB, EP>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      attr_set = true;
+    }
+  }
+  hipLaunchKernelGGL((gemm_pp_kernel<BM, BN, WGM, WGN, LA, LB, EP>), grid, dim3(WGM * WGN * 64), lds, stream, sh,
+                     la, lb, ep);
   return (int)hipGetLastError();
 }
 
@@ -1516,7 +1787,19 @@ template <class LA, class LB, class EP>
 inline int gemm_big_auto(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep, hipStream_t st) {
   // (256x256 keeps 128x64 fragments per wave live: only the all-K-contig case
   // fits the 256-VGPR budget without spilling)
-  if constexpr (LA::kKContig && LB::kKContig) {
+  // ping-pong schedule (gemm_pp_kernel): 1 = K-contig x K-contig, 2 = also MN x MN
+  // (default 1: +0.8 % per step, the 256x256 forward / data-gradient GEMMs +3 %)
+  static const int pp = getenv("VLP_PP") ? atoi(getenv("VLP_PP")) : 1;
+  constexpr bool kk = LA::kKContig && LB::kKContig;
+  constexpr bool mm = !LA::kKContig && !LB::kKContig;
+  if constexpr (kk || mm) {
+    if (pp >= (kk ? 1 : 2) && M >= 256 && N >= 256 && K % 64 == 0)
+      return launch_gemm_pp<256, 256, 2, 4>(M, N, K, ksplit, la, lb, ep, st);
+    if (pp == 3 && mm && N >= 256 && K % 64 == 0) return launch_gemm_pp<128, 256, 2, 4>(M, N, K, ksplit, la, lb, ep, st);
+    if (pp == 4 && kk && M >= 256 && N == 128 && K % 64 == 0)
+      return launch_gemm_pp<256, 128, 2, 4>(M, N, K, ksplit, la, lb, ep, st);
+  }
+  if constexpr (kk) {
     if (M >= 256 && N >= 256) return launch_gemm_big<256, 256, 2, 4>(M, N, K, ksplit, la, lb, ep, st);
   }
   if (N >= 256) return launch_gemm_big<128, 256, 2, 4>(M, N, K, ksplit, la, lb, ep, st);
