@@ -45,7 +45,7 @@ struct GemmShape {
   int kchunk;   // K range per split (multiple of BK); == K rounded up when no split
   int tiles_m, tiles_n;
   int xsplit;   // 1: split-K grid is 1-D and every split's tiles share one XCD
-  int dbg;      // diagnostics (VLP_GEMM_DBG, ms kernel): 1 skip epilogue, 2/4 freeze A/B MN rows
+  int dbg;      // reserved (0)
   int nsplit;   // K-splits (bk / big kernels: 1-D grid of nsplit * tiles)
 };
 
@@ -342,9 +342,6 @@ __device__ __forceinline__ void static_for(Fn&& fn) {
 }
 template <bool KC, int RB>
 __device__ __forceinline__ v8bf frag_big(const char* lds, int rb, int s) {
-#ifdef VLP_DBG_NOTR   // timing-only experiment: MN images read as if K-contig (wrong values)
-  return frag_bf16<true, RB, true>(lds, rb, s);
-#endif
   if constexpr (KC) return frag_bf16<true, RB, true>(lds, rb, s);
   else return frag_tr_asm<RB>(lds, rb, s);
 }
@@ -866,8 +863,8 @@ gemm_ms_kernel(GemmShape sh, LA la, LB lb, EP ep) {
     }
     if (t + S - 1 < nk) {
       char* f = smem + fill * STAGE;
-      sa.issue(la, kb + (t + S - 1) * BK, f, sh.dbg & 2);
-      sb.issue(lb, kb + (t + S - 1) * BK, f + ABYTES, sh.dbg & 4);
+      sa.issue(la, kb + (t + S - 1) * BK, f, false);
+      sb.issue(lb, kb + (t + S - 1) * BK, f + ABYTES, false);
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -881,15 +878,6 @@ gemm_ms_kernel(GemmShape sh, LA la, LB lb, EP ep) {
     fill = (fill + 1 == S) ? 0 : fill + 1;
   }
   __syncthreads();   // all waves done with the ring before the epilogue reuses LDS
-  if (sh.dbg & 1) {   // diagnostics: no epilogue (acc kept live)
-    float z = 0.f;
-#pragma unroll
-    for (int a = 0; a < MB; ++a)
-#pragma unroll
-      for (int b = 0; b < NB; ++b) z += acc[a][b][0] + acc[a][b][3];
-    if (z == 1234.5f) ep(row0, col0, acc[0][0], acc[0][0], acc[0][0]);
-    return;
-  }
 
   static_assert(!StageTrait<EP>::value || 4096 + BM * BN * 2 <= S * STAGE, "staging tile fits the ring");
   ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep, acc, row0, col0, wid, wm, wn, smem);
@@ -1257,15 +1245,6 @@ gemm_big_kernel(GemmShape sh, LA la, LB lb, EP ep) {
     body(std::integral_constant<int, 1>{}, t + 1);
   }
   __syncthreads();   // ring drained (incl. the null-resource tail fetches) before LDS is reused
-  if (sh.dbg & 1) {   // diagnostics: no epilogue (acc kept live)
-    float z = 0.f;
-#pragma unroll
-    for (int a = 0; a < MB; ++a)
-#pragma unroll
-      for (int b = 0; b < NB; ++b) z += acc[a][b][0] + acc[a][b][3];
-    if (z == 1234.5f) ep(row0, col0, acc[0][0], acc[0][0], acc[0][0]);
-    return;
-  }
   if constexpr (SplitTrait<EP>::value) {
     ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep.at_split(split), acc, row0, col0, wid, wm, wn, smem);
   } else {
@@ -1377,10 +1356,6 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   const int wm = wv / WGN, wn = wv - wm * WGN;
   const int grp = wm, wg = wn;
 
-  SA sa;
-  SB sb;
-  if (grp == 0) sa.init(la, row0, kb, wg);
-  else sb.init(lb, col0, kb, wg);
   const rsrc_t ra = la.rsrc(), rb = lb.rsrc();
   const rsrc_t rz = null_rsrc(zero_page());
   v4f acc[MB][NB];
@@ -1393,28 +1368,6 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   // parity = the half of its 64-deep step); nh % 4 == 2 starts at slot 2 so
   // the 4-phase unrolled loop ends on slot 3
   const int off = nh & 2;
-  auto fetchA = [&](auto hc, int u, char* slot) __attribute__((always_inline)) {
-    sa.template issue<decltype(hc)::value>(la, u < nh ? ra : rz, kb + (u >> 1) * BK, slot, wg);
-  };
-  auto fetchB = [&](auto hc, int u, char* slot) __attribute__((always_inline)) {
-    sb.template issue<decltype(hc)::value>(lb, u < nh ? rb : rz, kb + (u >> 1) * BK, slot + HA, wg);
-  };
-  using H0 = std::integral_constant<int, 0>;
-  using H1 = std::integral_constant<int, 1>;
-  if (grp == 0) {
-    fetchA(H0{}, 0, smem + off * SLOT);
-    fetchA(H1{}, 1, smem + ((off + 1) & 3) * SLOT);
-    wait_vmcnt<SA::P>();
-  } else {
-    fetchB(H0{}, 0, smem + off * SLOT);
-    fetchB(H1{}, 1, smem + ((off + 1) & 3) * SLOT);
-    fetchB(H0{}, 2, smem + ((off + 2) & 3) * SLOT);
-    wait_vmcnt<2 * SB::P>();
-  }
-  raw_barrier();
-  if (grp == 1) raw_barrier();   // the stagger
-  __builtin_amdgcn_sched_barrier(0);
-
   const int lane = threadIdx.x & 63;
   const int fi = lane & 15, fg = lane >> 4;
   const char* fbase = smem + fi * 64 + (pp_chunk(fi, fg) << 4);
@@ -1434,59 +1387,90 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
       for (int b = 0; b < QB; ++b) bbase[p][b] = mn_frag_base<BN * 2>(smem + 2 * p * SLOT + HA, wn * WTN + b * 16);
   }
 
-  auto phase = [&](auto slc, int q) __attribute__((always_inline)) {
-    constexpr int SL = decltype(slc)::value;
-    constexpr int SO = (SL & 1) * SLOT;   // offset inside the slot pair
-    v8bf fa[MB], fb[NB];
-    static_for<0, MB>([&](auto ac) {
-      constexpr int a = decltype(ac)::value;
-      if constexpr (LA::kKContig)
-        fa[a] = *reinterpret_cast<const v8bf*>(fbase + SL * SLOT + (wm * WTM + a * 16) * 64);
-      else
-        fa[a] = frag_tr_at<SO + (a >> 2) * 1024>(abase[SL >> 1][a & 3]);
-    });
-    static_for<0, NB>([&](auto bc) {
-      constexpr int b = decltype(bc)::value;
-      if constexpr (LB::kKContig)
-        fb[b] = *reinterpret_cast<const v8bf*>(fbase + SL * SLOT + HA + (wn * WTN + b * 16) * 64);
-      else
-        fb[b] = frag_tr_at<SO + (b >> 2) * 1024>(bbase[SL >> 1][b & 3]);
-    });
-    if (grp == 0) {
-      fetchA(std::integral_constant<int, SL & 1>{}, q + 2, smem + ((SL + 2) & 3) * SLOT);
+  // the main loop of one wave group: group 0 holds only A's loader state,
+  // group 1 only B's (the two paths share the register allocation)
+  auto run = [&](auto gc) __attribute__((always_inline)) {
+    constexpr int G = decltype(gc)::value;
+    using S = std::conditional_t<G == 0, SA, SB>;
+    S ss;
+    if constexpr (G == 0) ss.init(la, row0, kb, wg);
+    else ss.init(lb, col0, kb, wg);
+    auto fetch = [&](auto hc, int u, char* slot) __attribute__((always_inline)) {
+      if constexpr (G == 0) ss.template issue<decltype(hc)::value>(la, u < nh ? ra : rz, kb + (u >> 1) * BK, slot, wg);
+      else ss.template issue<decltype(hc)::value>(lb, u < nh ? rb : rz, kb + (u >> 1) * BK, slot + HA, wg);
+    };
+    using H0 = std::integral_constant<int, 0>;
+    using H1 = std::integral_constant<int, 1>;
+    if constexpr (G == 0) {
+      fetch(H0{}, 0, smem + off * SLOT);
+      fetch(H1{}, 1, smem + ((off + 1) & 3) * SLOT);
+      wait_vmcnt<S::P>();
     } else {
-      fetchB(std::integral_constant<int, 1 - (SL & 1)>{}, q + 3, smem + ((SL + 3) & 3) * SLOT);
-      wait_vmcnt<2 * SB::P>();
+      fetch(H0{}, 0, smem + off * SLOT);
+      fetch(H1{}, 1, smem + ((off + 1) & 3) * SLOT);
+      fetch(H0{}, 2, smem + ((off + 2) & 3) * SLOT);
+      wait_vmcnt<2 * S::P>();
     }
-    __builtin_amdgcn_sched_barrier(0);
     raw_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (G == 1) raw_barrier();   // the stagger
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
+
+    auto phase = [&](auto slc, int q) __attribute__((always_inline)) {
+      constexpr int SL = decltype(slc)::value;
+      constexpr int SO = (SL & 1) * SLOT;   // offset inside the slot pair
+      v8bf fa[MB], fb[NB];
+      static_for<0, MB>([&](auto ac) {
+        constexpr int a = decltype(ac)::value;
+        if constexpr (LA::kKContig)
+          fa[a] = *reinterpret_cast<const v8bf*>(fbase + SL * SLOT + (wm * WTM + a * 16) * 64);
+        else
+          fa[a] = frag_tr_at<SO + (a >> 2) * 1024>(abase[SL >> 1][a & 3]);
+      });
+      static_for<0, NB>([&](auto bc) {
+        constexpr int b = decltype(bc)::value;
+        if constexpr (LB::kKContig)
+          fb[b] = *reinterpret_cast<const v8bf*>(fbase + SL * SLOT + HA + (wn * WTN + b * 16) * 64);
+        else
+          fb[b] = frag_tr_at<SO + (b >> 2) * 1024>(bbase[SL >> 1][b & 3]);
+      });
+      if constexpr (G == 0) {
+        fetch(std::integral_constant<int, SL & 1>{}, q + 2, smem + ((SL + 2) & 3) * SLOT);
+      } else {
+        fetch(std::integral_constant<int, 1 - (SL & 1)>{}, q + 3, smem + ((SL + 3) & 3) * SLOT);
+        wait_vmcnt<2 * S::P>();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      raw_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int a = 0; a < MB; ++a)
+      for (int a = 0; a < MB; ++a)
 #pragma unroll
-      for (int b = 0; b < NB; ++b)
-        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], acc[a][b], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    if (grp == 0) wait_vmcnt<SA::P>();
-    __builtin_amdgcn_sched_barrier(0);
-    raw_barrier();
-    __builtin_amdgcn_sched_barrier(0);
+        for (int b = 0; b < NB; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], acc[a][b], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if constexpr (G == 0) wait_vmcnt<S::P>();
+      __builtin_amdgcn_sched_barrier(0);
+      raw_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    int q = 0;
+    if (off) {
+      phase(std::integral_constant<int, 2>{}, 0);
+      phase(std::integral_constant<int, 3>{}, 1);
+      q = 2;
+    }
+    for (; q < nh; q += 4) {
+      phase(std::integral_constant<int, 0>{}, q);
+      phase(std::integral_constant<int, 1>{}, q + 1);
+      phase(std::integral_constant<int, 2>{}, q + 2);
+      phase(std::integral_constant<int, 3>{}, q + 3);
+    }
+    if constexpr (G == 0) raw_barrier();   // matches group 1's stagger barrier
   };
-  int q = 0;
-  if (off) {
-    phase(std::integral_constant<int, 2>{}, 0);
-    phase(std::integral_constant<int, 3>{}, 1);
-    q = 2;
-  }
-  for (; q < nh; q += 4) {
-    phase(std::integral_constant<int, 0>{}, q);
-    phase(std::integral_constant<int, 1>{}, q + 1);
-    phase(std::integral_constant<int, 2>{}, q + 2);
-    phase(std::integral_constant<int, 3>{}, q + 3);
-  }
-  if (grp == 0) raw_barrier();   // matches group 1's stagger barrier
+  if (grp == 0) run(std::integral_constant<int, 0>{});
+  else run(std::integral_constant<int, 1>{});
   __syncthreads();   // ring drained (incl. the null-resource tail fetches) before LDS is reused
   if constexpr (SplitTrait<EP>::value) {
     ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep.at_split(split), acc, row0, col0, wid, wm, wn, smem);
@@ -1577,8 +1561,6 @@ inline int launch_gemm_ms(int M, int N, int K, int ksplit, const LA& la, const L
   if (ksplit < 1) ksplit = 1;
   sh.kchunk = kc;
   sh.xsplit = (ksplit >= 8 && ksplit % 8 == 0) ? 1 : 0;
-  static const int dbg = getenv("VLP_GEMM_DBG") ? atoi(getenv("VLP_GEMM_DBG")) : 0;
-  sh.dbg = dbg;
   dim3 grid = sh.xsplit ? dim3(sh.tiles_m * sh.tiles_n * ksplit, 1, 1)
                         : dim3(sh.tiles_m * sh.tiles_n, ksplit, 1);
   constexpr int lds = S * (BM + BN) * 128;
@@ -1633,8 +1615,6 @@ inline int launch_gemm_bk(int M, int N, int K, int ksplit, const LA& la, const L
   sh.xsplit = 0;
   sh.nsplit = ksplit;
   last_ksplit() = ksplit;
-  static const int dbg = getenv("VLP_GEMM_DBG") ? atoi(getenv("VLP_GEMM_DBG")) : 0;
-  sh.dbg = dbg;
   dim3 grid(sh.tiles_m * sh.tiles_n * ksplit, 1, 1);
   constexpr int lds = S * (BM + BN) * 128;
   static_assert(lds <= 160 * 1024, "LDS budget");
@@ -1688,8 +1668,6 @@ inline int launch_gemm_big(int M, int N, int K, int ksplit, const LA& la, const 
   sh.xsplit = 0;
   sh.nsplit = ksplit;
   last_ksplit() = ksplit;
-  static const int dbg = getenv("VLP_GEMM_DBG") ? atoi(getenv("VLP_GEMM_DBG")) : 0;
-  sh.dbg = dbg;
   dim3 grid(sh.tiles_m * sh.tiles_n * ksplit, 1, 1);
   constexpr int lds = big_lds_bytes<BM, BN, EP>();
   static_assert(lds <= 160 * 1024, "LDS budget");
@@ -1788,16 +1766,16 @@ inline int gemm_big_auto(int M, int N, int K, int ksplit, const LA& la, const LB
   // (256x256 keeps 128x64 fragments per wave live: only the all-K-contig case
   // fits the 256-VGPR budget without spilling)
   // ping-pong schedule (gemm_pp_kernel): 1 = K-contig x K-contig, 2 = also MN x MN
-  // (default 1: +0.8 % per step, the 256x256 forward / data-gradient GEMMs +3 %)
-  static const int pp = getenv("VLP_PP") ? atoi(getenv("VLP_PP")) : 1;
+  // (default 2, measured per step: K-contig +0.4-0.8 % (the 256x256 forward /
+  // data-gradient GEMMs +3 %), MN x MN weight gradients another +2.4 % (layers
+  // 3-4 +10-19 %); the 128x256 MN tiles of layer 2 lose (-10 %) and stay on
+  // gemm_big_kernel, as do 256x128 K-contig tiles)
+  static const int pp = getenv("VLP_PP") ? atoi(getenv("VLP_PP")) : 2;
   constexpr bool kk = LA::kKContig && LB::kKContig;
   constexpr bool mm = !LA::kKContig && !LB::kKContig;
   if constexpr (kk || mm) {
     if (pp >= (kk ? 1 : 2) && M >= 256 && N >= 256 && K % 64 == 0)
       return launch_gemm_pp<256, 256, 2, 4>(M, N, K, ksplit, la, lb, ep, st);
-    if (pp == 3 && mm && N >= 256 && K % 64 == 0) return launch_gemm_pp<128, 256, 2, 4>(M, N, K, ksplit, la, lb, ep, st);
-    if (pp == 4 && kk && M >= 256 && N == 128 && K % 64 == 0)
-      return launch_gemm_pp<256, 128, 2, 4>(M, N, K, ksplit, la, lb, ep, st);
   }
   if constexpr (kk) {
     if (M >= 256 && N >= 256) return launch_gemm_big<256, 256, 2, 4>(M, N, K, ksplit, la, lb, ep, st);
