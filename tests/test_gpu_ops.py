@@ -59,6 +59,10 @@ CONV_CASES = [
     (4, 14, 14, 256, 512, 3, 3, 2, 1),  # layer-4 stride-2 block at 224 px
     (2, 16, 16, 96, 192, 3, 3, 1, 1),   # NesT ConvPool (C = 96: K-steps straddle filter taps)
     (2, 8, 8, 192, 384, 3, 3, 1, 1),    # NesT ConvPool, level 2
+    # ping-pong kernel (gemm_pp_kernel, bf16 M, N >= 256): K = 2880 is an odd number of
+    # 64-deep steps (the half-tile ring starts on slot 2); N = 320 / M = 297 end in partial tiles
+    (4, 8, 8, 320, 256, 3, 3, 1, 1),
+    (3, 9, 11, 256, 320, 3, 3, 1, 1),
 ]
 
 

@@ -770,9 +770,13 @@ VLP_EXPORT int vlp_linear_wgrad_ws(int dtype, int M, int Nout, int Kin, const vo
                                    void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (dtype != VLP_BF16 || Kin % 4 || !ws) return (int)hipErrorInvalidValue;
+  // each split reduces >= VLP_LINW_WS_ROWS token rows: the text tower runs on a
+  // side stream beside the image tower, where CU time per FLOP (prologue,
+  // epilogue, slab traffic), not latency, is what the step pays for
+  static const int rows = getenv("VLP_LINW_WS_ROWS") ? atoi(getenv("VLP_LINW_WS_ROWS")) : 256;
   const int tiles = ((Nout + 127) / 128) * ((Kin + 127) / 128);
   int ks = (512 + tiles - 1) / tiles;
-  const int maxsplit = (M + 255) / 256;
+  const int maxsplit = (M + rows - 1) / rows;
   if (ks > maxsplit) ks = maxsplit;
   while (ks > 1 && (long long)ks * Nout * Kin > ws_elems) --ks;
   int kc = (M + ks - 1) / ks;
@@ -858,8 +862,12 @@ static void ln_bwd_t(int M, int D, const void* dy, float p_out, unsigned long lo
                      const float* mean, const float* rstd, const float* gamma, void* dx, void* dxd, float p_in,
                      unsigned long long seed_in, float* dgamma, float* dbeta, const void* addend,
                      const float* rscale, int rps, hipStream_t st) {
+  // rows are strided over a capped grid: every block ends in one dgamma / dbeta
+  // atomic per column, so the grid size is the atomic fan-in per address
+  // (640 blocks at M = 10240 serialised on 624 addresses: 36 us per launch)
+  static const int cap = getenv("VLP_LNB_BLOCKS") ? atoi(getenv("VLP_LNB_BLOCKS")) : 160;
   int blocks = (M + 15) / 16;
-  if (blocks > 4096) blocks = 4096;
+  if (blocks > cap) blocks = cap;
   hipLaunchKernelGGL((layernorm_bwd_kernel<T, NCH>), dim3(blocks), dim3(256), 0, st, M, D, (const T*)dy, p_out,
                      (uint64_t)seed_out, (const T*)x, mean, rstd, gamma, (T*)dx, (T*)dxd, p_in, (uint64_t)seed_in,
                      dgamma, dbeta, (const T*)addend, rscale, rps);

@@ -1324,7 +1324,7 @@ struct HStager<BM, L, NTG, false> {
 template <int BM, int BN, int WGM, int WGN, class LA, class LB, class EP>
 __global__ void __launch_bounds__(WGM * WGN * 64) __attribute__((amdgpu_waves_per_eu(2)))
 gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
-  static_assert(WGM == 2, "two M-half wave groups");
+  static_assert(WGM % 2 == 0, "two M-half wave groups");
   constexpr int NT = WGM * WGN * 64, NTG = NT / 2;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int MB = WTM / 16, NB = WTN / 16;
@@ -1354,7 +1354,7 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   const int nh = 2 * (nk > 0 ? nk : 0);
   const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int wm = wv / WGN, wn = wv - wm * WGN;
-  const int grp = wm, wg = wn;
+  const int grp = wm / (WGM / 2), wg = wv - grp * (WGM / 2) * WGN;
 
   const rsrc_t ra = la.rsrc(), rb = lb.rsrc();
   const rsrc_t rz = null_rsrc(zero_page());
