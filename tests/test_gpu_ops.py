@@ -62,6 +62,7 @@ CONV_CASES = [
     # ping-pong kernel (gemm_pp_kernel, bf16 M, N >= 256): K = 2880 is an odd number of
     # 64-deep steps (the half-tile ring starts on slot 2); N = 320 / M = 297 end in partial tiles
     (4, 8, 8, 320, 256, 3, 3, 1, 1),
+    (2, 12, 12, 128, 128, 3, 3, 1, 1),  # Co = 128 weight gradient: 128x384 ping-pong tiles
     (3, 9, 11, 256, 320, 3, 3, 1, 1),
 ]
 

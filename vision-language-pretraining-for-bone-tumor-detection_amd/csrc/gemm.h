@@ -711,7 +711,7 @@ __device__ __forceinline__ void ms_epilogue(const GemmShape& sh, const EP& ep, v
   constexpr int CPR = BN / 8;
   bf16* stg = reinterpret_cast<bf16*>(smem + 4096);
   
-  static_assert(WGM * BN * 2 * 4 <= 4096, "stats scratch");
+  static_assert(!EP::kStats || WGM * BN * 2 * 4 <= 4096, "stats scratch");
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const int coll = wn * WTN + b * 16 + 4 * lg;
@@ -1776,6 +1776,12 @@ inline int gemm_big_auto(int M, int N, int K, int ksplit, const LA& la, const LB
   if constexpr (kk || mm) {
     if (pp >= (kk ? 1 : 2) && M >= 256 && N >= 256 && K % 64 == 0)
       return launch_gemm_pp<256, 256, 2, 4>(M, N, K, ksplit, la, lb, ep, st);
+  }
+  if constexpr (mm) {
+    // Co = 128 weight gradients (layer 2, N = 9 * 128 = 3 * 384): 128x384 tiles,
+    // a 64x96 per-wave tile (20 transposing reads per 24 MFMAs)
+    if (pp >= 2 && pp != 7 && M > 64 && M <= 128 && N % 384 == 0 && K % 64 == 0)
+      return launch_gemm_pp<128, 384, 2, 4>(M, N, K, ksplit, la, lb, ep, st);
   }
   if constexpr (kk) {
     if (M >= 256 && N >= 256) return launch_gemm_big<256, 256, 2, 4>(M, N, K, ksplit, la, lb, ep, st);
