@@ -864,10 +864,13 @@ static void ln_bwd_t(int M, int D, const void* dy, float p_out, unsigned long lo
                      const float* rscale, int rps, hipStream_t st) {
   // rows are strided over a capped grid: every block ends in one dgamma / dbeta
   // atomic per column, so the grid size is the atomic fan-in per address
-  // (640 blocks at M = 10240 serialised on 624 addresses: 36 us per launch)
+  // (640 blocks at M = 10240 serialised on 624 addresses: 36 us per launch);
+  // the cap applies to text-sized M only: NesT's 0.1-2 M token rows need the
+  // wide grid for bandwidth (a 160 or M/2048 cap there: -3 % per NesT step)
   static const int cap = getenv("VLP_LNB_BLOCKS") ? atoi(getenv("VLP_LNB_BLOCKS")) : 160;
   int blocks = (M + 15) / 16;
-  if (blocks > cap) blocks = cap;
+  const int lim = M <= 65536 ? cap : 4096;
+  if (blocks > lim) blocks = lim;
   hipLaunchKernelGGL((layernorm_bwd_kernel<T, NCH>), dim3(blocks), dim3(256), 0, st, M, D, (const T*)dy, p_out,
                      (uint64_t)seed_out, (const T*)x, mean, rstd, gamma, (T*)dx, (T*)dxd, p_in, (uint64_t)seed_in,
                      dgamma, dbeta, (const T*)addend, rscale, rps);
