@@ -89,6 +89,13 @@ static int gemm_lin(int M, int N, int K, int ksplit, const LA& la, const LB& lb,
                     hipStream_t st) {
   if (N <= 64) return gemm_narrow<T>(M, N, K, ksplit, la, lb, ep, st);
   if (M <= 1024) return launch_gemm<T, 64, 256, 1>(M, N, K, ksplit, la, lb, ep, st);
+  // large same-layout GEMMs (NesT level-2 projections: M = 131 k tokens, K = 384 / 1536)
+  // take the 256x256 ping-pong kernel the convolutions use
+  if constexpr (use_bk<T, LA, LB>() && LA::kKContig == LB::kKContig) {
+    static const int lin_pp = getenv("VLP_LIN_PP") ? atoi(getenv("VLP_LIN_PP")) : 1;
+    if (lin_pp && gemm_variant() >= 5 && M >= 256 && N >= 256 && K >= 256 && K % 64 == 0)
+      return gemm_big_auto(M, N, K, ksplit, la, lb, ep, st);
+  }
   return gemm_wide<T>(M, N, K, ksplit, la, lb, ep, st);
 }
 
@@ -785,7 +792,20 @@ VLP_EXPORT int vlp_linear_wgrad_ws(int dtype, int M, int Nout, int Kin, const vo
   MNMat<bf16> la{(const bf16*)dy, lddy, Nout, M};
   MNMat<bf16> lb{(const bf16*)x, ldx, Kin, M};
   EpiSplitStore ep{nullptr, nullptr, ws, Kin, (size_t)Nout * Kin};
-  int r = launch_gemm_bk<128, 128, 2, 2>(Nout, Kin, M, ks, la, lb, ep, st);
+  static const int lin_pp = getenv("VLP_LIN_PP") ? atoi(getenv("VLP_LIN_PP")) : 1;
+  int r;
+  if (lin_pp && gemm_variant() >= 5 && Nout >= 256 && Kin >= 256 && M >= 16384 && M % 64 == 0) {
+    // deep token reductions (NesT level 2) on the 256x256 ping-pong kernel: one
+    // round of 256 workgroups, >= 2048 tokens per split, within the workspace
+    const int t256 = ((Nout + 255) / 256) * ((Kin + 255) / 256);
+    int k2 = (256 + t256 - 1) / t256;
+    if (k2 > M / 2048) k2 = M / 2048 > 0 ? M / 2048 : 1;
+    while (k2 > 1 && (long long)k2 * Nout * Kin > ws_elems) --k2;
+    r = launch_gemm_pp<256, 256, 2, 4>(Nout, Kin, M, k2, la, lb, ep, st);
+    ks = last_ksplit();
+  } else {
+    r = launch_gemm_bk<128, 128, 2, 2>(Nout, Kin, M, ks, la, lb, ep, st);
+  }
   if (r) return r;
   const size_t n4 = (size_t)Nout * Kin / 4;
   int blocks = (int)((n4 + 255) / 256);
