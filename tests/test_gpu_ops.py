@@ -341,7 +341,8 @@ def test_bn_bwd_apply_transposed(ops, has_b, bcast, C):
 
 
 @pytest.mark.parametrize("dt", DT)
-@pytest.mark.parametrize("shape", [(640, 936, 312), (300, 312, 1200), (1100, 312, 312)])
+@pytest.mark.parametrize("shape", [(640, 936, 312), (300, 312, 1200), (1100, 312, 312),
+                                   (16384, 384, 1152)])   # deep token reduction: ping-pong kernel (bf16)
 def test_linear_wgrad(ops, dt, shape):
     """dW += dy^T x (TinyBERT weight gradients): fp32 atomic split-K and the bf16
     split-K workspace path (vlp_linear_wgrad_ws) against fp32 math."""
@@ -354,6 +355,25 @@ def test_linear_wgrad(ops, dt, shape):
     ops.linear_wgrad(dy.to(dt).cuda(), x.to(dt).cuda(), dw, M, Nout, Kin)
     torch.cuda.synchronize()
     assert rel(dw, ref) < tol(dt) / 4
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("M,N,K", [(512, 1152, 384), (300, 384, 1536)])
+def test_linear_fwd_dgrad_large(ops, dt, M, N, K):
+    """y = x W^T + b and dx = dy W at NesT level-2 sizes (M, N, K >= 256: the 256x256
+    ping-pong kernel in bf16; M = 300 ends in a partial tile) against fp32 math."""
+    torch.manual_seed(8)
+    x = torch.randn(M, K).to(dt).float()
+    w = (torch.randn(N, K) * K ** -0.5).to(dt).float()
+    b = torch.randn(N)
+    y = torch.empty(M, N, device="cuda", dtype=dt)
+    ops.linear_fwd(x.to(dt).cuda(), w.to(dt).cuda(), b.cuda(), y, M, N, K)
+    dy = torch.randn(M, N).to(dt).float()
+    dx = torch.empty(M, K, device="cuda", dtype=dt)
+    ops.linear_dgrad(dy.to(dt).cuda(), w.to(dt).cuda(), dx, M, K, N)
+    torch.cuda.synchronize()
+    assert rel(y.float().cpu(), x @ w.t() + b) < tol(dt) / 2
+    assert rel(dx.float().cpu(), dy @ w) < tol(dt) / 2
 
 
 @pytest.mark.parametrize("M,N,ld,off", [(10240, 312, 312, 0), (10240, 1200, 1200, 0), (777, 936, 944, 8),

@@ -91,10 +91,15 @@ static int gemm_lin(int M, int N, int K, int ksplit, const LA& la, const LB& lb,
   if (M <= 1024) return launch_gemm<T, 64, 256, 1>(M, N, K, ksplit, la, lb, ep, st);
   // large same-layout GEMMs (NesT level-2 projections: M = 131 k tokens, K = 384 / 1536)
   // take the 256x256 ping-pong kernel the convolutions use
-  if constexpr (use_bk<T, LA, LB>() && LA::kKContig == LB::kKContig) {
-    static const int lin_pp = getenv("VLP_LIN_PP") ? atoi(getenv("VLP_LIN_PP")) : 1;
-    if (lin_pp && gemm_variant() >= 5 && M >= 256 && N >= 256 && K >= 256 && K % 64 == 0)
-      return gemm_big_auto(M, N, K, ksplit, la, lb, ep, st);
+  if constexpr (use_bk<T, LA, LB>()) {
+    // VLP_LIN_PP: 0 off, 1 same-layout GEMMs only, 2 (default) also the data gradients
+    // (NesT step +2.6 % and +0.7 %)
+    static const int lin_pp = getenv("VLP_LIN_PP") ? atoi(getenv("VLP_LIN_PP")) : 2;
+    if (lin_pp && gemm_variant() >= 5 && M >= 256 && N >= 256 && K >= 256 && K % 64 == 0) {
+      if constexpr (LA::kKContig == LB::kKContig) return gemm_big_auto(M, N, K, ksplit, la, lb, ep, st);
+      // data gradients (K-contig dy x MN-contig W)
+      else if (lin_pp >= 2) return launch_gemm_pp<256, 256, 2, 4>(M, N, K, ksplit, la, lb, ep, st);
+    }
   }
   return gemm_wide<T>(M, N, K, ksplit, la, lb, ep, st);
 }
