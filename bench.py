@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--kernel-report", default="")
     ap.add_argument("--pcie-steps", type=int, default=5,
                     help="steps timed with the batch copied from pinned host memory (0: skip)")
+    ap.add_argument("--wgrad-stream-steps", type=int, default=10,
+                    help="steps timed with the weight gradients on a side stream, reported beside value (0: skip)")
     a = ap.parse_args()
     nest = a.image_model != "resnet34"
     if a.batch is None:
@@ -363,6 +365,25 @@ def main():
     tot = ktimer.totals().get(tk, (0.0, 0, 0.0))
     # the same K steps on a batch already resident in HBM (no upload at all)
     el_hbm, _ = timed(lambda: [step() for _ in range(args.steps)])
+    # the same K prefetched steps with the image tower's weight gradients on a side
+    # stream beside the data-gradient chain (vlp_amd.resnet34 VLP_WGRAD_STREAM): its
+    # MFMA-bound launches then overlap the HBM-bound BN passes and the epilogue
+    # bursts.  Reported beside `value`, not as it: those launches share the CUs, so
+    # the per-kernel roofline above is timed with the stream off
+    wgs = None
+    if args.image_model == "resnet34" and args.wgrad_stream_steps > 0:
+        from vlp_amd import resnet34 as _r34
+        was = _r34._USE_WG_STREAM
+        _r34._USE_WG_STREAM = True
+        try:
+            prefetched_steps(2)
+            ktimer.enable(tk)
+            el_ws, _ = timed(lambda: prefetched_steps(args.wgrad_stream_steps))
+            ktimer.disable()
+            tws = ktimer.totals().get(tk, (0.0, 0, 0.0))
+        finally:
+            _r34._USE_WG_STREAM = was
+        wgs = (el_ws, tws)
     pcie = pcie_inclusive(args, model, opt, world, dev) if args.pcie_steps > 0 else None
     ldelta = loss_delta_vs_fp32(args, model, host) if (world == 1 and args.loss_check) else None
     peak_meas = mfma_peak_measured(dev) if args.dtype == "bf16" else None
@@ -407,6 +428,15 @@ def main():
             "hbm_resident": {"value": round(pairs / el_hbm, 2), "ms_per_step": round(el_hbm / args.steps * 1e3, 3),
                              "note": "same steps, batch resident in HBM (no upload)"},
         }
+        if wgs is not None:
+            el_ws, (ms_w, nl_w, fl_w) = wgs
+            pw = world * args.batch * args.wgrad_stream_steps
+            res["wgrad_stream"] = {"value": round(pw / el_ws, 2),
+                                   "ms_per_step": round(el_ws / args.wgrad_stream_steps * 1e3, 3),
+                                   "steps": args.wgrad_stream_steps,
+                                   "roofline_kernel_achieved": round((fl_w / (ms_w / 1e3)) / 1e12, 2) if ms_w > 0 else None,
+                                   "note": "same prefetched steps, weight gradients on a side stream (VLP_WGRAD_STREAM=1); "
+                                           "their launches share the CUs with the data-gradient chain"}
         if ldelta is not None:
             res["loss_delta_vs_fp32"] = ldelta
         if pcie is not None:
