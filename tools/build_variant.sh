@@ -6,9 +6,12 @@ ROOT=$(cd $(dirname $0)/.. && pwd)
 CSRC=$ROOT/vision-language-pretraining-for-bone-tumor-detection_amd/csrc
 OUT=$ROOT/build_exp/$NAME
 mkdir -p $OUT/obj
-for f in conv_ops bn_ops bert_ops head_ops optim_ops probe_ops retrieval_ops; do
+for f in conv_ops bn_ops bert_ops head_ops optim_ops probe_ops retrieval_ops nest_ops prep_ops; do
+  EXTRA=""
+  [ $f = nest_ops ] && EXTRA="-mllvm -amdgpu-mfma-vgpr-form=1"
+  [ $f = prep_ops ] && EXTRA="-ffp-contract=off"
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -fvisibility=hidden \
-    -Wno-unused-result $FLAGS -c $CSRC/$f.hip -o $OUT/obj/$f.o &
+    -Wno-unused-result $EXTRA $FLAGS -c $CSRC/$f.hip -o $OUT/obj/$f.o &
 done
 wait
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $OUT/libvlp_hip.so $OUT/obj/*.o

@@ -1271,6 +1271,11 @@ gemm_big_kernel(GemmShape sh, LA la, LB lb, EP ep) {
 // half-tile retired behind a barrier (q+2 / q+3 land in slots last read in
 // phases q-2 / q-1), and half-tile q+1 is read only after both issuers'
 // counted waits and a barrier.
+// MFMA issue of a phase at raised wave priority (the partner wave's loads then
+// issue in the MFMA gaps, MI355X guide 8-phase template)
+#ifndef VLP_PP_PRIO
+#define VLP_PP_PRIO 1
+#endif
 __device__ __forceinline__ int pp_chunk(int r, int c) { return c ^ (((r >> 3) & 1) << 1); }
 template <int BM, class L, int NTG, bool KC = L::kKContig>
 struct HStager;
@@ -1443,13 +1448,17 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
       raw_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
+#if VLP_PP_PRIO
       __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
       for (int a = 0; a < MB; ++a)
 #pragma unroll
         for (int b = 0; b < NB; ++b)
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], acc[a][b], 0, 0, 0);
+#if VLP_PP_PRIO
       __builtin_amdgcn_s_setprio(0);
+#endif
       if constexpr (G == 0) wait_vmcnt<S::P>();
       __builtin_amdgcn_sched_barrier(0);
       raw_barrier();
