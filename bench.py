@@ -68,8 +68,17 @@ def parse():
     ap.add_argument("--kernel-report", default="")
     ap.add_argument("--pcie-steps", type=int, default=5,
                     help="steps timed with the batch copied from pinned host memory (0: skip)")
-    ap.add_argument("--wgrad-stream-steps", type=int, default=10,
-                    help="steps timed with the weight gradients on a side stream, reported beside value (0: skip)")
+    ap.add_argument("--wgrad-stream", type=int, default=1, choices=[0, 1],
+                    help="ResNet34 weight gradients on a side stream beside the data-gradient chain (default 1)")
+    ap.add_argument("--roofline-steps", type=int, default=5,
+                    help="steps of the isolated (serial-schedule) pass that times the roofline kernel")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo for CPU rehearsal)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU work: exercise the launcher, the rendezvous and the max-over-ranks timing "
+                         "and print the JSON line (CPU test of the N-rank path)")
+    ap.add_argument("--master-port", type=int, default=None,
+                    help="rendezvous port when bench.py launches its own ranks (default: a free port)")
     a = ap.parse_args()
     nest = a.image_model != "resnet34"
     if a.batch is None:
@@ -89,15 +98,79 @@ def flop_per_pair(args):
     return nest_flops_per_image(args.image_model, args.image_size) + 1.117e9
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv):
+    """`python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment:
+    start the N ranks as ONE child process tree (`python -m torch.distributed.run
+    --nproc-per-node N ... bench.py <same args>`), one process per GPU.  This
+    process has not touched the GPU (no HIP call before this point) and never
+    re-execs: it waits for the child, whose rank 0 prints the JSON line on the
+    inherited stdout, and returns the child's exit code."""
+    import subprocess
+    port = args.master_port or _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def setup_dist(args):
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if ws > 1:
         lr = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(lr)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", lr))
+        if args.gpus != ws:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}")
+        if args.backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(lr)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", lr))
         return dist.get_rank(), ws, lr
-    torch.cuda.set_device(0)
+    if args.gpus != 1:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} needs {args.gpus} ranks (run without WORLD_SIZE "
+                         "and bench.py launches them)")
+    if not args.dry_run:
+        torch.cuda.set_device(0)
     return 0, 1, 0
+
+
+def dry_run(args, rank, world):
+    """The N-rank bench path without GPU work: barrier-bracketed timed region,
+    max over ranks, rank 0 prints one JSON line with the same keys as a real run."""
+    def timed():
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        acc = torch.zeros(1 << 16)
+        for _ in range(args.steps):
+            acc.add_(1.0)
+        if world > 1:
+            dist.barrier()
+        e = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        return e.item()
+    el = max(timed(), 1e-9)
+    if rank == 0:
+        print(json.dumps({
+            "metric": f"image-text pairs/sec (fwd+bwd) at bs={args.batch}/GPU, 1/2/4/8 MI355X",
+            "value": round(world * args.batch * args.steps / el, 2), "unit": "image-text pairs/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(el / args.steps * 1e3, 6), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": args.dtype, "data": "dry run (no GPU work)",
+            "config": {"workload": "dry run of the launcher and rank timing", "global_batch": world * args.batch,
+                       "per_gpu_batch": args.batch, "parallelism": f"dp{world}"},
+            "backend": args.backend if world > 1 else None}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def make_batch(B, H, T, device, seed, form="fp32"):
@@ -283,7 +356,12 @@ def _traffic(family):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args, sys.argv[1:]))
     rank, world, local = setup_dist(args)
+    if args.dry_run:
+        dry_run(args, rank, world)
+        return
     from src.models.pretrain.VisionLanguageModule import VisionLanguageModule
     from vlp_amd import ktimer
     import functools
@@ -308,17 +386,32 @@ def main():
         opt.step()
         return loss
 
+    # schedule: the image tower's weight gradients run on a side stream beside
+    # the data-gradient chain (vlp_amd.resnet34._USE_WG_STREAM, the default).
+    # The roofline kernel is timed in a separate pass with the serial schedule,
+    # where its launches do not share the CUs with the data-gradient chain.
+    from vlp_amd import resnet34 as _r34
+    from vlp_amd._lib import lib as _vlib
+    resnet = args.image_model == "resnet34"
+
+    def set_wgrad_stream(on):
+        if resnet:
+            _r34._USE_WG_STREAM = bool(on) and args.wgrad_stream
+    set_wgrad_stream(True)
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # select the dominant kernel family to time (by total time in one step)
+    # select the dominant kernel family to time (by total time in one serial step)
     tk = args.roofline_kernel
     if tk == "auto":
+        set_wgrad_stream(False)
         ktimer.enable(None)
         step()
         torch.cuda.synchronize()
         totals = ktimer.totals()
         ktimer.disable()
+        set_wgrad_stream(True)
         tk = max(totals, key=lambda k: totals[k][0]) if totals else None
         if args.kernel_report and rank == 0:
             with open(args.kernel_report, "w") as f:
@@ -359,35 +452,36 @@ def main():
         return loss
 
     prefetched_steps(2)   # warm the copy stream and the pinned buffers
-    ktimer.enable(tk)
     el, loss = timed(lambda: prefetched_steps(args.steps))
+    # isolated roofline pass: serial schedule, the dominant family timed with HIP
+    # events on its launch stream; bracketed by marker dispatches so a rocprofv3
+    # kernel trace of this command averages exactly these launches
+    # (tools/roofline_window.py)
+    set_wgrad_stream(False)
+    prefetched_steps(1)
+    torch.cuda.synchronize()
+    _vlib().vlp_trace_marker(0, torch.cuda.current_stream(dev).cuda_stream)
+    ktimer.enable(tk)
+    el_serial, _ = timed(lambda: prefetched_steps(args.roofline_steps))
     ktimer.disable()
+    _vlib().vlp_trace_marker(1, torch.cuda.current_stream(dev).cuda_stream)
     tot = ktimer.totals().get(tk, (0.0, 0, 0.0))
+    # the same family under the default (stream) schedule, for reference
+    set_wgrad_stream(True)
+    shared = None
+    if resnet and args.wgrad_stream and tk and tk.startswith("conv_wgrad"):
+        prefetched_steps(1)
+        ktimer.enable(tk)
+        timed(lambda: prefetched_steps(args.roofline_steps))
+        ktimer.disable()
+        shared = ktimer.totals().get(tk, (0.0, 0, 0.0))
     # the same K steps on a batch already resident in HBM (no upload at all)
     el_hbm, _ = timed(lambda: [step() for _ in range(args.steps)])
-    # the same K prefetched steps with the image tower's weight gradients on a side
-    # stream beside the data-gradient chain (vlp_amd.resnet34 VLP_WGRAD_STREAM): its
-    # MFMA-bound launches then overlap the HBM-bound BN passes and the epilogue
-    # bursts.  Reported beside `value`, not as it: those launches share the CUs, so
-    # the per-kernel roofline above is timed with the stream off
-    wgs = None
-    if args.image_model == "resnet34" and args.wgrad_stream_steps > 0:
-        from vlp_amd import resnet34 as _r34
-        was = _r34._USE_WG_STREAM
-        _r34._USE_WG_STREAM = True
-        try:
-            prefetched_steps(2)
-            ktimer.enable(tk)
-            el_ws, _ = timed(lambda: prefetched_steps(args.wgrad_stream_steps))
-            ktimer.disable()
-            tws = ktimer.totals().get(tk, (0.0, 0, 0.0))
-        finally:
-            _r34._USE_WG_STREAM = was
-        wgs = (el_ws, tws)
     pcie = pcie_inclusive(args, model, opt, world, dev) if args.pcie_steps > 0 else None
     ldelta = loss_delta_vs_fp32(args, model, host) if (world == 1 and args.loss_check) else None
     peak_meas = mfma_peak_measured(dev) if args.dtype == "bf16" else None
     ms_k, nl, flop_k = tot
+    set_wgrad_stream(True)
     if rank == 0:
         pairs = world * args.batch * args.steps
         value = pairs / el
@@ -423,20 +517,21 @@ def main():
                          "flop_per_launch": round(flop_k / max(nl, 1)), "peak_measured": peak_meas,
                          "frac_of_measured": round(achieved / peak_meas, 4) if peak_meas else None,
                          "traffic_unit": "HBM bytes/launch",
-                         "traffic": _traffic(tk)},
+                         "traffic": _traffic(tk),
+                         "timed_in": f"isolated pass of {args.roofline_steps} steps, serial schedule "
+                                     "(bracketed by vlp_trace_marker dispatches)"},
             "loss": round(loss.item(), 5),
             "hbm_resident": {"value": round(pairs / el_hbm, 2), "ms_per_step": round(el_hbm / args.steps * 1e3, 3),
                              "note": "same steps, batch resident in HBM (no upload)"},
         }
-        if wgs is not None:
-            el_ws, (ms_w, nl_w, fl_w) = wgs
-            pw = world * args.batch * args.wgrad_stream_steps
-            res["wgrad_stream"] = {"value": round(pw / el_ws, 2),
-                                   "ms_per_step": round(el_ws / args.wgrad_stream_steps * 1e3, 3),
-                                   "steps": args.wgrad_stream_steps,
-                                   "roofline_kernel_achieved": round((fl_w / (ms_w / 1e3)) / 1e12, 2) if ms_w > 0 else None,
-                                   "note": "same prefetched steps, weight gradients on a side stream (VLP_WGRAD_STREAM=1); "
-                                           "their launches share the CUs with the data-gradient chain"}
+        ps = world * args.batch * args.roofline_steps
+        res["serial_schedule"] = {"value": round(ps / el_serial, 2),
+                                  "ms_per_step": round(el_serial / args.roofline_steps * 1e3, 3),
+                                  "steps": args.roofline_steps,
+                                  "note": "the roofline pass: same prefetched steps with the weight gradients on the "
+                                          "main stream (no CU sharing); `value` uses the side-stream schedule"}
+        if shared is not None and shared[0] > 0:
+            res["roofline"]["achieved_under_default_schedule"] = round((shared[2] / (shared[0] / 1e3)) / 1e12, 2)
         if ldelta is not None:
             res["loss_delta_vs_fp32"] = ldelta
         if pcie is not None:

@@ -37,6 +37,10 @@ int vlp_abi_version(void);
  * MFMA ceiling next to the vendor figure.
  * FLOP = blocks * 4 * iters * 8 * 16384; out: blocks * 256 floats. */
 int vlp_mfma_peak_probe(int blocks, int iters, float* out, void* stream);
+/* Diagnostic: an empty kernel dispatch (end = 0: begin marker, 1: end marker)
+ * that brackets bench.py's isolated roofline pass in a rocprofv3 kernel trace
+ * (tools/roofline_window.py).  No reference counterpart. */
+int vlp_trace_marker(int end, void* stream);
 
 /* ---------------- image tower: convolutions ----------------
  * Replace the cuDNN conv fwd/dgrad/wgrad calls made by timm resnet34

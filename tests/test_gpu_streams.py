@@ -1,0 +1,115 @@
+"""Cross-stream schedules must not change results.
+
+The training step runs work on three HIP streams: the main stream (image
+tower), the text-tower stream (TinyBERT forward/backward beside the image
+tower, clip_model._USE_TEXT_STREAM) and, optionally, the image tower's
+weight-gradient stream (resnet34._USE_WG_STREAM).  The split-K weight-gradient
+workspaces (ops.wgrad_ws / ops._linw_ws) are per (device, stream); before that
+fix the text stream's linear weight gradients and NesT's (main stream) shared
+one buffer, as did the side-stream conv weight gradients and the main-stream
+stem weight gradient.
+
+Test A: bf16 ResNet34 + TinyBERT step, weight-gradient stream on vs off.  The
+image tower's conv weight gradients come from deterministic split slabs, so
+they must equal the stream-off result bit for bit, or within 4x the run-to-run
+noise of two stream-off steps when that is not 0 (an fp64 BN-sum atomic landing
+on a rounding boundary).
+Test B: bf16 NesT + TinyBERT step at 64^2, text stream on vs off: every
+gradient within max(1e-6, 4 x run-to-run noise of either schedule) rel-L2.
+"""
+import functools
+
+import pytest
+import torch
+
+from tests.golden.synth import synth_batch
+
+pytestmark = pytest.mark.gpu
+
+
+def _grads(m, b):
+    for p in m.parameters():
+        p.grad = None
+    loss, *_ = m.training_step_outputs(b)
+    loss.backward()
+    torch.cuda.synchronize()
+    return loss.item(), {k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def test_wgrad_stream_matches_serial_bf16():
+    from src.models.pretrain.VisionLanguageModule import VisionLanguageModule
+    from vlp_amd import resnet34 as r34
+    torch.manual_seed(0)
+    m = VisionLanguageModule("resnet34", "tinybert", functools.partial(torch.optim.AdamW, lr=5e-5), False, False,
+                             512, 312, 128, compute_dtype="bf16", text_dropout=0.0)
+    m.train()
+    # non-zero bn2 gammas so every block's gradient path is live
+    with torch.no_grad():
+        for k, p in m.named_parameters():
+            if k.endswith("bn2.weight"):
+                p.fill_(0.5)
+    b = synth_batch(8, 128, 16, 3, with_u8=True)
+    b = {"x-ray-u8": b["x-ray-u8"].cuda(), "label": b["label"], "caption": b["caption"],
+         "caption_tokenized": {k: v.cuda() for k, v in b["caption_tokenized"].items()}}
+    was = r34._USE_WG_STREAM
+    try:
+        r34._USE_WG_STREAM = False
+        l0, g0 = _grads(m, b)
+        l1, g1 = _grads(m, b)
+        r34._USE_WG_STREAM = True
+        l2, g2 = _grads(m, b)
+        l3, g3 = _grads(m, b)
+    finally:
+        r34._USE_WG_STREAM = was
+    conv = [k for k in g0 if k.startswith("image_encoder.") and (".conv" in k or "downsample.0" in k)]
+    assert len(conv) == 36
+    for k in conv:
+        noise = (g0[k] - g1[k]).abs().max().item()
+        for g in (g2, g3):
+            d = (g[k] - g0[k]).abs().max().item()
+            assert d <= 4 * noise, (k, d, noise)
+    assert abs(l2 - l0) <= 4 * abs(l1 - l0) + 1e-7, (l0, l1, l2)
+
+
+def test_text_stream_matches_serial_nest_bf16():
+    from src.models.pretrain.VisionLanguageModule import VisionLanguageModule
+    from vlp_amd import clip_model as cm
+    torch.manual_seed(1)
+    m = VisionLanguageModule("nest_small", "tinybert", functools.partial(torch.optim.AdamW, lr=5e-5), False,
+                             False, 384, 312, 128, compute_dtype="bf16", text_dropout=0.0, image_size=64,
+                             drop_path_rate=0.0)
+    m.train()
+    b = synth_batch(8, 64, 24, 5, with_u8=True)
+    b = {"x-ray-u8": b["x-ray-u8"].cuda(), "label": b["label"], "caption": b["caption"],
+         "caption_tokenized": {k: v.cuda() for k, v in b["caption_tokenized"].items()}}
+    was = cm._USE_TEXT_STREAM
+    try:
+        cm._USE_TEXT_STREAM = False
+        l0, g0 = _grads(m, b)
+        l1, g1 = _grads(m, b)
+        cm._USE_TEXT_STREAM = True
+        l2, g2 = _grads(m, b)
+        l3, g3 = _grads(m, b)
+    finally:
+        cm._USE_TEXT_STREAM = was
+    assert len(g0) > 300
+    assert abs(l2 - l0) <= max(1e-6, 4 * abs(l1 - l0)), (l0, l1, l2)
+    worst = []
+    for k in g0:
+        if g0[k].norm() == 0:
+            continue
+        # run-to-run noise of each schedule (fp32 atomics in the LayerNorm /
+        # embedding backward reorder between runs)
+        noise = max(_rel(g1[k], g0[k]), _rel(g3[k], g2[k]))
+        tol = max(1e-6, 4 * noise)
+        for g in (g2, g3):
+            r = _rel(g[k], g0[k])
+            worst.append((r - tol, k, r, tol))
+    worst.sort()
+    print("text stream on vs off, worst (excess, name, rel, tol):", worst[-3:])
+    assert worst[-1][0] <= 0, worst[-3:]

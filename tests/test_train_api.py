@@ -136,10 +136,10 @@ class _Toy(torch.nn.Module):
         return ((self.w * batch["x"]).sum() - 1.0) ** 2
 
 
-def test_trainer_loop_semantics():
+def test_trainer_loop_semantics(tmp_path):
     m = _Toy()
     data = [{"x": torch.full((3,), float(i + 1))} for i in range(5)]
-    t = Trainer(max_epochs=3, log_every_n_steps=2, max_steps=7)
+    t = Trainer(max_epochs=3, log_every_n_steps=2, max_steps=7, default_root_dir=str(tmp_path))
     t.fit(m, train_dataloaders=data)
     assert t.global_step == 7 and t.current_epoch == 1
     assert [s for s, _ in t.history] == [2, 4, 6]
@@ -147,7 +147,7 @@ def test_trainer_loop_semantics():
     # the step really optimises: w moved away from ones by SGD
     assert not torch.allclose(m.w.detach(), torch.ones(3))
     m2 = _Toy()
-    Trainer(max_epochs=1, limit_train_batches=2).fit(m2, train_dataloaders=data)
+    Trainer(max_epochs=1, limit_train_batches=2, default_root_dir=str(tmp_path)).fit(m2, train_dataloaders=data)
     assert [c for c in m2.calls if isinstance(c, tuple)] == [("step", 0), ("step", 1)]
     with pytest.raises(ValueError):
         Trainer(min_epochs=3, max_epochs=2)
@@ -377,3 +377,65 @@ def test_datamodules_shard_per_rank_gloo_ws2():
     assert sorted(p0 + p1) == sorted(f"synthetic://downstream/{i}.png" for i in range(12))
     assert lw0 == lw1
     assert i0 != i1
+
+
+def test_shard_indices_pad_like_distributed_sampler():
+    """ranks must get equal sample (hence batch) counts; the pad wraps."""
+    from src.data.DownstreamDataModule import DownstreamDataModule as D
+    for n, world in ((257, 2), (13, 4), (8, 8), (3, 8), (12, 2)):
+        shards = [D.shard_indices(n, r, world) for r in range(world)]
+        per = -(-n // world)
+        assert all(len(s) == per for s in shards)
+        flat = sorted(i for s in shards for i in s)
+        assert set(flat) == set(range(n))          # every sample is read, the pad repeats the head
+        assert len(flat) == per * world
+    # n = 257, world = 2, bs = 128 -> 2 batches on both ranks (129 samples each)
+    assert all(-(-len(D.shard_indices(257, r, 2)) // 128) == 2 for r in range(2))
+
+
+def _sync_worker(rank, world, port, q, tmp):
+    import os
+    import sys
+    from tests.conftest import ROOT
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "vision-language-pretraining-for-bone-tumor-detection_amd")]
+    import torch.distributed as dist
+    from src.utils.trainer import EarlyStopping, ModelCheckpoint, Trainer
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # rank-local validation losses disagree: rank 0 keeps improving, rank 1 stalls
+    seq = [3.0, 2.0, 1.5, 1.0, 0.5] if rank == 0 else [3.0, 3.5, 3.6, 3.7, 3.8]
+    m = _ValToy(seq)
+    ck = ModelCheckpoint(monitor="val/combined/loss", mode="min", save_top_k=1, dirpath=tmp)
+    es = EarlyStopping(monitor="val/combined/loss", mode="min", patience=2)
+    t = Trainer(max_epochs=5, callbacks=[ck, es], default_root_dir=tmp)
+    data = [{"x": torch.ones(3)}]
+    t.fit(m, train_dataloaders=data, val_dataloaders=[data])
+    q.put((rank, t.current_epoch, ck.best_model_path, ck.best_model_score, os.path.exists(ck.best_model_path)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_trainer_decisions_agree_across_ranks_gloo_ws2(tmp_path):
+    """the monitored metric is the mean over ranks, so EarlyStopping and
+    ModelCheckpoint decide identically on every rank, and the best checkpoint
+    exists for every rank when it reads best_model_path."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_sync_worker, args=(r, 2, port, q, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: rest for r, *rest in (q.get(timeout=180) for _ in range(2))}
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    (e0, p0, s0, x0), (e1, p1, s1, x1) = res[0], res[1]
+    # means over ranks: 3.0, 2.75, 2.55, 2.35, 2.15 -> keeps improving, no early stop
+    assert e0 == e1 == 4
+    assert p0 == p1 and x0 and x1
+    assert abs(s0 - 2.15) < 1e-6 and s0 == s1   # fp32 logged values

@@ -32,9 +32,21 @@ __global__ void __launch_bounds__(256) mfma_peak_kernel(int iters, float* __rest
   out[blockIdx.x * 256 + l] = s;
 }
 
+// Empty kernels whose dispatches bracket a region in a rocprofv3 kernel trace
+// (bench.py's isolated roofline pass): tools/roofline_window.py averages the
+// roofline kernel's dispatches between them.
+__global__ void trace_marker_begin_kernel() {}
+__global__ void trace_marker_end_kernel() {}
+
 }  // namespace vlp
 
 using namespace vlp;
+
+VLP_EXPORT int vlp_trace_marker(int end, void* stream) {
+  if (end) hipLaunchKernelGGL(trace_marker_end_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream);
+  else hipLaunchKernelGGL(trace_marker_begin_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream);
+  return (int)hipGetLastError();
+}
 
 // FLOP = blocks * 4 waves * iters * kProbeAcc * 16*16*32*2 (iters: a multiple of 4); out: blocks*256 floats
 VLP_EXPORT int vlp_mfma_peak_probe(int blocks, int iters, float* out, void* stream) {

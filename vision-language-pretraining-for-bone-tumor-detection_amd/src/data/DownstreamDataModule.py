@@ -102,14 +102,27 @@ class DownstreamDataModule:
         self.collate = ClinicalCollator(upload if num_channels == 3 else "fp32", num_channels)
 
     @staticmethod
-    def _shard(ds):
+    def shard_indices(n, rank, world):
+        """DistributedSampler(drop_last=False)'s split: the index list is padded by
+        wrapping to ceil(n / world) * world, then rank r takes r, r + world, ...
+        Every rank gets the same number of samples (hence batches), so the
+        per-step gradient all-reduce never waits on a rank that has run out."""
+        per = -(-n // world)
+        idx = list(range(n))
+        total = per * world
+        while len(idx) < total:
+            idx += idx[:total - len(idx)]
+        return idx[rank:total:world]
+
+    @classmethod
+    def _shard(cls, ds):
         """Data parallel: each rank reads its own interleaved shard of the dataset
         (DistributedSampler's split, which Lightning's DDP inserts for the
         reference); the label weights stay those of the whole training set."""
         d = torch.distributed
         if not (d.is_available() and d.is_initialized()) or d.get_world_size() == 1:
             return ds
-        return Subset(ds, list(range(d.get_rank(), len(ds), d.get_world_size())))
+        return Subset(ds, cls.shard_indices(len(ds), d.get_rank(), d.get_world_size()))
 
     def _loader(self, ds, shuffle):
         return DataLoader(self._shard(ds), batch_size=self.batch_size, shuffle=shuffle,

@@ -543,7 +543,16 @@ class VisionLanguageModule(_Base):
 
     def on_validation_epoch_end(self):
         if self._val_loss_n:
-            self.log("val/combined/loss", self._val_loss_sum / self._val_loss_n, prog_bar=True)
+            # the reference's MeanMetric syncs across ranks: sum and count over every rank
+            tot = torch.stack([self._val_loss_sum.double().reshape(()),
+                               torch.tensor(float(self._val_loss_n), dtype=torch.float64,
+                                            device=self._val_loss_sum.device)])
+            d = torch.distributed
+            if d.is_available() and d.is_initialized() and d.get_world_size() > 1:
+                dev = self._val_loss_sum.device if d.get_backend() == "nccl" else torch.device("cpu")
+                tot = tot.to(dev)
+                d.all_reduce(tot)
+            self.log("val/combined/loss", (tot[0] / tot[1]).float(), prog_bar=True)
         ie, te, labels = self._get_cached_embeddings_and_labels(mode="val")
         for k, v in self.precision_at_k_on_image_embeddings(ie, labels, ks=self.k_for_precision_at_k).items():
             self.log(f"val/combined/label_precision_at_{k}", v, batch_size=ie.shape[0])

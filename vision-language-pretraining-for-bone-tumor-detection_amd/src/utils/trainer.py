@@ -55,6 +55,58 @@ def _rank0():
     return not (d.is_available() and d.is_initialized()) or d.get_rank() == 0
 
 
+def _dist_on():
+    d = torch.distributed
+    return d.is_available() and d.is_initialized() and d.get_world_size() > 1
+
+
+def _dist_device():
+    """Device of the collective's tensors: the rank's GPU for RCCL, the host for gloo."""
+    d = torch.distributed
+    if d.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def sync_val_metrics(metrics: dict) -> None:
+    """Mean over ranks of every `val*` scalar (in place), as Lightning's
+    sync_dist / torchmetrics sync does for the monitored metrics: every rank
+    then takes the same checkpoint and early-stopping decisions.  The union of
+    the ranks' keys is used; a key a rank lacks counts only where present."""
+    if not _dist_on():
+        return
+    d = torch.distributed
+    mine = sorted(k for k, v in metrics.items() if k.startswith("val") and isinstance(v, (int, float)))
+    keys = [None] * d.get_world_size()
+    d.all_gather_object(keys, mine)
+    allk = sorted(set().union(*keys))
+    if not allk:
+        return
+    t = torch.zeros(2, len(allk), dtype=torch.float64, device=_dist_device())
+    for i, k in enumerate(allk):
+        if k in metrics:
+            t[0, i] = float(metrics[k])
+            t[1, i] = 1.0
+    d.all_reduce(t)
+    for i, k in enumerate(allk):
+        if t[1, i] > 0:
+            metrics[k] = float(t[0, i] / t[1, i])
+
+
+def _any_rank(flag: bool) -> bool:
+    """MAX over ranks of a boolean (Lightning's reduce_boolean_decision)."""
+    if not _dist_on():
+        return flag
+    t = torch.tensor([1.0 if flag else 0.0], dtype=torch.float64, device=_dist_device())
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return bool(t.item() > 0)
+
+
+def _barrier():
+    if _dist_on():
+        torch.distributed.barrier()
+
+
 def serializable_hparams(hp) -> dict:
     """Module hyper-parameters as a weights_only-loadable dict: primitives kept,
     functools.partial (optimizer / scheduler factories) as a `_target_` /
@@ -131,6 +183,7 @@ class ModelCheckpoint:
         if _rank0():
             os.makedirs(d, exist_ok=True)
             trainer.save_checkpoint(path, pl_module)
+        _barrier()   # the file exists for every rank once it is named best_model_path
         if self.monitor is None:
             for _, old in self._kept:
                 if old != path and _rank0() and os.path.exists(old):
@@ -326,6 +379,7 @@ class Trainer:
                 if val_dataloaders and self.limit_val_batches != 0:
                     self.validate(model, val_dataloaders)
                 self._hook("on_validation_end", model)    # checkpointing, early stopping
+                self.should_stop = _any_rank(self.should_stop)
             if sched is not None:
                 s = sched["scheduler"] if isinstance(sched, dict) else sched
                 s.step()
@@ -353,4 +407,6 @@ class Trainer:
                 self.logged_metrics[k] = float(v.detach())
             elif k.startswith("val") and isinstance(v, (int, float)):
                 self.logged_metrics[k] = float(v)
+        # monitored metrics are identical on every rank before the callbacks read them
+        sync_val_metrics(self.logged_metrics)
         model.train()

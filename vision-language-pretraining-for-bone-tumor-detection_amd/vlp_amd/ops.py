@@ -103,8 +103,29 @@ def conv_wgrad(dy, x, KH, KW, S, P, dw_ws, in_scale=None, in_shift=None, dyT=Non
     return dw_ws
 
 
-_WGRAD_WS = {}
 WGRAD_WS_FLOATS = 32 << 20   # 128 MB of split-K slabs (the largest conv needs ~17M floats at bs=256)
+# Split-K slab workspaces, one per (device, stream).  A workspace is only ever
+# written and folded by launches on ONE stream, so the stream order is its
+# only synchronisation: the text tower's backward (its own stream), the image
+# tower's weight-gradient side stream and the main stream each get their own
+# buffer.  Allocated while that stream is current, so the caching allocator
+# also ties the block (and a replaced, smaller block) to that stream.
+_WS_CACHE = {}
+
+
+def _stream_ws(kind, device, elems):
+    import torch as _t
+    st = _t.cuda.current_stream(device) if device.type == "cuda" else None
+    key = (kind, str(device), st.cuda_stream if st is not None else 0)
+    buf = _WS_CACHE.get(key)
+    if buf is None or buf.numel() < elems:
+        buf = torch.empty(elems, dtype=torch.float32, device=device)
+        _WS_CACHE[key] = buf
+    return buf
+
+
+def wgrad_ws(device):
+    return _stream_ws("wgrad", device, WGRAD_WS_FLOATS)
 
 
 def conv_wgrad_into(dy, x, KH, KW, S, P, grad):
@@ -114,10 +135,7 @@ def conv_wgrad_into(dy, x, KH, KW, S, P, grad):
     import ctypes
     N, H, W, C = x.shape
     Co, Ho, Wo = dy.shape[-1], dy.shape[1], dy.shape[2]
-    ws = _WGRAD_WS.get(dy.device)
-    if ws is None:
-        ws = torch.empty(WGRAD_WS_FLOATS, dtype=torch.float32, device=dy.device)
-        _WGRAD_WS[dy.device] = ws
+    ws = wgrad_ws(dy.device)
     ns = ctypes.c_int(0)
     tk = ktimer.begin(f"conv_wgrad[raw]{_tile_wgrad(Co)}", 2.0 * N * Ho * Wo * Co * C * KH * KW)
     lib().vlp_conv_wgrad_ws(dcode(dy), ptr(dy), ptr(x), ptr(ws), ws.numel(), ctypes.addressof(ns), N, H, W, C,
@@ -131,10 +149,7 @@ def stem_wgrad_into(dy, xp, N, H, W, grad):
     """grad[64][3][7][7] = stem weight gradient (overwrites), via per-split
     fp32 slabs of the shared weight-gradient workspace and one fold pass."""
     import ctypes
-    ws = _WGRAD_WS.get(dy.device)
-    if ws is None:
-        ws = torch.empty(WGRAD_WS_FLOATS, dtype=torch.float32, device=dy.device)
-        _WGRAD_WS[dy.device] = ws
+    ws = wgrad_ws(dy.device)
     ns = ctypes.c_int(0)
     tk = ktimer.begin("stem_wgrad", 2.0 * dy.numel() * 147)
     lib().vlp_stem_wgrad_ws(dcode(dy), ptr(dy), ptr(xp), ptr(ws), ws.numel(), ctypes.addressof(ns), N, H, W, _s())
@@ -179,10 +194,7 @@ def stem1_fwd(xs, wp1, N, H, W, y, stat_sum, stat_sumsq, stat_rep=1):
 def stem1_wgrad_into(dy, xs, N, H, W, grad):
     """grad[64][3][7][7] = stem weight gradient of the single-channel path (overwrites)."""
     import ctypes
-    ws = _WGRAD_WS.get(dy.device)
-    if ws is None:
-        ws = torch.empty(WGRAD_WS_FLOATS, dtype=torch.float32, device=dy.device)
-        _WGRAD_WS[dy.device] = ws
+    ws = wgrad_ws(dy.device)
     ns = ctypes.c_int(0)
     tk = ktimer.begin("stem_wgrad", 2.0 * dy.numel() * 147)
     lib().vlp_stem1_wgrad_ws(dcode(dy), ptr(dy), ptr(xs), ptr(ws), ws.numel(), ctypes.addressof(ns), N, H, W, _s())
@@ -322,15 +334,11 @@ def linear_dgrad(dy, w, dx, M, Kin, Nout, lddy=None, lddx=None, mode=0, aux=None
     ktimer.end(tk)
 
 
-_LINW_WS = {}
-
-
 def _linw_ws(device, elems):
-    buf = _LINW_WS.get(device)
-    if buf is None or buf.numel() < elems:
-        buf = torch.empty(elems, dtype=torch.float32, device=device)
-        _LINW_WS[device] = buf
-    return buf
+    """Split-K slabs of the linear weight gradients: per (device, stream), so the
+    text tower's backward on its own stream and NesT's on the main stream never
+    share (or free under each other) a workspace."""
+    return _stream_ws("linw", device, elems)
 
 
 def linear_wgrad(dy, x, dw, M, Nout, Kin, lddy=None, ldx=None):

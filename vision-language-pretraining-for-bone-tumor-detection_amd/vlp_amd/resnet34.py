@@ -39,12 +39,14 @@ WIDTHS = (64, 128, 256, 512)
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
 _USE_DYT = os.environ.get("VLP_WGRAD_DYT", "0") != "0"
-# weight gradients on a side stream (VLP_WGRAD_STREAM=1): they are off the
-# data-gradient chain, so the MFMA-bound wgrad GEMMs overlap the HBM-bound BN /
-# elementwise passes.  Measured +0.8 % per step, but every wgrad launch then
-# shares the CUs and its own duration stretches by ~50 %, so it is off by
-# default (the per-kernel roofline is read from those durations)
-_USE_WG_STREAM = os.environ.get("VLP_WGRAD_STREAM", "0") != "0"
+# weight gradients on a side stream: they are off the data-gradient chain, so
+# the MFMA-bound wgrad GEMMs overlap the HBM-bound BN / elementwise passes and
+# the data-gradient epilogue bursts (r2 driver: +2.4 % pairs/s).  Each side-
+# stream launch shares the CUs, so bench.py times the roofline kernel in a
+# separate serial pass (this attribute set False).  Each stream has its own
+# split-K workspace (ops.wgrad_ws), so the main-stream stem weight gradient
+# never shares slabs with the side stream's.
+_USE_WG_STREAM = True
 _WG_STREAMS = {}   # measured: the extra transposed write costs more than it saves
 STAT_REP = 64   # replicas of per-channel fp64 sums (see vlp_stat_reduce)
 # single-channel stem for the uint8 upload (VLP_STEM1=0: always the 3-channel NHWC4 path)
