@@ -121,3 +121,43 @@ def test_augment_draw_protocol(aug):
     assert p["translate"].abs().max() <= 20 and p["shear"].abs().max() <= 5
     assert p["angle"].abs().max() <= math.pi / 6 and p["zoom"].min() >= 1.1 and p["zoom"].max() <= 1.3
     assert p["noise_std"].max() <= 0.01
+
+
+def _pad_mask(ref_shape, hw):
+    """True on the padded columns (h > w after the crop) or rows (w > h)."""
+    side = ref_shape[-1]
+    m = torch.zeros(ref_shape, dtype=torch.bool)
+    h, w = hw
+    if h == w:
+        return m
+    # the crop leaves the larger side equal to `side`; the shorter one is padded
+    short = w if h > w else h
+    lo = (side - short) // 2
+    idx = list(range(lo)) + list(range(lo + short, side))
+    if h > w:
+        m[:, idx] = True
+    else:
+        m[idx, :] = True
+    return m
+
+
+def test_crop_pad_vs_reference_transforms(aug):
+    """vlp_prep_images' crop + pad stage against the reference's own
+    CropLargerDimension / PadToSquaredEdgeAverage (tests/golden/make_prep_golden.py
+    ran them on the equalised images): S = the padded side, so the area resize is
+    the identity and mean / std are 0 / 1.  The image pixels must be bit-exact (the
+    equalisation is numpy-exact and the crop moves no values); the padded columns
+    or rows are edge means, summed in another order than torch's: <= 1e-4 of the
+    0..255 range."""
+    import os
+    gd = torch.load(os.path.join(os.path.dirname(__file__), "golden", "prep_crop_pad.pt"), weights_only=True)
+    assert len(gd["cases"]) == 8
+    for c in gd["cases"]:
+        u8, ref = c["u8"].numpy(), c["eq"]
+        S = ref.shape[-1]
+        out = aug.preprocess([u8], S, 0.0, 1.0, channels=1).cpu()[0, 0]
+        assert out.shape == ref.shape
+        pm = _pad_mask(ref.shape, u8.shape)
+        assert torch.equal(out[~pm], ref[~pm]), (u8.shape, (out - ref).abs()[~pm].max().item())
+        if pm.any():
+            assert (out - ref).abs()[pm].max().item() <= 255 * 1e-4, u8.shape

@@ -125,3 +125,18 @@ def test_full_step_against_reference():
     sd = model.state_dict()
     torch.testing.assert_close(sd["image_encoder.model.bn1.running_mean"], gd["bn1_running_mean"])
     torch.testing.assert_close(sd["image_encoder.model.bn1.running_var"], gd["bn1_running_var"])
+
+
+def test_prep_crop_pad_vs_reference_transforms():
+    """oracle/prep.py's restatement of CropLargerDimension / PadToSquaredEdgeAverage
+    against the reference's own transforms (tests/golden/make_prep_golden.py):
+    exact, on the raw images and after the equalisation."""
+    import numpy as np
+    import oracle.prep as op
+    gd = torch.load(os.path.join(GOLD, "prep_crop_pad.pt"), weights_only=True)
+    for c in gd["cases"]:
+        u8 = c["u8"].numpy()
+        raw = torch.from_numpy(u8.astype(np.float32))[None]
+        eq = torch.from_numpy(op.histogram_normalize(u8.astype(np.float32)))[None]
+        assert torch.equal(op.pad_to_square_edge_average(op.crop_larger_dimension(raw))[0], c["raw"]), u8.shape
+        assert torch.equal(op.pad_to_square_edge_average(op.crop_larger_dimension(eq))[0], c["eq"]), u8.shape
