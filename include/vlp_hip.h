@@ -130,6 +130,24 @@ int vlp_stem1_fwd(int dtype, const void* xs, const void* wp, void* y, int N, int
 int vlp_stem1_wgrad_ws(int dtype, const void* dy, const void* xs, float* split_ws, long long ws_floats,
                        int* nsplit, int N, int H, int W, void* stream);
 int vlp_stem1_wgrad_fold(int nsplit, const float* split_ws, float* grad, void* stream);
+/* Fused stem (bf16, single-channel upload): replaces timm's conv1 -> bn1 ->
+ * act1 -> maxpool (VisionLanguageModule.py:30-32) without ever writing the
+ * full-resolution conv output.  vlp_stem1_pool_fwd computes the conv per
+ * output row on MFMA, the BatchNorm sums (stat_* may be NULL: eval mode) and
+ * the 3x3/2 pad-1 max-pool of sign(gamma)*y0, i.e. the window's max (gamma >= 0)
+ * or min (gamma < 0) of y0, which is where relu(bn(y0)) peaks; it stores the
+ * raw y0 there (yarg [N][Ho/2][Wo/2][64]) and the tap kh*3+kw (idx).  Then
+ * p = relu(sc*yarg + sh) is vlp_bn_add_relu over the pooled tensor.
+ * vlp_stem1_route_bwd writes dy = dBN(route(dp)) for the stem weight gradient,
+ * recomputing y0 instead of reading it; dp must be ReLU-masked (p > 0, as the
+ * layer-1 data-gradient epilogue produces it).  vlp_stem1_fused_ok(H, W) = 1 when the
+ * shape qualifies (Wo a multiple of 64 up to 256, Ho even). */
+int vlp_stem1_fused_ok(int H, int W);
+int vlp_stem1_pool_fwd(const void* xs, const void* wp1, const float* gamma, void* yarg, uint8_t* idx, int N,
+                       int H, int W, double* stat_sum, double* stat_sumsq, int stat_rep, void* stream);
+int vlp_stem1_route_bwd(const void* xs, const void* wp1, const void* dp, const uint8_t* idx, const float* sc,
+                        const float* sh, const float* mean, const float* istd, const float* gamma,
+                        const double* sum_g, const double* sum_gx, void* dy, int N, int H, int W, void* stream);
 
 /* ---------------- image tower: BatchNorm / residual / pooling ----------------
  * Replace timm resnet34's BatchNorm2d (train-mode batch statistics), ReLU,
@@ -313,15 +331,20 @@ int vlp_l2norm_bwd(int dtype, int R, int E, const float* y, const float* norm, c
 int vlp_scale(int n, const float* x, const float* s, float* y, int accumulate, void* stream);
 /* out[3] = {(parts0 + parts1) / (2N), parts0 / N, parts1 / N} */
 int vlp_clip_loss_finish(const float* parts, int N, float* out, void* stream);
-/* Fused global-batch symmetric InfoNCE, forward + backward.  img_all/txt_all:
- * [N][E] gathered normalised embeddings; this rank owns rows [offset, offset+B).
- * g_img_all/g_txt_all (+=, zero first): d loss / d embeddings for all N rows;
- * d_logit_scale (+=); loss_parts[0] (+=) sum of image->text CE terms of the
- * local rows, loss_parts[1] text->image; lse_out (optional) [2][B]. */
+/* Fused global-batch symmetric InfoNCE, forward + backward (replaces the
+ * logits matmul and the two F.cross_entropy calls of VisionLanguageModule.py
+ * :456-459 / :550-552 with their autograd backward).  img_all/txt_all: [N][E]
+ * gathered normalised embeddings (E <= 128); this rank owns rows
+ * [offset, offset+B).  Written (not accumulated): g_img_all/g_txt_all, d loss /
+ * d embeddings for all N rows; d_logit_scale; loss_parts[0] the sum of the
+ * image->text CE terms of the local rows, loss_parts[1] text->image; lse_out
+ * (optional) [2][B].  ws: vlp_clip_loss_ws_floats(B, N, E) floats of scratch
+ * (split-key partials and gradient slabs; no atomics, bitwise reproducible). */
+int vlp_clip_loss_ws_floats(int B, int N, int E, long long* n);
 int vlp_clip_loss_fused(int B, int N, int E, int offset, const float* img_all,
                         const float* txt_all, const float* logit_scale, float* g_img_all,
                         float* g_txt_all, float* d_logit_scale, float* loss_parts,
-                        float* lse_out, void* stream);
+                        float* lse_out, float* ws, long long ws_floats, void* stream);
 /* symmetric CE over explicit logits [B][B]: out = {loss, image_loss, text_loss} (+=);
  * dlogits (+=, optional) */
 int vlp_ce_sym(int B, const float* logits, float* out, float* dlogits, void* stream);

@@ -1,7 +1,9 @@
 """Summarise rocprofv3 --pmc counter_collection CSVs: per kernel (short name),
 mean value of each counter over its dispatches.
-  python tools/pmc_summary.py file1.csv [file2.csv ...]"""
+  python tools/pmc_summary.py file1.csv [file2.csv ...]
+(PMC_FILTER: regex of the kernel names to print; default gemm / conv kernels)"""
 import csv
+import os
 import re
 import sys
 from collections import defaultdict
@@ -18,8 +20,9 @@ vals = defaultdict(lambda: defaultdict(list))
 for path in sys.argv[1:]:
     for r in csv.DictReader(open(path)):
         vals[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+flt = re.compile(os.environ.get("PMC_FILTER", "gemm|conv|Conv"))
 for k, d in vals.items():
-    if "gemm" not in k and "conv" not in k.lower():
+    if not flt.search(k):
         continue
     print(k)
     for c, v in sorted(d.items()):

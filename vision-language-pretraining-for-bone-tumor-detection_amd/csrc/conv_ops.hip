@@ -18,6 +18,7 @@
 // can apply the ReLU mask of the producer layer and accumulate that BN's
 // backward statistics, or add a residual-branch gradient.
 #include "gemm.h"
+#include "stem_geom.h"
 
 namespace vlp {
 
@@ -724,11 +725,6 @@ static PixStep make_stem_pixstep(const StemGeom& g, int BK) {
 // 6 pixels: output column wo reads copy s = wo & 3 at column 2wo - 2s (a multiple
 // of 8).  Xs[s][n][Hp][Wp1], Wp1 = round8(2Wo + 8), zero outside the image.
 // Requires Wo % 4 == 0 (then s is constant along the pixel walk of a K-step).
-struct Stem1Geom {
-  int N, Ho, Wo, Hp, Wp1, M;
-  size_t copy;   // elements per shifted copy
-  FastDiv fd_howo, fd_wo;
-};
 template <typename T>
 struct Stem1A {
   static constexpr bool kKContig = true;
@@ -1622,19 +1618,6 @@ __global__ void stem_prep_u8_kernel(const uint8_t* __restrict__ x, T* __restrict
   }
 }
 
-static Stem1Geom make_stem1(int N, int H, int W) {
-  Stem1Geom g;
-  g.N = N;
-  g.Ho = (H + 6 - 7) / 2 + 1;
-  g.Wo = (W + 6 - 7) / 2 + 1;
-  g.Hp = 2 * g.Ho + 6;
-  g.Wp1 = (2 * g.Wo + 8 + 7) / 8 * 8;
-  g.M = N * g.Ho * g.Wo;
-  g.copy = (size_t)N * g.Hp * g.Wp1;
-  g.fd_howo = make_fastdiv(g.Ho * g.Wo);
-  g.fd_wo = make_fastdiv(g.Wo);
-  return g;
-}
 // uint8 [N][1][H][W] -> normalised single-channel padded image in 4 shifted copies
 // (Xs[s][n][h][j] = Xpad[n][h][j + 2s], Xpad = the image at (3, 3), zeros around);
 // one thread per 8 output elements, every element written (no pre-zeroing)

@@ -203,6 +203,23 @@ def stem1_wgrad_into(dy, xs, N, H, W, grad):
     return grad
 
 
+def stem1_fused_ok(H, W):
+    return bool(lib()._dll.vlp_stem1_fused_ok(int(H), int(W)))
+
+
+def stem1_pool_fwd(xs, wp1, gamma, yarg, idx, N, H, W, stat_sum=None, stat_sumsq=None, stat_rep=1):
+    """Fused stem conv + BN sums + 3x3/2 max-pool of sign(gamma)*y0 (bf16); y0 is never stored."""
+    tk = ktimer.begin("stem_fwd", 2.0 * N * (H // 2) * (W // 2) * 64 * 147)
+    lib().vlp_stem1_pool_fwd(ptr(xs), ptr(wp1), ptr(gamma), ptr(yarg), ptr(idx), N, H, W, ptr(stat_sum),
+                             ptr(stat_sumsq), int(stat_rep), _s())
+    ktimer.end(tk)
+
+
+def stem1_route_bwd(xs, wp1, dp, idx, sc, sh, mean, istd, gamma, sum_g, sum_gx, dy, N, H, W):
+    lib().vlp_stem1_route_bwd(ptr(xs), ptr(wp1), ptr(dp), ptr(idx), ptr(sc), ptr(sh), ptr(mean), ptr(istd),
+                              ptr(gamma), ptr(sum_g), ptr(sum_gx), ptr(dy), N, H, W, _s())
+
+
 def stem_prep(x_nchw, xp):
     N, _, H, W = x_nchw.shape
     lib().vlp_stem_prep(dcode(xp), ptr(x_nchw), ptr(xp), N, H, W, _s())
@@ -418,9 +435,15 @@ def clip_loss_finish(parts, N, out):
 
 def clip_loss_fused(B, N, E, offset, img_all, txt_all, logit_scale, g_img_all, g_txt_all, d_ls,
                     loss_parts, lse_out=None):
+    """Global-batch symmetric InfoNCE + gradients (three launches, split over key
+    chunks; the scratch is a per-(device, stream) cached workspace)."""
+    import ctypes
+    n = ctypes.c_longlong(0)
+    lib().vlp_clip_loss_ws_floats(B, N, E, ctypes.addressof(n))
+    ws = _stream_ws("clip", img_all.device, n.value)
     lib().vlp_clip_loss_fused(B, N, E, offset, ptr(img_all), ptr(txt_all), ptr(logit_scale),
                               ptr(g_img_all), ptr(g_txt_all), ptr(d_ls), ptr(loss_parts),
-                              ptr(lse_out), _s())
+                              ptr(lse_out), ptr(ws), ws.numel(), _s())
 
 
 def ce_sym(logits, out, dlogits=None):

@@ -51,6 +51,9 @@ _WG_STREAMS = {}   # measured: the extra transposed write costs more than it sav
 STAT_REP = 64   # replicas of per-channel fp64 sums (see vlp_stat_reduce)
 # single-channel stem for the uint8 upload (VLP_STEM1=0: always the 3-channel NHWC4 path)
 _USE_STEM1 = os.environ.get("VLP_STEM1", "1") != "0"
+# bf16: stem conv + BN sums + max-pool fused (stem_ops.hip); False keeps the
+# conv -> y0 -> max-pool kernels (tests compare the two)
+_USE_STEM_FUSED = True
 
 
 STAGES = ("stem", "layer1", "layer2", "layer3", "layer4")
@@ -289,6 +292,34 @@ class ResNet34Tower(ArenaModule):
         # replicates it 3x, PretrainDataModule.py:167-171): the stem then runs as a
         # K = 64 single-channel conv with channel-summed weights (vlp_stem1_*)
         g1 = ops.stem1_geom(H, W) if (x is None and _USE_STEM1) else None
+        fused = g1 is not None and T == torch.bfloat16 and _USE_STEM_FUSED and ops.stem1_fused_ok(H, W)
+        if fused:
+            # conv + BN sums + max-pool in one pass (vlp_stem1_pool_fwd): the
+            # full-resolution conv output is never written; the pooled window
+            # extreme (sign of gamma) of y0 and its tap are
+            Ho, Wo, Hp, Wp1 = g1
+            key = ("xs", N, H, W)
+            xs = ws.get(key)
+            if xs is None:
+                xs = torch.empty(4, N, Hp, Wp1, dtype=T, device=dev)
+                ws[key] = xs
+            ops.stem1_prep_u8(x_u8.contiguous(), xs, u8_norm[0], u8_norm[1])
+            if "conv1.wp1" not in ws:
+                ws["conv1.wp1"] = torch.empty(64, 64, dtype=T, device=dev)
+            ops.pack_stem1(self.arena.view("conv1.weight"), ws["conv1.wp1"])
+            Hq, Wq = (Ho + 2 - 3) // 2 + 1, (Wo + 2 - 3) // 2 + 1
+            yarg = torch.empty(N, Hq, Wq, 64, dtype=T, device=dev)
+            idx = torch.empty(N, Hq, Wq, 64, dtype=torch.uint8, device=dev)
+            s, ss = self._fstat(ws, "bn1", full=True) if training else (None, None)
+            ops.stem1_pool_fwd(xs, ws["conv1.wp1"], self.arena.view("bn1.weight"), yarg, idx, N, H, W, s, ss,
+                               STAT_REP)
+            sc0, sh0 = self._bn_finalize(ws, "bn1", N * Ho * Wo, training)
+            p = torch.empty(N, Hq, Wq, 64, dtype=T, device=dev)
+            pm = torch.empty(p.numel() // 8, dtype=torch.uint8, device=dev) if training else None
+            ops.bn_add_relu(yarg, sc0, sh0, None, None, None, p, relu_mask=pm)
+            saved = {"N": N, "H": H, "W": W, "xs": xs, "training": training, "stem_fused": True,
+                     "y0": None, "idx": idx, "yarg": yarg if training else None}
+            return self._run_blocks(ws, T, dev, N, p, pm, saved, training)
         if g1 is not None:
             Ho, Wo, Hp, Wp1 = g1
             key = ("xs", N, H, W)
@@ -328,6 +359,10 @@ class ResNet34Tower(ArenaModule):
         pm = torch.empty(p.numel() // 8, dtype=torch.uint8, device=dev) if bits else None
         ops.maxpool_fwd(y0, sc0, sh0, p, idx, yarg, relu_mask=pm)
         saved["y0"], saved["idx"], saved["yarg"] = y0, idx, yarg
+        return self._run_blocks(ws, T, dev, N, p, pm, saved, training)
+
+    def _run_blocks(self, ws, T, dev, N, p, pm, saved, training):
+        bits = training and T == torch.bfloat16
         xmask = pm
         xcur = p
         blocks = []
@@ -511,6 +546,19 @@ class ResNet34Tower(ArenaModule):
         y0, idx = saved["y0"], saved["idx"]
         sc0, sh0, mu0, is0 = self._coef(ws, "bn1")
         sg0f, sgx0f = self._bstat(ws, "bn1", full=True)
+        if saved.get("stem_fused"):
+            # the pooled gradient routed to each window's tap and through the BN
+            # backward, y0 recomputed on the fly (vlp_stem1_route_bwd)
+            ops.bn_grad_rep(STAT_REP, 64, sg0f, sgx0f, self.arena.gview("bn1.weight"),
+                            self.arena.gview("bn1.bias"))
+            N, H, W = saved["N"], saved["H"], saved["W"]
+            Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
+            dy0 = torch.empty(N, Ho, Wo, 64, dtype=T, device=dev)
+            ops.stem1_route_bwd(saved["xs"], ws["conv1.wp1"], dout, idx, sc0, sh0, mu0, is0,
+                                self.arena.view("bn1.weight"), sg0f[:64], sgx0f[:64], dy0, N, H, W)
+            ops.stem1_wgrad_into(dy0, saved["xs"], N, H, W, self.arena.gview("conv1.weight"))
+            self._stage_done(["layer1", "stem"], on_stage_done, dev)
+            return
         if saved.get("yarg") is None:
             ops.maxpool_bwd(dout, idx, y0, sc0, sh0, mu0, is0, sg0f, sgx0f, stat_rep=STAT_REP)
         ops.bn_grad_rep(STAT_REP, 64, sg0f, sgx0f, self.arena.gview("bn1.weight"), self.arena.gview("bn1.bias"))
