@@ -223,8 +223,19 @@ def loss_delta_vs_fp32(args, model, host):
         lg, oie, ote = o({"x-ray": x, "caption_tokenized": host["caption_tokenized"]})
         lo = compute_loss(lg)[0].item()
     rel = lambda a, b: ((a.double() - b.double()).norm() / b.double().norm()).item()   # noqa: E731
+    # eval-mode image features (the linear-probe embedding) of the first 8 images: for
+    # NesT the logits can sit at the uniform ln(B) fixed point, where the loss says nothing
+    xp = host["x-ray-u8"][:8] if "x-ray-u8" in host else host["x-ray"][:8]
+    model.eval()
+    o.eval()
+    with torch.no_grad():
+        f = model.image_encoder(xp.to(next(model.parameters()).device)).float().cpu()
+        fo = o.image_encoder(x[:8])
+    model.train()
     return {"loss": round(loss, 6), "loss_fp32_oracle": round(lo, 6), "abs_delta": abs(loss - lo),
             "img_emb_rel_l2": rel(ie, oie), "txt_emb_rel_l2": rel(te, ote),
+            "probe_features_rel_l2": rel(f, fo),
+            "logit_spread": round(float(lg.std()), 6),
             "note": (f"bench weights and batch, train-mode forward, text dropout off; oracle fp32 on "
                      f"{torch.get_num_threads()} CPU threads ({time.perf_counter() - t0:.1f} s)")}
 

@@ -148,6 +148,14 @@ int vlp_stem1_pool_fwd(const void* xs, const void* wp1, const float* gamma, void
 int vlp_stem1_route_bwd(const void* xs, const void* wp1, const void* dp, const uint8_t* idx, const float* sc,
                         const float* sh, const float* mean, const float* istd, const float* gamma,
                         const double* sum_g, const double* sum_gx, void* dy, int N, int H, int W, void* stream);
+/* The whole stem backward in one pass (route + BN backward + weight gradient
+ * on MFMA, y0 recomputed, dy kept in LDS): one fp32 [64][64] slab per
+ * workgroup (vlp_stem1_bwd_fused_slabs), summed and replicated over the 3 input
+ * channels by vlp_stem1_wgrad_fold.  dp ReLU-masked as above. */
+int vlp_stem1_bwd_fused_slabs(int N, int H, int W, int* nslabs);
+int vlp_stem1_bwd_fused(const void* xs, const void* wp1, const void* dp, const uint8_t* idx, const float* mean,
+                        const float* istd, const float* gamma, const double* sum_g, const double* sum_gx,
+                        float* slabs, long long slab_floats, int N, int H, int W, void* stream);
 
 /* ---------------- image tower: BatchNorm / residual / pooling ----------------
  * Replace timm resnet34's BatchNorm2d (train-mode batch statistics), ReLU,

@@ -23,7 +23,9 @@ Gates (measured values are printed):
     features (eval, first 32 images) and embeddings rel-L2 <= 2e-2; gradient
     groups vs fp32 (whole image-tower conv vector, BN params, projections,
     text tower) <= 0.30 (measured 0.06-0.23)
-  bs=16, 256 px: every group's error <= 1.5 x torch-autocast-bf16's + 0.01
+    and per tensor <= 0.4 (BN parameters, sums of cancelling terms: 0.8), median <= 0.1
+  bs=16, 256 px: every group's error <= 1.5 x torch-autocast-bf16's + 0.01, every
+    tensor's <= 1.5 x torch autocast's own error on that tensor + 0.02
 """
 import functools
 import statistics
@@ -130,12 +132,28 @@ def test_bf16_loss_features_embeddings_bs256(runs256):
     assert rf <= 2e-2 and ri <= 2e-2 and rt <= 2e-2
 
 
+def tensor_errors(ga, gb):
+    """rel-L2 per parameter tensor (same exclusions as group_errors)."""
+    return {k: rel(ga[k], gb[k]) for k in gb if k in ga and gb[k].norm() > 0 and "key.bias" not in k}
+
+
 def test_bf16_gradients_bs256(runs256):
     hip, ora = runs256
     errs = group_errors(hip["grads"], ora["grads"])
     print("bs=256 bf16 vs fp32 oracle gradient groups:", {k: round(v, 4) for k, v in errs.items()})
     for k, v in errs.items():
         assert v <= 0.30, (k, v)
+    # per tensor: a single wrong layer (e.g. a downsample weight gradient) is not
+    # diluted by its group.  Conv / projection / text weights carry many terms and
+    # stay close to their group's error; BN parameters are sums of cancelling
+    # terms (relative bf16 error up to ~0.5 on a handful of them)
+    te = tensor_errors(hip["grads"], ora["grads"])
+    worst = sorted(te.items(), key=lambda kv: -kv[1])[:8]
+    print("bs=256 worst tensors:", [(k, round(v, 3)) for k, v in worst])
+    for k, v in te.items():
+        is_bn = ora["grads"][k].dim() == 1 and k.startswith("image_encoder")
+        assert v <= (0.8 if is_bn else 0.4), (k, v)
+    assert statistics.median(te.values()) <= 0.1
 
 
 def test_bf16_gradients_vs_torch_autocast():
@@ -154,3 +172,17 @@ def test_bf16_gradients_vs_torch_autocast():
         assert e_hip[k] <= 1.5 * e_ac[k] + 0.01, (k, e_hip[k], e_ac[k])
     assert abs(hip["loss"] - ref["loss"]) <= 5e-2
     assert statistics.mean(e_hip.values()) <= statistics.mean(e_ac.values()) * 1.5 + 0.01
+    # embeddings: the text tower keeps its residual stream in bf16 like autocast's
+    # matmul outputs; its deviation must stay within autocast's own
+    r_img = (rel(hip["ie"], ref["ie"]), rel(ac["ie"], ref["ie"]))
+    r_txt = (rel(hip["te"], ref["te"]), rel(ac["te"], ref["te"]))
+    print(f"bs=16 embeddings rel-L2 (hip, autocast): image {r_img[0]:.2e} {r_img[1]:.2e}; "
+          f"text {r_txt[0]:.2e} {r_txt[1]:.2e}")
+    assert r_img[0] <= 1.5 * r_img[1] + 5e-3, r_img
+    assert r_txt[0] <= 1.5 * r_txt[1] + 5e-3, r_txt
+    # per tensor against torch's own per-tensor autocast error
+    t_hip, t_ac = tensor_errors(hip["grads"], ref["grads"]), tensor_errors(ac["grads"], ref["grads"])
+    excess = sorted(((t_hip[k] - (1.5 * t_ac[k] + 0.02), k, t_hip[k], t_ac[k]) for k in t_hip), reverse=True)
+    print("bs=16 per-tensor worst (excess, name, hip, autocast):", [(round(a, 3), k, round(b, 3), round(c, 3))
+                                                                   for a, k, b, c in excess[:5]])
+    assert excess[0][0] <= 0, excess[:3]

@@ -146,3 +146,47 @@ def test_clip_step_nest_tinybert_vs_oracle():
                 if p.grad is not None and og[k].grad is not None and og[k].grad.norm() > 0
                 and not k.endswith("attention.self.key.bias"))
     assert worst[0] < 2e-3, worst
+
+
+def test_clip_step_nest_tinybert_bf16_256px():
+    """BASELINE configs[3]'s workload in its compute dtype: the bf16 NesT-Small +
+    TinyBERT contrastive step (text tower on its own stream, as the bench runs
+    it) at 256^2 (level-0 blocks of 1024 tokens: the 512^2 block size) against
+    the fp32 oracle on the same weights and batch.  DropPath off, text dropout
+    off.  Gates as the bf16 tower test: loss |delta| <= 5e-2, embeddings rel-L2
+    <= 5e-2, every gradient <= 0.3 and the median <= 2e-2."""
+    import statistics
+    from oracle.clip import OracleVLP, compute_loss
+    from src.models.pretrain.VisionLanguageModule import VisionLanguageModule
+    torch.manual_seed(3)
+    m = VisionLanguageModule("nest_small", "tinybert", functools.partial(torch.optim.AdamW, lr=5e-5), False,
+                             False, 384, 312, 128, compute_dtype="bf16", text_dropout=0.0, image_size=256,
+                             drop_path_rate=0.0)
+    m.train()
+    o = OracleVLP(128, text_dropout=0.0, image_model="nest_small", img_size=256)
+    o.load_state_dict({k: v.detach().float().cpu() for k, v in m.state_dict().items()}, strict=False)
+    o.train()
+    for lvl in o.image_encoder.model.levels:
+        for layer in lvl.transformer_encoder:
+            layer.drop_path = 0.0
+    b = synth_batch(4, 256, 40, 21, with_u8=True)
+    bu = {"x-ray-u8": b["x-ray-u8"].cuda(), "label": b["label"], "caption": b["caption"],
+          "caption_tokenized": {k: v.cuda() for k, v in b["caption_tokenized"].items()}}
+    loss, li, lt, ie, te = m.training_step_outputs(bu)
+    loss.backward()
+    torch.cuda.synchronize()
+    logits, oie, ote = o({"x-ray": b["x-ray"], "caption_tokenized": b["caption_tokenized"]})
+    lo, _, _ = compute_loss(logits)
+    lo.backward()
+    d = abs(loss.item() - lo.item())
+    ri, rt = rel(ie.float(), oie.detach()), rel(te.float(), ote.detach())
+    og = dict(o.named_parameters())
+    errs = {k: rel(p.grad, og[k].grad) for k, p in m.named_parameters()
+            if p.grad is not None and og[k].grad is not None and og[k].grad.norm() > 0
+            and not k.endswith("attention.self.key.bias")}
+    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:5]
+    print(f"NesT bf16 256px: loss {loss.item():.5f} vs {lo.item():.5f}; emb rel {ri:.2e} / {rt:.2e}; "
+          f"grad median {statistics.median(errs.values()):.3e}; worst {worst}")
+    assert d <= 5e-2 and ri <= 5e-2 and rt <= 5e-2
+    assert worst[0][1] <= 0.3, worst
+    assert statistics.median(errs.values()) <= 2e-2

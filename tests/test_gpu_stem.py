@@ -217,3 +217,55 @@ def test_tower_fused_stem_matches_unfused_bf16():
     worst.sort()
     print("fused vs unfused stem, worst (excess, name, err_fused, err_unfused):", worst[-3:])
     assert worst[-1][0] <= 0, worst[-3:]
+
+
+@pytest.mark.parametrize("N,H,W", SHAPES)
+def test_stem_bwd_fused_weight_gradient(N, H, W):
+    """vlp_stem1_bwd_fused (route + BN backward + weight gradient in one pass, dy in
+    LDS only) against (a) the two-pass path (vlp_stem1_route_bwd writing dy, then
+    the stem weight-gradient GEMM): same bf16 dy, only the fp32 summation order
+    differs -> rel 1e-4; (b) the fp64 weight gradient of the fp64 BN backward of
+    the routed gradient: rel-L2 <= 1e-2 (dy rounded to bf16 in both kernels)."""
+    from vlp_amd import ops
+    xu, w, gamma = _inputs(N, H, W, 5 * H + W)
+    xs, wp1, yarg, idx, s, ss = _run_fwd(xu, w, gamma)
+    Ho, Wo = H // 2, W // 2
+    M = N * Ho * Wo
+    g = torch.Generator().manual_seed(13)
+    mean = (s / M).float()
+    var = (ss / M - (s / M) ** 2).clamp_min(0).float()
+    istd = 1.0 / torch.sqrt(var + 1e-5)
+    beta = torch.randn(64, generator=g)
+    sc, sh = gamma * istd, beta - mean * gamma * istd
+    dp = torch.randn(N, Ho // 2, Wo // 2, 64, generator=g)
+    p = torch.relu(yarg * sc.view(1, 1, 1, 64) + sh.view(1, 1, 1, 64))
+    dp = torch.where(p > 0, dp, torch.zeros_like(dp)).to(torch.bfloat16)
+    sum_g = torch.randn(64, generator=g).double() * 10
+    sum_gx = torch.randn(64, generator=g).double() * 10
+    dev = "cuda"
+    args = [t.to(dev) for t in (mean, istd, gamma, sum_g, sum_gx)]
+    gf = torch.full((64, 3, 7, 7), float("nan"), device=dev)
+    ops.stem1_bwd_fused_into(xs, wp1, dp.to(dev), idx.to(dev), *args, N, H, W, gf)
+    dy = torch.empty(N, Ho, Wo, 64, dtype=torch.bfloat16, device=dev)
+    ops.stem1_route_bwd(xs, wp1, dp.to(dev), idx.to(dev), sc.to(dev), sh.to(dev), mean.to(dev), istd.to(dev),
+                        gamma.to(dev), sum_g.to(dev), sum_gx.to(dev), dy, N, H, W)
+    g2 = torch.full((64, 3, 7, 7), float("nan"), device=dev)
+    ops.stem1_wgrad_into(dy, xs, N, H, W, g2)
+    torch.cuda.synchronize()
+    gf, g2 = gf.double().cpu(), g2.double().cpu()
+    assert torch.isfinite(gf).all()
+    assert torch.equal(gf[:, 0], gf[:, 1]) and torch.equal(gf[:, 0], gf[:, 2])
+    r_two = ((gf - g2).norm() / g2.norm()).item()
+    # fp64 reference: BN backward of the routed gradient, then the conv weight gradient
+    y0 = _ref_y0(xu, w).to(torch.bfloat16).double()
+    gr = _route_ref(dp, idx, Ho, Wo)
+    v = lambda t: t.double().view(1, 64, 1, 1)              # noqa: E731
+    k = v(gamma) * v(istd)
+    mg, mgx = v(sum_g / M), v(sum_gx / M)
+    dyr = k * gr - k * v(istd) * mgx * y0 - k * mg + k * v(istd) * mgx * v(mean)
+    x = ((xu.float() - MEAN) * (1.0 / STD)).to(torch.bfloat16).double()
+    wref = torch.nn.grad.conv2d_weight(x, (64, 1, 7, 7), dyr, stride=2, padding=3)
+    r_ref = ((gf[:, :1] - wref).norm() / wref.norm()).item()
+    print(f"stem fused backward {N}x{H}x{W}: vs two-pass {r_two:.2e}, vs fp64 {r_ref:.2e}")
+    assert r_two < 1e-4, r_two
+    assert r_ref < 1e-2, r_ref

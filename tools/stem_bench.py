@@ -79,10 +79,17 @@ def main():
     res["fused_route_bwd_us"] = timeit(
         lambda: ops.stem1_route_bwd(xs, wp1, dp, idx, sc, sh, mean, istd, gamma, sg[0], sgx[0], dy0, N, H, W),
         a.iters)
+    gw = torch.empty(64, 3, 7, 7, device=dev)
+    res["stem_wgrad_us"] = timeit(lambda: ops.stem1_wgrad_into(dy0, xs, N, H, W, gw), a.iters)
+    res["fused_bwd_all_us"] = timeit(
+        lambda: ops.stem1_bwd_fused_into(xs, wp1, dp, idx, mean, istd, gamma, sg[0], sgx[0], N, H, W, gw), a.iters)
     res["stem1_prep_u8_us"] = timeit(lambda: ops.stem1_prep_u8(xu, xs, 127.5, 73.9), a.iters)
     res["unfused_total_us"] = round(res["unfused_stem_fwd_us"] + res["unfused_maxpool_fwd_us"]
                                     + res["unfused_maxpool_bwd_apply_us"], 1)
     res["fused_total_us"] = round(res["fused_pool_fwd_us"] + res["pooled_bn_relu_us"] + res["fused_route_bwd_us"], 1)
+    res["unfused_with_wgrad_us"] = round(res["unfused_total_us"] + res["stem_wgrad_us"], 1)
+    res["fused_one_pass_bwd_total_us"] = round(res["fused_pool_fwd_us"] + res["pooled_bn_relu_us"]
+                                               + res["fused_bwd_all_us"], 1)
     print(json.dumps(res))
 
 

@@ -94,7 +94,7 @@ static int gemm_lin(int M, int N, int K, int ksplit, const LA& la, const LB& lb,
   if constexpr (use_bk<T, LA, LB>()) {
     // VLP_LIN_PP: 0 off, 1 same-layout GEMMs only, 2 (default) also the data gradients
     // (NesT step +2.6 % and +0.7 %)
-    static const int lin_pp = getenv("VLP_LIN_PP") ? atoi(getenv("VLP_LIN_PP")) : 2;
+    constexpr int lin_pp = 2;   // linear GEMMs on the ping-pong kernel: same-layout and data gradients (measured)
     if (lin_pp && gemm_variant() >= 5 && M >= 256 && N >= 256 && K >= 256 && K % 64 == 0) {
       if constexpr (LA::kKContig == LB::kKContig) return gemm_big_auto(M, N, K, ksplit, la, lb, ep, st);
       // data gradients (K-contig dy x MN-contig W)
@@ -759,7 +759,7 @@ VLP_EXPORT int vlp_linear_wgrad(int dtype, int M, int Nout, int Kin, const void*
                                 const void* x, int ldx, float* dw, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   // each split reduces >= 1024 token rows (short splits were prologue/atomic bound)
-  static const int rows_per_split = getenv("VLP_LINW_ROWS") ? atoi(getenv("VLP_LINW_ROWS")) : 1024;
+  constexpr int rows_per_split = 1024;
   int tiles = ((Nout + 127) / 128) * ((Kin + 127) / 128);
   int ksplit = (512 + tiles - 1) / tiles;
   int maxsplit = (M + rows_per_split - 1) / rows_per_split;
@@ -785,7 +785,7 @@ VLP_EXPORT int vlp_linear_wgrad_ws(int dtype, int M, int Nout, int Kin, const vo
   // each split reduces >= VLP_LINW_WS_ROWS token rows: the text tower runs on a
   // side stream beside the image tower, where CU time per FLOP (prologue,
   // epilogue, slab traffic), not latency, is what the step pays for
-  static const int rows = getenv("VLP_LINW_WS_ROWS") ? atoi(getenv("VLP_LINW_WS_ROWS")) : 256;
+  constexpr int rows = 256;   // minimum token rows per split of the text weight gradients
   const int tiles = ((Nout + 127) / 128) * ((Kin + 127) / 128);
   int ks = (512 + tiles - 1) / tiles;
   const int maxsplit = (M + rows - 1) / rows;
@@ -797,7 +797,7 @@ VLP_EXPORT int vlp_linear_wgrad_ws(int dtype, int M, int Nout, int Kin, const vo
   MNMat<bf16> la{(const bf16*)dy, lddy, Nout, M};
   MNMat<bf16> lb{(const bf16*)x, ldx, Kin, M};
   EpiSplitStore ep{nullptr, nullptr, ws, Kin, (size_t)Nout * Kin};
-  static const int lin_pp = getenv("VLP_LIN_PP") ? atoi(getenv("VLP_LIN_PP")) : 1;
+  constexpr int lin_pp = 1;   // weight gradients: the same-layout ping-pong tiles only (measured)
   int r;
   if (lin_pp && gemm_variant() >= 5 && Nout >= 256 && Kin >= 256 && M >= 16384 && M % 64 == 0) {
     // deep token reductions (NesT level 2) on the 256x256 ping-pong kernel: one
@@ -892,7 +892,7 @@ static void ln_bwd_t(int M, int D, const void* dy, float p_out, unsigned long lo
   // (640 blocks at M = 10240 serialised on 624 addresses: 36 us per launch);
   // the cap applies to text-sized M only: NesT's 0.1-2 M token rows need the
   // wide grid for bandwidth (a 160 or M/2048 cap there: -3 % per NesT step)
-  static const int cap = getenv("VLP_LNB_BLOCKS") ? atoi(getenv("VLP_LNB_BLOCKS")) : 160;
+  constexpr int cap = 160;   // LayerNorm-backward grid cap for text-sized M (atomic fan-in)
   int blocks = (M + 15) / 16;
   const int lim = M <= 65536 ? cap : 4096;
   if (blocks > lim) blocks = lim;

@@ -922,14 +922,10 @@ static inline int ew_grid(size_t nchunks) { return ew_blocks(nchunks, 256, 4096)
 // stores take bn_add_relu from 4.8-4.9 to 5.2-6.3 TB/s at layers 1-2 and do
 // not help bn_bwd_apply, so the defaults are 4 and 0.
 static inline int ew_variant() {
-  static int v = -1;
-  if (v < 0) v = getenv("VLP_EW") ? atoi(getenv("VLP_EW")) : 4;
-  return v;
+  return 4;
 }
 static inline int ewb_variant() {
-  static int v = -1;
-  if (v < 0) v = getenv("VLP_EWB") ? atoi(getenv("VLP_EWB")) : 0;
-  return v;
+  return 0;
 }
 
 }  // namespace vlp

@@ -1090,7 +1090,7 @@ template <typename T, class LA, class LB, class EP>
 static int gemm_s2(int M, int N, int K, const LA& la, const LB& lb, const EP& ep, hipStream_t st) {
   if constexpr (use_bk<T, LA, LB>()) {
     // 256x64 on the two-tiles-in-flight engine: +3 % over the one-tile ring
-    static const int s2v = getenv("VLP_S2_BIG") ? atoi(getenv("VLP_S2_BIG")) : 1;
+    constexpr int s2v = 1;
     if (N <= 64 && s2v == 1) return launch_gemm_big<256, 64, 4, 1>(M, N, K, 1, la, lb, ep, st);
     if (N <= 64 && s2v == 2) return launch_gemm_big<128, 64, 2, 1>(M, N, K, 1, la, lb, ep, st);
   }
@@ -1106,13 +1106,13 @@ template <typename T, class LA, class LB, class EP>
 static int gemm_wgrad(int M, int N, int K, const LA& la, const LB& lb, const EP& ep, hipStream_t st) {
   if (M <= 64) return gemm_short<T>(M, N, K, -2048, la, lb, ep, st);
   if constexpr (use_bk<T, LA, LB>()) {   // large tiles, one workgroup per CU: slot-balanced split
-    static const int mink5 = getenv("VLP_WGRAD_MINK") ? atoi(getenv("VLP_WGRAD_MINK")) : 2048;
+    constexpr int mink5 = 2048;
     if (gemm_variant() >= 5) return gemm_conv_wide<T>(M, N, K, -mink5, la, lb, ep, st);
   }
-  static const int balanced = getenv("VLP_WGRAD_BALANCED") ? atoi(getenv("VLP_WGRAD_BALANCED")) : 0;
+  constexpr int balanced = 0;
   if (balanced) return gemm_wide<T>(M, N, K, -balanced, la, lb, ep, st);
-  static const int target = getenv("VLP_WGRAD_TARGET") ? atoi(getenv("VLP_WGRAD_TARGET")) : 1024;
-  static const int mink = getenv("VLP_WGRAD_MINK") ? atoi(getenv("VLP_WGRAD_MINK")) : 4096;
+  constexpr int target = 1024;
+  constexpr int mink = 4096;
   const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
   int ksplit = (target + tiles - 1) / tiles;
   const int maxsplit = (K + mink - 1) / mink;
@@ -1343,7 +1343,7 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
 }
 
 static bool rows_c64_ok(const ConvGeom& g) {
-  static const int off = getenv("VLP_NO_ROWCONV") ? atoi(getenv("VLP_NO_ROWCONV")) : 0;
+  constexpr int off = 0;
   return !off && g.C == 64 && g.Co == 64 && g.KH == 3 && g.KW == 3 && g.S == 1 && g.P == 1 && g.W == kRcW &&
          g.H >= 3 && (size_t)g.N * g.H * kRcW * 128 < (1ull << 31);
 }
@@ -1540,7 +1540,7 @@ static int conv_wgrad_ws_t(const void* dy, const void* x, float* ws, long long w
   if constexpr (std::is_same<T, bf16>::value) {
     // tile engines whose epilogue honours per-split output slabs
     if (gemm_variant() >= 5 && g.K % 4 == 0) {
-      static const int mink5 = getenv("VLP_WGRAD_MINK") ? atoi(getenv("VLP_WGRAD_MINK")) : 2048;
+      constexpr int mink5 = 2048;
       int mink = g.Co <= 64 ? 2048 : mink5;
       const int need = (g.M + max_ks - 1) / max_ks;
       if (mink < need) mink = need;

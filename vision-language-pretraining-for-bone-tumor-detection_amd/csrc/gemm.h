@@ -1747,18 +1747,13 @@ constexpr int gemm_lds_bytes() { return 2 * (BM + BN) * 128; }
 
 // ---------------- variant dispatch ----------------
 // bf16 + direct loaders -> multi-stage kernels; everything else -> the
-// register-staged 2-stage kernel.  VLP_GEMM_VARIANT selects among tile /
-// stage configurations (for on-device A/B runs; the default is the measured best).
+// register-staged 2-stage kernel.  VLP_GEMM_DEFAULT_VARIANT (compile time) selects among tile /
+// stage configurations (tools/build_variant.sh builds A/B libraries; the default is the measured best).
 #ifndef VLP_GEMM_DEFAULT_VARIANT
 #define VLP_GEMM_DEFAULT_VARIANT 5
 #endif
 inline int gemm_variant() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("VLP_GEMM_VARIANT");
-    v = e ? atoi(e) : VLP_GEMM_DEFAULT_VARIANT;
-  }
-  return v;
+  return VLP_GEMM_DEFAULT_VARIANT;
 }
 template <typename T, class LA, class LB>
 constexpr bool use_ms() {
@@ -1779,7 +1774,7 @@ inline int gemm_big_auto(int M, int N, int K, int ksplit, const LA& la, const LB
   // data-gradient GEMMs +3 %), MN x MN weight gradients another +2.4 % (layers
   // 3-4 +10-19 %); the 128x256 MN tiles of layer 2 lose (-10 %) and stay on
   // gemm_big_kernel, as do 256x128 K-contig tiles)
-  static const int pp = getenv("VLP_PP") ? atoi(getenv("VLP_PP")) : 2;
+  constexpr int pp = 2;   // ping-pong kernel for K-contig 256x256 and MNxMN weight gradients
   constexpr bool kk = LA::kKContig && LB::kKContig;
   constexpr bool mm = !LA::kKContig && !LB::kKContig;
   if constexpr (kk || mm) {
@@ -1799,7 +1794,7 @@ inline int gemm_big_auto(int M, int N, int K, int ksplit, const LA& la, const LB
   // N = 128: 128x128 tiles (4 waves, 64 KB ring) run two workgroups per CU, so
   // one tile's epilogue overlaps the other's main loop (layer 2, K = 1152 is
   // only 18 K-steps per tile); measured +1 % per step over 256x128
-  static const int n128 = getenv("VLP_BIG_N128") ? atoi(getenv("VLP_BIG_N128")) : 1;
+  constexpr int n128 = 1;
   if (n128 == 1) return launch_gemm_big<128, 128, 2, 2>(M, N, K, ksplit, la, lb, ep, st);
   return launch_gemm_big<256, 128, 4, 2>(M, N, K, ksplit, la, lb, ep, st);
 }
@@ -1855,7 +1850,7 @@ inline int gemm_short(int M, int N, int K, int ksplit, const LA& la, const LB& l
   if constexpr (use_bk<T, LA, LB>()) {
     // 64 x 192 tiles (3 taps of 64 channels) on the two-K-tiles-in-flight engine:
     // the 4-wave 64 x 128 ring kept one K-tile in flight and was latency-bound
-    static const int short_big = getenv("VLP_SHORT_BIG") ? atoi(getenv("VLP_SHORT_BIG")) : 1;
+    constexpr int short_big = 1;
     if (gemm_variant() >= 5 && short_big && N % 192 == 0)
       return launch_gemm_big<64, 192, 1, 4>(M, N, K, ksplit, la, lb, ep, st);
     if (gemm_variant() >= 4) return launch_gemm_bk<64, 128, 1, 4>(M, N, K, ksplit, la, lb, ep, st);

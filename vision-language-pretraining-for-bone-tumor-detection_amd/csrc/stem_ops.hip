@@ -51,6 +51,10 @@ __device__ __forceinline__ uint4 neg_bf16x8(uint4 u) {
   return u;
 }
 
+__device__ __forceinline__ unsigned lds_addr_stem(const void* p) {
+  return (unsigned)(unsigned long long)(const __attribute__((address_space(3))) char*)p;
+}
+
 __device__ __forceinline__ v8bf as_v8bf(const uint4& u) { return *reinterpret_cast<const v8bf*>(&u); }
 
 // LDS-only barrier: waits for this wave's LDS traffic, not for its global
@@ -409,6 +413,223 @@ stem1_route_bwd_kernel(Stem1Geom g, const bf16* __restrict__ xs, const bf16* __r
   }
 }
 
+
+// ---------------------------------------------------------------- fused backward
+// The stem's whole backward in one pass: per pair of conv-output rows,
+//   1. the patch tile P [2 rows][Wo px][64 k] (bf16, from xs) is staged in LDS,
+//   2. y0 = W1 * P is recomputed on MFMA into the row tile Y [2][Wo][64],
+//   3. the pooled gradient is routed and dy = k*g + b*y0 + c written over Y,
+//   4. dW1[co][k] += sum_px dy[px][co] * P[px][k] on MFMA, both operands read
+//      transposed from LDS (ds_read_b64_tr_b16: lane i of a 16-lane group gets
+//      column i of 4 consecutive rows),
+// so neither y0 nor dy ever reaches HBM.  Each workgroup accumulates its
+// band's 64 x 64 weight gradient in registers (each wave a 32 x 32 quadrant
+// over every other k-step), sums the pairs in LDS and writes one fp32 slab [64][64];
+// vlp_stem1_wgrad_fold sums the slabs and replicates them over the 3 input
+// channels.  512 threads; LDS: W1 8 KB + P 2*Wo*128 + Y 2*Wo*128 + 1.25 KB.
+constexpr int kStemFusedPairs = 16;   // row pairs per workgroup
+
+// transposed fragment of a [px][64] tile (stile_off layout): lane (i, g) gets
+// column col0 + i of rows row0 + 8g .. +7 (the MFMA operand with k = px)
+__device__ __forceinline__ v8bf tile_tr(const char* tile, int row0, int col0) {
+  const int l = threadIdx.x & 63;
+  const int i = l & 15, g = l >> 4;
+  const int q = i >> 2, p = i & 3;
+  const int col = col0 + 4 * p;
+  const int r = row0 + 8 * g + q;
+  const char* a0 = tile + stile_off(r, col >> 3) + ((col >> 2) & 1) * 8;
+  const char* a1 = tile + stile_off(r + 4, col >> 3) + ((col >> 2) & 1) * 8;
+  v4bf lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(lds_addr_stem(a0)));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(lds_addr_stem(a1)));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+template <int NA>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+stem1_bwd_fused_kernel(Stem1Geom g, const bf16* __restrict__ xs, const bf16* __restrict__ wp1, int Hq, int Wq,
+                       const bf16* __restrict__ dp, const uint8_t* __restrict__ idx,
+                       const float* __restrict__ mean, const float* __restrict__ istd,
+                       const float* __restrict__ gamma, const double* __restrict__ sg,
+                       const double* __restrict__ sgx, float* __restrict__ slabs) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int Ho = g.Ho, Wo = g.Wo;
+  const int tile_bytes = 2 * Wo * 128;                // two conv-output rows
+  char* wl = smem;
+  char* ptile = smem + 8192;
+  char* ytile = ptile + tile_bytes;
+  float* cl = reinterpret_cast<float*>(smem + 8192 + (2 * tile_bytes > 131072 ? 2 * tile_bytes : 131072));
+  const int HP = Ho / 2;
+  const int bands = (HP + kStemFusedPairs - 1) / kStemFusedPairs;
+  const int n = blockIdx.x / bands, band = blockIdx.x - n * bands;
+  const int a0 = band * kStemFusedPairs;
+  int a1 = a0 + kStemFusedPairs;
+  if (a1 > HP) a1 = HP;
+  const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
+  const int c = tid & 7;                               // routing: this thread's 8-channel chunk
+  const bf16* xn = xs + (size_t)n * g.Hp * g.Wp1;
+  const bf16* dp_n = dp + (size_t)n * Hq * Wq * 64;
+  const uint8_t* idx_n = idx + (size_t)n * Hq * Wq * 64;
+  const char* xb = reinterpret_cast<const char*>(xn);
+
+  // patch tile staging: item = (row r, pixel px, chunk kh) -> 16 B of xs
+  constexpr int NP = 2 * NA;                           // 2 rows * Wo * 8 chunks / 512 threads
+  uint4 pf[NP];
+  auto p_load = [&](int pa) __attribute__((always_inline)) {
+#pragma unroll
+    for (int it = 0; it < NP; ++it) {
+      const int item = tid + 512 * it;
+      const int r = item / (Wo * 8), rem = item - r * Wo * 8;
+      const int px = rem >> 3, kh = rem & 7;
+      const int sh = px & 3, ho = 2 * pa + r;
+      const unsigned e = (unsigned)sh * (unsigned)g.copy + (unsigned)(2 * ho + kh) * (unsigned)g.Wp1 +
+                         (unsigned)(2 * px - 2 * sh);
+      pf[it] = ldg16(xb + 2u * e);
+    }
+  };
+  auto p_store = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int it = 0; it < NP; ++it) {
+      const int item = tid + 512 * it;
+      const int r = item / (Wo * 8), rem = item - r * Wo * 8;
+      *reinterpret_cast<uint4*>(ptile + r * (Wo * 128) + stile_off(rem >> 3, rem & 7)) = pf[it];
+    }
+  };
+  p_load(a0);
+  stage_w(wp1, nullptr, wl);
+  if (tid < 64) {
+    const int co = tid;
+    const float inv_count = 1.f / (float)((double)g.N * Ho * Wo);
+    const float is = istd[co];
+    const float k = gamma[co] * is;
+    const float mg = (float)(sg[co] * (double)inv_count), mgx = (float)(sgx[co] * (double)inv_count);
+    cl[co] = k;
+    cl[64 + co] = -k * is * mgx;
+    cl[128 + co] = -k * mg + k * is * mgx * mean[co];
+  }
+  // dW1[co][k] split over the waves: wave wv owns the 32 x 32 quadrant (co half
+  // (wv >> 1) & 1, k half wv & 1) and every other 32-px k-step (parity wv >> 2)
+  const int qco = 32 * ((wv >> 1) & 1), qk = 32 * (wv & 1);
+  v4f dw[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) dw[a][b] = v4f{0.f, 0.f, 0.f, 0.f};
+  // y0 recompute split: wave -> row (wv >> 2), columns 16*NA*(wv & 3) ..
+  const int yr = wv >> 2, yseg = 16 * NA * (wv & 3);
+  for (int pa = a0; pa < a1; ++pa) {
+    p_store();
+    if (pa + 1 < a1) p_load(pa + 1);                   // the next pair's patches fly across this pair
+    lds_barrier();
+    // ---- 2: y0 on MFMA (A = W1 from LDS, B = patch fragments from the P tile), one
+    //         16-px fragment at a time (16 accumulator registers live) ----
+    {
+      const char* prow = ptile + yr * (Wo * 128);
+      char* yrow = ytile + yr * (Wo * 128);
+#pragma unroll 1
+      for (int a = 0; a < NA; ++a) {
+        const int px = yseg + 16 * a + (l & 15);
+        const v8bf p0 = *reinterpret_cast<const v8bf*>(prow + stile_off(px, l >> 4));
+        const v8bf p1 = *reinterpret_cast<const v8bf*>(prow + stile_off(px, 4 + (l >> 4)));
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int co = 16 * b + (l & 15);
+          const v8bf w0 = *reinterpret_cast<const v8bf*>(wl + stile_off(co, l >> 4));
+          const v8bf w1 = *reinterpret_cast<const v8bf*>(wl + stile_off(co, 4 + (l >> 4)));
+          v4f t = v4f{0.f, 0.f, 0.f, 0.f};
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, p0, t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, p1, t, 0, 0, 0);
+          const int co0 = 16 * b + 4 * (l >> 4);
+          v4bf v;
+          v[0] = (bf16)t[0]; v[1] = (bf16)t[1]; v[2] = (bf16)t[2]; v[3] = (bf16)t[3];
+          *reinterpret_cast<v4bf*>(yrow + stile_off(px, co0 >> 3) + ((co0 >> 2) & 1) * 8) = v;
+        }
+      }
+    }
+    lds_barrier();
+    // ---- 3: route the pooled gradient; dy = k*g + b*y0 + c over the Y tile ----
+    const bool v10 = pa + 1 < Hq;
+#pragma unroll 1
+    for (int item = tid; item < 4 * Wo; item += 512) {
+      const int q = item >> 3;                         // column pair 2q, 2q + 1 (chunk c = item & 7)
+      const bool v01 = q + 1 < Wq;
+      const int pa1 = v10 ? pa + 1 : pa, q1 = v01 ? q + 1 : q;
+      uint4 pv[4];
+      uint2 ib[4];
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) {
+        const int ho = (k4 >> 1) ? pa1 : pa, wo = (k4 & 1) ? q1 : q;
+        const unsigned po = ((unsigned)ho * Wq + wo) * 64 + 8 * c;
+        pv[k4] = ldg16(dp_n + po);
+        ib[k4] = *reinterpret_cast<const uint2*>(idx_n + po);
+      }
+      float ka[8], ba[8], ca[8];
+      ld8f_lds(cl + 8 * c, ka);
+      ld8f_lds(cl + 64 + 8 * c, ba);
+      ld8f_lds(cl + 128 + 8 * c, ca);
+      float f[4][8];
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) unpack8(pv[k4], f[k4]);
+      const bool v11 = v01 && v10;
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) {   // pixel (2pa + (k4 >> 1), 2q + (k4 & 1))
+        float yv[8], d[8];
+        const int px = 2 * q + (k4 & 1);
+        char* at = ytile + (k4 >> 1) * (Wo * 128) + stile_off(px, c);
+        unpack8(*reinterpret_cast<const uint4*>(at), yv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          unsigned t[4];
+#pragma unroll
+          for (int m = 0; m < 4; ++m) t[m] = (((e >> 2) ? ib[m].y : ib[m].x) >> (8 * (e & 3))) & 255u;
+          float gsum;
+          if (k4 == 0) gsum = t[0] == 4u ? f[0][e] : 0.f;
+          else if (k4 == 1) gsum = (t[0] == 5u ? f[0][e] : 0.f) + ((v01 && t[1] == 3u) ? f[1][e] : 0.f);
+          else if (k4 == 2) gsum = (t[0] == 7u ? f[0][e] : 0.f) + ((v10 && t[2] == 1u) ? f[2][e] : 0.f);
+          else
+            gsum = (t[0] == 8u ? f[0][e] : 0.f) + ((v01 && t[1] == 6u) ? f[1][e] : 0.f) +
+                   ((v10 && t[2] == 2u) ? f[2][e] : 0.f) + ((v11 && t[3] == 0u) ? f[3][e] : 0.f);
+          d[e] = fmaf(ka[e], gsum, fmaf(ba[e], yv[e], ca[e]));
+        }
+        *reinterpret_cast<uint4*>(at) = Chunk<bf16>::pack(d);
+      }
+    }
+    lds_barrier();
+    // ---- 4: dW1 += dy^T P over this pair's 2*Wo pixels (k-steps of 32 px split over the waves) ----
+    for (int ks = wv >> 2; ks < Wo / 16; ks += 2) {
+      const int r = (32 * ks) / Wo, px0 = 32 * ks - r * Wo;
+      const char* yb = ytile + r * (Wo * 128);
+      const char* pb = ptile + r * (Wo * 128);
+      v8bf fa[2], fb[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) fa[a] = tile_tr(yb, px0, qco + 16 * a);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) fb[b] = tile_tr(pb, px0, qk + 16 * b);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the asm reads' results (hipcc does not track them)
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) dw[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[b], dw[a][b], 0, 0, 0);
+    }
+    lds_barrier();                                     // P and Y are rewritten by the next pair
+  }
+  // ---- the two k-parity waves of each quadrant summed through LDS: one fp32 slab per workgroup ----
+  float* red = reinterpret_cast<float*>(ptile);        // [2 parities][64 co][64 k]
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = qco + 16 * a + 4 * (l >> 4) + r, k = qk + 16 * b + (l & 15);
+        red[((wv >> 2) * 64 + co) * 64 + k] = dw[a][b][r];
+      }
+  __syncthreads();
+  float* slab = slabs + (size_t)blockIdx.x * 4096;
+  for (int e = tid; e < 4096; e += 512) slab[e] = red[e] + red[4096 + e];
+}
+
 }  // namespace vlp
 
 using namespace vlp;
@@ -470,5 +691,44 @@ VLP_EXPORT int vlp_stem1_route_bwd(const void* xs, const void* wp1, const void* 
                      hipLaunchKernelGGL(stem1_route_bwd_kernel<NAC>, dim3(N * bands), dim3(256), lds, st, g,
                                         (const bf16*)xs, (const bf16*)wp1, Hq, Wq, (const bf16*)dp, idx, sc, sh,
                                         mean, istd, gamma, sum_g, sum_gx, (bf16*)dy));
+  return (int)hipGetLastError();
+}
+
+static int stem1_bwd_fused_wgs(int N, int H, int W) {
+  const Stem1Geom g = make_stem1(N, H, W);
+  return N * ((g.Ho / 2 + kStemFusedPairs - 1) / kStemFusedPairs);
+}
+// Number of fp32 [64][64] slabs vlp_stem1_bwd_fused writes (one per workgroup).
+VLP_EXPORT int vlp_stem1_bwd_fused_slabs(int N, int H, int W, int* nslabs) {
+  *nslabs = stem1_bwd_fused_wgs(N, H, W);
+  return 0;
+}
+
+// The whole stem backward (route + BN backward + weight gradient), y0 and dy
+// never materialised: slabs [vlp_stem1_bwd_fused_slabs][64][64] -> vlp_stem1_wgrad_fold.
+VLP_EXPORT int vlp_stem1_bwd_fused(const void* xs, const void* wp1, const void* dp, const uint8_t* idx,
+                                   const float* mean, const float* istd, const float* gamma, const double* sum_g,
+                                   const double* sum_gx, float* slabs, long long slab_floats, int N, int H, int W,
+                                   void* stream) {
+  if (!vlp_stem1_fused_ok(H, W) || N < 1) return (int)hipErrorInvalidValue;
+  const Stem1Geom g = make_stem1(N, H, W);
+  if (!stem1_offsets_fit(g)) return (int)hipErrorInvalidValue;
+  const int nwg = stem1_bwd_fused_wgs(N, H, W);
+  if ((long long)nwg * 4096 > slab_floats) return (int)hipErrorInvalidValue;
+  const int Hq = (g.Ho + 2 - 3) / 2 + 1, Wq = (g.Wo + 2 - 3) / 2 + 1;
+  // the P and Y tiles (4 * Wo * 128 B), at least the 8 x 16 KB of the final cross-wave sum
+  const size_t tiles = 4 * (size_t)g.Wo * 128 > 131072 ? 4 * (size_t)g.Wo * 128 : 131072;
+  const size_t lds = 8192 + tiles + 3 * 64 * sizeof(float);
+  hipStream_t st = (hipStream_t)stream;
+  VLP_STEM_NA_SWITCH(g.Wo / 64, {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)&stem1_bwd_fused_kernel<NAC>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 4 * 256 * 128 + 3 * 64 * 4);
+      attr = true;
+    }
+    hipLaunchKernelGGL(stem1_bwd_fused_kernel<NAC>, dim3(nwg), dim3(512), lds, st, g, (const bf16*)xs,
+                       (const bf16*)wp1, Hq, Wq, (const bf16*)dp, idx, mean, istd, gamma, sum_g, sum_gx, slabs);
+  });
   return (int)hipGetLastError();
 }

@@ -220,6 +220,22 @@ def stem1_route_bwd(xs, wp1, dp, idx, sc, sh, mean, istd, gamma, sum_g, sum_gx, 
                               ptr(gamma), ptr(sum_g), ptr(sum_gx), ptr(dy), N, H, W, _s())
 
 
+def stem1_bwd_fused_into(xs, wp1, dp, idx, mean, istd, gamma, sum_g, sum_gx, N, H, W, grad):
+    """grad[64][3][7][7] = the stem weight gradient from the pooled gradient dp
+    (ReLU-masked): routing, BN backward and the weight-gradient GEMM in one pass
+    (y0 and dy never written), per-workgroup slabs folded by vlp_stem1_wgrad_fold."""
+    import ctypes
+    ns = ctypes.c_int(0)
+    lib().vlp_stem1_bwd_fused_slabs(N, H, W, ctypes.addressof(ns))
+    ws = wgrad_ws(dp.device)
+    tk = ktimer.begin("stem_bwd_fused", 4.0 * N * (H // 2) * (W // 2) * 64 * 64)
+    lib().vlp_stem1_bwd_fused(ptr(xs), ptr(wp1), ptr(dp), ptr(idx), ptr(mean), ptr(istd), ptr(gamma), ptr(sum_g),
+                              ptr(sum_gx), ptr(ws), ws.numel(), N, H, W, _s())
+    ktimer.end(tk)
+    lib().vlp_stem1_wgrad_fold(ns.value, ptr(ws), ptr(grad), _s())
+    return grad
+
+
 def stem_prep(x_nchw, xp):
     N, _, H, W = x_nchw.shape
     lib().vlp_stem_prep(dcode(xp), ptr(x_nchw), ptr(xp), N, H, W, _s())

@@ -547,16 +547,13 @@ class ResNet34Tower(ArenaModule):
         sc0, sh0, mu0, is0 = self._coef(ws, "bn1")
         sg0f, sgx0f = self._bstat(ws, "bn1", full=True)
         if saved.get("stem_fused"):
-            # the pooled gradient routed to each window's tap and through the BN
-            # backward, y0 recomputed on the fly (vlp_stem1_route_bwd)
+            # the pooled gradient routed to each window's tap, through the BN backward
+            # (y0 recomputed) and into the weight gradient in one pass (vlp_stem1_bwd_fused)
             ops.bn_grad_rep(STAT_REP, 64, sg0f, sgx0f, self.arena.gview("bn1.weight"),
                             self.arena.gview("bn1.bias"))
             N, H, W = saved["N"], saved["H"], saved["W"]
-            Ho, Wo = (H + 6 - 7) // 2 + 1, (W + 6 - 7) // 2 + 1
-            dy0 = torch.empty(N, Ho, Wo, 64, dtype=T, device=dev)
-            ops.stem1_route_bwd(saved["xs"], ws["conv1.wp1"], dout, idx, sc0, sh0, mu0, is0,
-                                self.arena.view("bn1.weight"), sg0f[:64], sgx0f[:64], dy0, N, H, W)
-            ops.stem1_wgrad_into(dy0, saved["xs"], N, H, W, self.arena.gview("conv1.weight"))
+            ops.stem1_bwd_fused_into(saved["xs"], ws["conv1.wp1"], dout, idx, mu0, is0, self.arena.view("bn1.weight"),
+                                     sg0f[:64], sgx0f[:64], N, H, W, self.arena.gview("conv1.weight"))
             self._stage_done(["layer1", "stem"], on_stage_done, dev)
             return
         if saved.get("yarg") is None:
