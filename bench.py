@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--cpu-sample-batch", type=int, default=None,
                     help="CPU-baseline sample batch (default 32; 4 for nest_small)")
     ap.add_argument("--cpu-sample-steps", type=int, default=3)
+    ap.add_argument("--no-cpu-configs0", dest="cpu_configs0", action="store_false",
+                    help="skip the cpu_baseline sample at BASELINE configs[0] (bs=8, 224^2)")
     ap.add_argument("--roofline-kernel", default="auto")
     ap.add_argument("--kernel-report", default="")
     ap.add_argument("--pcie-steps", type=int, default=5,
@@ -241,13 +243,22 @@ def loss_delta_vs_fp32(args, model, host):
 
 
 def cpu_baseline(args):
-    """Oracle (reference CPU fp32 path, restated) on a bounded sample."""
+    """Oracle (reference CPU fp32 path, restated) on a bounded sample of the bench
+    workload, plus the same step at BASELINE configs[0] (bs=8, 224^2, the
+    reference's own CPU-runnable case) beside it."""
+    res = _cpu_oracle_steps(args, args.cpu_sample_batch, args.image_size, args.seq_len)
+    if args.image_model == "resnet34" and args.cpu_configs0:
+        c0 = _cpu_oracle_steps(args, 8, 224, args.seq_len)
+        res["configs0"] = {k: c0[k] for k in ("value", "unit", "cores", "sample")}
+    return res
+
+
+def _cpu_oracle_steps(args, B, H, T):
     from oracle import weights as W
     from oracle.clip import OracleVLP, compute_loss
     from tests.golden.synth import synth_batch
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     torch.set_num_threads(threads)
-    B, H, T = args.cpu_sample_batch, args.image_size, args.seq_len
     model = OracleVLP(128, text_dropout=0.1, image_model=args.image_model, img_size=H)
     if args.image_model == "resnet34":
         W.apply_recipe(model, 0)

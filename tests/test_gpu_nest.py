@@ -99,6 +99,26 @@ def test_tower_bf16_vs_oracle():
     assert errs[len(errs) // 2][0] < 2e-2, errs[len(errs) // 2]
 
 
+def test_tower_bf16_512px_features():
+    """BASELINE configs[3]'s resolution (512^2: 16 level-0 blocks of 32 x 32 tokens),
+    B = 1: the bf16 tower's eval features against the fp32 oracle (rel-L2 <= 5e-2,
+    the bf16 tower gate above)."""
+    import oracle.nest as on
+    from vlp_amd.nest import NestTower
+    torch.manual_seed(9)
+    t = NestTower("nest_small", img_size=512, compute_dtype="bf16", device="cuda")
+    o = on.nest_small(img_size=512)
+    o.load_state_dict({k: v.detach().float().cpu() for k, v in t.state_dict().items()})
+    t.eval(); o.eval()
+    x = torch.randn(1, 3, 512, 512, generator=torch.Generator().manual_seed(9))
+    with torch.no_grad():
+        f = t(x.cuda()).float()
+        fo = o(x)
+    ef = rel(f, fo)
+    print(f"NesT bf16 512px B=1 eval features rel-L2 {ef:.3e}")
+    assert ef < 5e-2, ef
+
+
 def test_uint8_input_matches_float():
     t, _ = make_pair(64, "fp32", seed=2)
     t.eval()
@@ -153,8 +173,12 @@ def test_clip_step_nest_tinybert_bf16_256px():
     TinyBERT contrastive step (text tower on its own stream, as the bench runs
     it) at 256^2 (level-0 blocks of 1024 tokens: the 512^2 block size) against
     the fp32 oracle on the same weights and batch.  DropPath off, text dropout
-    off.  Gates as the bf16 tower test: loss |delta| <= 5e-2, embeddings rel-L2
-    <= 5e-2, every gradient <= 0.3 and the median <= 2e-2."""
+    off.  Loss |delta| <= 5e-2 and embeddings rel-L2 <= 5e-2.  At the module's
+    init the contrastive logits are nearly uniform (loss ~ ln B), so every
+    gradient is a difference of nearly equal embedding terms and bf16 rounding
+    alone moves it by 10-40 %: each gradient tensor is therefore gated against
+    torch's own CPU bf16 autocast run of the same oracle, err(HIP) <= 1.5 *
+    err(autocast) + 0.02, as the ResNet34 step's test_bf16_gradients_vs_torch_autocast."""
     import statistics
     from oracle.clip import OracleVLP, compute_loss
     from src.models.pretrain.VisionLanguageModule import VisionLanguageModule
@@ -163,30 +187,41 @@ def test_clip_step_nest_tinybert_bf16_256px():
                              False, 384, 312, 128, compute_dtype="bf16", text_dropout=0.0, image_size=256,
                              drop_path_rate=0.0)
     m.train()
-    o = OracleVLP(128, text_dropout=0.0, image_model="nest_small", img_size=256)
-    o.load_state_dict({k: v.detach().float().cpu() for k, v in m.state_dict().items()}, strict=False)
-    o.train()
-    for lvl in o.image_encoder.model.levels:
-        for layer in lvl.transformer_encoder:
-            layer.drop_path = 0.0
+    sd = {k: v.detach().float().cpu() for k, v in m.state_dict().items()}
     b = synth_batch(4, 256, 40, 21, with_u8=True)
     bu = {"x-ray-u8": b["x-ray-u8"].cuda(), "label": b["label"], "caption": b["caption"],
           "caption_tokenized": {k: v.cuda() for k, v in b["caption_tokenized"].items()}}
     loss, li, lt, ie, te = m.training_step_outputs(bu)
     loss.backward()
     torch.cuda.synchronize()
-    logits, oie, ote = o({"x-ray": b["x-ray"], "caption_tokenized": b["caption_tokenized"]})
-    lo, _, _ = compute_loss(logits)
-    lo.backward()
-    d = abs(loss.item() - lo.item())
-    ri, rt = rel(ie.float(), oie.detach()), rel(te.float(), ote.detach())
-    og = dict(o.named_parameters())
-    errs = {k: rel(p.grad, og[k].grad) for k, p in m.named_parameters()
-            if p.grad is not None and og[k].grad is not None and og[k].grad.norm() > 0
-            and not k.endswith("attention.self.key.bias")}
-    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:5]
-    print(f"NesT bf16 256px: loss {loss.item():.5f} vs {lo.item():.5f}; emb rel {ri:.2e} / {rt:.2e}; "
-          f"grad median {statistics.median(errs.values()):.3e}; worst {worst}")
+    hip_g = {k: p.grad.float().cpu() for k, p in m.named_parameters() if p.grad is not None}
+
+    def oracle(autocast):
+        o = OracleVLP(128, text_dropout=0.0, image_model="nest_small", img_size=256)
+        o.load_state_dict(sd, strict=False)
+        o.train()
+        for lvl in o.image_encoder.model.levels:
+            for layer in lvl.transformer_encoder:
+                layer.drop_path = 0.0
+        with torch.autocast("cpu", dtype=torch.bfloat16, enabled=autocast):
+            logits, oie, ote = o({"x-ray": b["x-ray"], "caption_tokenized": b["caption_tokenized"]})
+        lo = compute_loss(logits.float())[0]
+        lo.backward()
+        return lo.item(), oie.detach().float(), ote.detach().float(), dict(o.named_parameters())
+
+    lo, oie, ote, og = oracle(False)
+    _, aie, ate, ag = oracle(True)
+    d = abs(loss.item() - lo)
+    ri, rt = rel(ie.float(), oie), rel(te.float(), ote)
+    keys = [k for k in hip_g if og[k].grad is not None and og[k].grad.norm() > 0
+            and not k.endswith("attention.self.key.bias")]
+    e_hip = {k: rel(hip_g[k], og[k].grad) for k in keys}
+    e_ac = {k: rel(ag[k].grad, og[k].grad) for k in keys}
+    excess = sorted(((e_hip[k] - (1.5 * e_ac[k] + 0.02), k, e_hip[k], e_ac[k]) for k in keys), reverse=True)
+    print(f"NesT bf16 256px: loss {loss.item():.5f} vs {lo:.5f}; emb rel {ri:.2e} / {rt:.2e} "
+          f"(autocast {rel(aie, oie):.2e} / {rel(ate, ote):.2e}); grad median hip {statistics.median(e_hip.values()):.3e} "
+          f"autocast {statistics.median(e_ac.values()):.3e}; worst excess "
+          f"{[(round(a, 3), k, round(h, 3), round(c, 3)) for a, k, h, c in excess[:5]]}")
     assert d <= 5e-2 and ri <= 5e-2 and rt <= 5e-2
-    assert worst[0][1] <= 0.3, worst
-    assert statistics.median(errs.values()) <= 2e-2
+    assert excess[0][0] <= 0, excess[:3]
+    assert statistics.median(e_hip.values()) <= 1.5 * statistics.median(e_ac.values()) + 0.01
