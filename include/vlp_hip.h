@@ -148,14 +148,17 @@ int vlp_stem1_pool_fwd(const void* xs, const void* wp1, const float* gamma, void
 int vlp_stem1_route_bwd(const void* xs, const void* wp1, const void* dp, const uint8_t* idx, const float* sc,
                         const float* sh, const float* mean, const float* istd, const float* gamma,
                         const double* sum_g, const double* sum_gx, void* dy, int N, int H, int W, void* stream);
-/* The whole stem backward in one pass (route + BN backward + weight gradient
- * on MFMA, y0 recomputed, dy kept in LDS): one fp32 [64][64] slab per
- * workgroup (vlp_stem1_bwd_fused_slabs), summed and replicated over the 3 input
- * channels by vlp_stem1_wgrad_fold.  dp ReLU-masked as above. */
-int vlp_stem1_bwd_fused_slabs(int N, int H, int W, int* nslabs);
+/* The whole stem backward in one pass (routing + BN backward + weight gradient;
+ * replaces the stem's autograd backward behind VisionLanguageModule.py:30-32):
+ * dW1 = k R + b W1 G + c S with R = sum g P^T (the pooled gradient routed to its
+ * arg-max pixel), G = sum P P^T, S = sum P over the conv-output pixels, so neither
+ * y0 nor dy is formed.  grad [64][3][7][7] is overwritten (the same gradient for
+ * the 3 identical input channels).  dp ReLU-masked as above; ws holds
+ * vlp_stem1_bwd_fused_ws_floats fp32 elements. */
+int vlp_stem1_bwd_fused_ws_floats(int N, int H, int W, long long* n);
 int vlp_stem1_bwd_fused(const void* xs, const void* wp1, const void* dp, const uint8_t* idx, const float* mean,
-                        const float* istd, const float* gamma, const double* sum_g, const double* sum_gx,
-                        float* slabs, long long slab_floats, int N, int H, int W, void* stream);
+                        const float* istd, const float* gamma, const double* sum_g, const double* sum_gx, float* ws,
+                        long long ws_floats, float* grad, int N, int H, int W, void* stream);
 
 /* ---------------- image tower: BatchNorm / residual / pooling ----------------
  * Replace timm resnet34's BatchNorm2d (train-mode batch statistics), ReLU,
@@ -251,6 +254,9 @@ int vlp_linear_wgrad(int dtype, int M, int Nout, int Kin, const void* dy, int ld
  * split partials are plain stores, then one pass folds them into dw (no atomics) */
 int vlp_linear_wgrad_ws(int dtype, int M, int Nout, int Kin, const void* dy, int lddy, const void* x,
                         int ldx, float* dw, float* ws, long long ws_elems, void* stream);
+/* fp32 elements of the workspace vlp_linear_wgrad_ws uses at its full split count
+ * for this shape (host-side query; a smaller workspace trims the splits) */
+int vlp_linear_wgrad_ws_floats(int M, int Nout, int Kin, long long* n);
 /* out[n] += sum_m x[m][n] (bias gradients; fp32 atomics) */
 int vlp_colsum(int dtype, int M, int N, const void* x, int ld, float* out, void* stream);
 int vlp_layernorm_fwd(int dtype, int M, int D, const void* x, const float* gamma,

@@ -221,11 +221,14 @@ def test_tower_fused_stem_matches_unfused_bf16():
 
 @pytest.mark.parametrize("N,H,W", SHAPES)
 def test_stem_bwd_fused_weight_gradient(N, H, W):
-    """vlp_stem1_bwd_fused (route + BN backward + weight gradient in one pass, dy in
-    LDS only) against (a) the two-pass path (vlp_stem1_route_bwd writing dy, then
-    the stem weight-gradient GEMM): same bf16 dy, only the fp32 summation order
-    differs -> rel 1e-4; (b) the fp64 weight gradient of the fp64 BN backward of
-    the routed gradient: rel-L2 <= 1e-2 (dy rounded to bf16 in both kernels)."""
+    """vlp_stem1_bwd_fused (dW1 = k R + b W1 G + c S from the routed-gradient,
+    Gram and patch-sum batch sums; y0 and dy never formed) against (a) the fp64
+    weight gradient of the fp64 BN backward of the routed gradient, on the
+    kernel's bf16 operands with y0 unrounded (what the Gram form computes):
+    rel-L2 <= 2e-3 (the only roundings left: bf16 sums where two pooling windows
+    route to one pixel, fp32 accumulation); (b) the two-pass path
+    (vlp_stem1_route_bwd writing a bf16 dy, then the stem weight-gradient GEMM):
+    rel-L2 <= 1e-2 (that path rounds y0 and dy to bf16)."""
     from vlp_amd import ops
     xu, w, gamma = _inputs(N, H, W, 5 * H + W)
     xs, wp1, yarg, idx, s, ss = _run_fwd(xu, w, gamma)
@@ -246,18 +249,24 @@ def test_stem_bwd_fused_weight_gradient(N, H, W):
     args = [t.to(dev) for t in (mean, istd, gamma, sum_g, sum_gx)]
     gf = torch.full((64, 3, 7, 7), float("nan"), device=dev)
     ops.stem1_bwd_fused_into(xs, wp1, dp.to(dev), idx.to(dev), *args, N, H, W, gf)
+    gf_again = torch.full((64, 3, 7, 7), float("nan"), device=dev)
+    ops.stem1_bwd_fused_into(xs, wp1, dp.to(dev), idx.to(dev), *args, N, H, W, gf_again)
     dy = torch.empty(N, Ho, Wo, 64, dtype=torch.bfloat16, device=dev)
     ops.stem1_route_bwd(xs, wp1, dp.to(dev), idx.to(dev), sc.to(dev), sh.to(dev), mean.to(dev), istd.to(dev),
                         gamma.to(dev), sum_g.to(dev), sum_gx.to(dev), dy, N, H, W)
     g2 = torch.full((64, 3, 7, 7), float("nan"), device=dev)
     ops.stem1_wgrad_into(dy, xs, N, H, W, g2)
     torch.cuda.synchronize()
-    gf, g2 = gf.double().cpu(), g2.double().cpu()
+    # the routed-gradient scatter adds with LDS atomics: a pixel reached by two
+    # windows may sum them in either order (bf16 addition is not associative), so
+    # run-to-run equality is checked to within that rounding, not bit for bit
+    gf, g2, gfa = gf.double().cpu(), g2.double().cpu(), gf_again.double().cpu()
     assert torch.isfinite(gf).all()
     assert torch.equal(gf[:, 0], gf[:, 1]) and torch.equal(gf[:, 0], gf[:, 2])
     r_two = ((gf - g2).norm() / g2.norm()).item()
+    r_rep = ((gf - gfa).norm() / gf.norm()).item()
     # fp64 reference: BN backward of the routed gradient, then the conv weight gradient
-    y0 = _ref_y0(xu, w).to(torch.bfloat16).double()
+    y0 = _ref_y0(xu, w)
     gr = _route_ref(dp, idx, Ho, Wo)
     v = lambda t: t.double().view(1, 64, 1, 1)              # noqa: E731
     k = v(gamma) * v(istd)
@@ -266,6 +275,7 @@ def test_stem_bwd_fused_weight_gradient(N, H, W):
     x = ((xu.float() - MEAN) * (1.0 / STD)).to(torch.bfloat16).double()
     wref = torch.nn.grad.conv2d_weight(x, (64, 1, 7, 7), dyr, stride=2, padding=3)
     r_ref = ((gf[:, :1] - wref).norm() / wref.norm()).item()
-    print(f"stem fused backward {N}x{H}x{W}: vs two-pass {r_two:.2e}, vs fp64 {r_ref:.2e}")
-    assert r_two < 1e-4, r_two
-    assert r_ref < 1e-2, r_ref
+    print(f"stem fused backward {N}x{H}x{W}: vs fp64 {r_ref:.2e}, vs two-pass {r_two:.2e}, run-to-run {r_rep:.1e}")
+    assert r_ref < 2e-3, r_ref
+    assert r_two < 1e-2, r_two
+    assert r_rep < 1e-6, r_rep

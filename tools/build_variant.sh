@@ -6,7 +6,7 @@ ROOT=$(cd $(dirname $0)/.. && pwd)
 CSRC=$ROOT/vision-language-pretraining-for-bone-tumor-detection_amd/csrc
 OUT=$ROOT/build_exp/$NAME
 mkdir -p $OUT/obj
-for f in conv_ops bn_ops bert_ops head_ops optim_ops probe_ops retrieval_ops nest_ops prep_ops; do
+for f in conv_ops stem_ops bn_ops bert_ops head_ops optim_ops probe_ops retrieval_ops nest_ops prep_ops; do
   EXTRA=""
   [ $f = nest_ops ] && EXTRA="-mllvm -amdgpu-mfma-vgpr-form=1"
   [ $f = prep_ops ] && EXTRA="-ffp-contract=off"

@@ -4,6 +4,8 @@ reading y0) against the fused one (vlp_stem1_pool_fwd + the pooled BN/ReLU pass,
 vlp_stem1_route_bwd).  Median of HIP-event timings per kernel, us.
 
   python tools/stem_bench.py [--batch 256] [--size 512] [--iters 10]
+(fused_bwd_all_us: vlp_stem1_bwd_fused, routing + BN backward + weight gradient in
+one pass, the path the step runs; fused_route_bwd_us + stem_wgrad_us: the two-pass form)
 """
 import argparse
 import json

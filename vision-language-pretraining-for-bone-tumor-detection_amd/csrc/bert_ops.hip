@@ -12,11 +12,44 @@
 
 namespace vlp {
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+// NesT short-K / short-side token GEMMs on gemm_big_kernel (tools/build_variant.sh A/B knobs)
+#ifndef VLP_LIN_SHORTK
+#define VLP_LIN_SHORTK 0
+#endif
+#ifndef VLP_LINW_BIG
+#define VLP_LINW_BIG 1
+#endif
+
+// GELU(erf) = x * Phi(x), Phi(x) = (1 + erf(x / sqrt 2)) / 2, with erf from
+// Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, branch-free: one reciprocal and
+// one exp): 1 - erf(z) = P(t) exp(-z^2), t = 1 / (1 + p z), z = |x| / sqrt 2 >= 0.
+// The tail 1 - erf is formed directly (no cancellation for x < 0); the result is
+// within 3.3e-7 absolute of the exact GELU over [-12, 12], as close as
+// 0.5 * x * (1 + erff(.)) in fp32 (4.5e-7), at a third of its VALU cost (the
+// library erff is two branchy polynomials; the NesT fc1 epilogue spent more time
+// in it than in the GEMM).  exp(-z^2) = exp(-x^2 / 2) is also the Gaussian
+// density's exponential, shared by the gradient.
+__device__ __forceinline__ float gelu_tail(float x, float& e) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.2316418883f, ax, 1.f));   // p / sqrt 2 = 0.3275911 / 1.41421356
+  float P = fmaf(t, 1.061405429f, -1.453152027f);
+  P = fmaf(t, P, 1.421413741f);
+  P = fmaf(t, P, -0.284496736f);
+  P = fmaf(t, P, 0.254829592f);
+  P *= t;
+  e = __expf(-0.5f * x * x);
+  return P * e;
+}
+__device__ __forceinline__ float gelu_erf(float x) {
+  float e;
+  const float q = 0.5f * x * gelu_tail(x, e);   // x * (1 - Phi(|x|))
+  return x >= 0.f ? x - q : q;
+}
 __device__ __forceinline__ float gelu_erf_grad(float x) {
-  float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-  float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
+  float e;
+  const float h = 0.5f * gelu_tail(x, e);       // 1 - Phi(|x|)
+  const float cdf = x >= 0.f ? 1.f - h : h;
+  return fmaf(x * 0.3989422804014327f, e, cdf);   // Phi(x) + x phi(x)
 }
 __device__ __forceinline__ float drop_scale(uint64_t seed, uint64_t idx, float p) {
   return hash_uniform(seed, idx) >= p ? 1.f / (1.f - p) : 0.f;
@@ -49,6 +82,41 @@ struct EpiLinear {
     }
     store4(out + (size_t)row * ldo + col, v);
   }
+  // bf16 GEMMs: the row-chunk epilogue (gemm.h ms_epilogue).  acc + bias is staged
+  // once as bf16 (what torch autocast's bf16 linear output holds), then every
+  // thread streams 16-B row chunks of one fixed 8-column group: contiguous 16-B
+  // stores of out / aux and 16-B loads of res instead of 8-B pieces of 16 rows.
+  static constexpr bool kRow = true;
+  static constexpr bool kStageBias = true;
+  static constexpr int kPreDepth = 16;
+  __device__ void pre8(int row, int col, RowPre& pr) const {
+    if (mode == 2) pr.u[0] = ldg16(res + (size_t)row * ldr + col);
+  }
+  __device__ void row8(int row, int col, const float (&v)[8], const RowPre& pr, float (&)[8], float (&)[8]) const {
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = v[j];
+    if (mode == 1) {
+      stg16(aux + (size_t)row * ldo + col, Chunk<T>::pack(o));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = gelu_erf(o[j]);
+    } else if (mode == 2) {
+      if (p > 0.f) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] *= drop_scale(seed, (uint64_t)row * N + col + j, p);
+      }
+      if (rscale) {
+        const float rs = rscale[row / rps];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] *= rs;
+      }
+      float r[8];
+      Chunk<T>::unpack(pr.u[0], r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] += r[j];
+    }
+    stg16(out + (size_t)row * ldo + col, Chunk<T>::pack(o));
+  }
 };
 
 // linear data-gradient epilogue: modes
@@ -68,6 +136,30 @@ struct EpiLinearBwd {
       v += load4(addend + (size_t)row * ldad + col);
     }
     store4(out + (size_t)row * ldo + col, v);
+  }
+  // bf16 GEMMs: row-chunk epilogue (see EpiLinear)
+  static constexpr bool kRow = true;
+  static constexpr int kPreDepth = 16;
+  __device__ void pre8(int row, int col, RowPre& p) const {
+    if (mode == 1) p.u[0] = ldg16(aux + (size_t)row * lda + col);
+    else if (addend) p.u[0] = ldg16(addend + (size_t)row * ldad + col);
+  }
+  __device__ void row8(int row, int col, const float (&v)[8], const RowPre& p, float (&)[8], float (&)[8]) const {
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = v[j];
+    if (mode == 1 || addend) {
+      float u[8];
+      Chunk<T>::unpack(p.u[0], u);
+      if (mode == 1) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] *= gelu_erf_grad(u[j]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] += u[j];
+      }
+    }
+    stg16(out + (size_t)row * ldo + col, Chunk<T>::pack(o));
   }
 };
 
@@ -99,6 +191,13 @@ static int gemm_lin(int M, int N, int K, int ksplit, const LA& la, const LB& lb,
       if constexpr (LA::kKContig == LB::kKContig) return gemm_big_auto(M, N, K, ksplit, la, lb, ep, st);
       // data gradients (K-contig dy x MN-contig W)
       else if (lin_pp >= 2) return launch_gemm_pp<256, 256, 2, 4>(M, N, K, ksplit, la, lb, ep, st);
+    }
+    // short-K token GEMMs (NesT levels 0 / 1: K = 96 / 192 over 0.5-2 M token rows)
+    // are HBM-bound: the LDS-DMA kernel with two K-tiles in flight instead of the
+    // one-tile ring (the loaders zero-fill the K tail)
+    if constexpr (LA::kKContig && LB::kKContig) {
+      if (VLP_LIN_SHORTK && gemm_variant() >= 5 && M >= 65536 && N >= 96)
+        return gemm_big_auto(M, N, K, ksplit, la, lb, ep, st);
     }
   }
   return gemm_wide<T>(M, N, K, ksplit, la, lb, ep, st);
@@ -775,6 +874,34 @@ VLP_EXPORT int vlp_linear_wgrad(int dtype, int M, int Nout, int Kin, const void*
   return launch_gemm<float, 128, 128, 2>(Nout, Kin, M, ksplit, la, lb, ep, st);
 }
 
+// split counts of vlp_linear_wgrad_ws before the workspace cap: the one-tile ring /
+// gemm_big_kernel paths (128 x 128 tiles, >= 256 token rows per split, ~512
+// workgroups) and the 256 x 256 ping-pong path (one round of 256, >= 2048 rows)
+static int linw_splits(int M, int Nout, int Kin) {
+  const int tiles = ((Nout + 127) / 128) * ((Kin + 127) / 128);
+  int ks = (512 + tiles - 1) / tiles;
+  const int maxsplit = (M + 255) / 256;
+  if (ks > maxsplit) ks = maxsplit;
+  return ks;
+}
+static int linw_splits_pp(int M, int Nout, int Kin) {
+  const int t256 = ((Nout + 255) / 256) * ((Kin + 255) / 256);
+  int k2 = (256 + t256 - 1) / t256;
+  if (k2 > M / 2048) k2 = M / 2048 > 0 ? M / 2048 : 1;
+  return k2;
+}
+static bool linw_use_pp(int M, int Nout, int Kin) {
+  return gemm_variant() >= 5 && Nout >= 256 && Kin >= 256 && M >= 16384 && M % 64 == 0;
+}
+// fp32 elements of the split-K workspace vlp_linear_wgrad_ws uses at its full split
+// count for this shape (a smaller workspace trims the splits)
+VLP_EXPORT int vlp_linear_wgrad_ws_floats(int M, int Nout, int Kin, long long* n) {
+  if (M < 1 || Nout < 1 || Kin < 1 || !n) return (int)hipErrorInvalidValue;
+  const int ks = linw_use_pp(M, Nout, Kin) ? linw_splits_pp(M, Nout, Kin) : linw_splits(M, Nout, Kin);
+  *n = (long long)(ks > 1 ? ks : 1) * Nout * Kin;
+  return 0;
+}
+
 // dW[Nout][Kin] += sum_m dy[m][n] x[m][k] through a split-K workspace
 // ws[ks][Nout][Kin] fp32 (ws_elems >= ks * Nout * Kin; Kin % 4 == 0)
 VLP_EXPORT int vlp_linear_wgrad_ws(int dtype, int M, int Nout, int Kin, const void* dy, int lddy,
@@ -785,11 +912,7 @@ VLP_EXPORT int vlp_linear_wgrad_ws(int dtype, int M, int Nout, int Kin, const vo
   // each split reduces >= VLP_LINW_WS_ROWS token rows: the text tower runs on a
   // side stream beside the image tower, where CU time per FLOP (prologue,
   // epilogue, slab traffic), not latency, is what the step pays for
-  constexpr int rows = 256;   // minimum token rows per split of the text weight gradients
-  const int tiles = ((Nout + 127) / 128) * ((Kin + 127) / 128);
-  int ks = (512 + tiles - 1) / tiles;
-  const int maxsplit = (M + rows - 1) / rows;
-  if (ks > maxsplit) ks = maxsplit;
+  int ks = linw_splits(M, Nout, Kin);   // >= 256 token rows per split
   while (ks > 1 && (long long)ks * Nout * Kin > ws_elems) --ks;
   int kc = (M + ks - 1) / ks;
   kc = (kc + 63) / 64 * 64;
@@ -797,16 +920,19 @@ VLP_EXPORT int vlp_linear_wgrad_ws(int dtype, int M, int Nout, int Kin, const vo
   MNMat<bf16> la{(const bf16*)dy, lddy, Nout, M};
   MNMat<bf16> lb{(const bf16*)x, ldx, Kin, M};
   EpiSplitStore ep{nullptr, nullptr, ws, Kin, (size_t)Nout * Kin};
-  constexpr int lin_pp = 1;   // weight gradients: the same-layout ping-pong tiles only (measured)
   int r;
-  if (lin_pp && gemm_variant() >= 5 && Nout >= 256 && Kin >= 256 && M >= 16384 && M % 64 == 0) {
+  if (linw_use_pp(M, Nout, Kin)) {
     // deep token reductions (NesT level 2) on the 256x256 ping-pong kernel: one
     // round of 256 workgroups, >= 2048 tokens per split, within the workspace
-    const int t256 = ((Nout + 255) / 256) * ((Kin + 255) / 256);
-    int k2 = (256 + t256 - 1) / t256;
-    if (k2 > M / 2048) k2 = M / 2048 > 0 ? M / 2048 : 1;
+    int k2 = linw_splits_pp(M, Nout, Kin);
     while (k2 > 1 && (long long)k2 * Nout * Kin > ws_elems) --k2;
     r = launch_gemm_pp<256, 256, 2, 4>(Nout, Kin, M, k2, la, lb, ep, st);
+    ks = last_ksplit();
+  } else if (VLP_LINW_BIG && M >= 65536) {
+    // deep token reductions with a short side (NesT levels 0 / 1: Nout or Kin = 96 / 192):
+    // two K-tiles in flight (gemm_big_kernel) instead of the one-tile ring
+    r = VLP_LINW_BIG == 2 && Kin >= 256 ? launch_gemm_big<128, 256, 2, 4>(Nout, Kin, M, ks, la, lb, ep, st)
+                                        : launch_gemm_big<128, 128, 2, 2>(Nout, Kin, M, ks, la, lb, ep, st);
     ks = last_ksplit();
   } else {
     r = launch_gemm_bk<128, 128, 2, 2>(Nout, Kin, M, ks, la, lb, ep, st);

@@ -188,6 +188,12 @@ template <class L> struct DirectTrait<L, std::void_t<decltype(L::kDirect)>> {
 };
 // row-chunk epilogues: per-channel coefficient arrays (E::kCoefs, E::coef(k))
 // and how many row chunks of operands to keep in flight (E::kPreDepth)
+// row-chunk epilogues that add a per-column bias (E::bias, may be null) to the raw
+// accumulators before they are staged as bf16 (one rounding of acc + bias)
+template <class E, class = void> struct StageBiasTrait { static constexpr bool value = false; };
+template <class E> struct StageBiasTrait<E, std::void_t<decltype(E::kStageBias)>> {
+  static constexpr bool value = E::kStageBias;
+};
 template <class E, class = void> struct CoefTrait { static constexpr int value = 0; };
 template <class E> struct CoefTrait<E, std::void_t<decltype(E::kCoefs)>> { static constexpr int value = E::kCoefs; };
 template <class E, class = void> struct PreDepthTrait { static constexpr int value = 8; };
@@ -625,12 +631,21 @@ __device__ __forceinline__ void ms_epilogue(const GemmShape& sh, const EP& ep, v
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const int coll = wn * WTN + b * 16 + 4 * lg;
+      v4f bb = v4f{0.f, 0.f, 0.f, 0.f};
+      if constexpr (StageBiasTrait<EP>::value) {
+        if (ep.bias != nullptr && col0 + coll < sh.N) bb = *reinterpret_cast<const v4f*>(ep.bias + col0 + coll);
+      }
 #pragma unroll
       for (int a = 0; a < MB; ++a) {
         const int rowl = wm * WTM + a * 16 + li;
         v4bf ob;
-        ob[0] = (bf16)acc[a][b][0]; ob[1] = (bf16)acc[a][b][1];
-        ob[2] = (bf16)acc[a][b][2]; ob[3] = (bf16)acc[a][b][3];
+        if constexpr (StageBiasTrait<EP>::value) {
+          ob[0] = (bf16)(acc[a][b][0] + bb[0]); ob[1] = (bf16)(acc[a][b][1] + bb[1]);
+          ob[2] = (bf16)(acc[a][b][2] + bb[2]); ob[3] = (bf16)(acc[a][b][3] + bb[3]);
+        } else {
+          ob[0] = (bf16)acc[a][b][0]; ob[1] = (bf16)acc[a][b][1];
+          ob[2] = (bf16)acc[a][b][2]; ob[3] = (bf16)acc[a][b][3];
+        }
         *reinterpret_cast<v4bf*>(stg + rowl * BN + (((coll >> 3) ^ (rowl & (CPR - 1))) << 3) + (coll & 4)) = ob;
       }
     }

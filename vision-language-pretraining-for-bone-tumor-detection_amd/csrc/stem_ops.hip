@@ -415,19 +415,39 @@ stem1_route_bwd_kernel(Stem1Geom g, const bf16* __restrict__ xs, const bf16* __r
 
 
 // ---------------------------------------------------------------- fused backward
-// The stem's whole backward in one pass: per pair of conv-output rows,
-//   1. the patch tile P [2 rows][Wo px][64 k] (bf16, from xs) is staged in LDS,
-//   2. y0 = W1 * P is recomputed on MFMA into the row tile Y [2][Wo][64],
-//   3. the pooled gradient is routed and dy = k*g + b*y0 + c written over Y,
-//   4. dW1[co][k] += sum_px dy[px][co] * P[px][k] on MFMA, both operands read
-//      transposed from LDS (ds_read_b64_tr_b16: lane i of a 16-lane group gets
-//      column i of 4 consecutive rows),
-// so neither y0 nor dy ever reaches HBM.  Each workgroup accumulates its
-// band's 64 x 64 weight gradient in registers (each wave a 32 x 32 quadrant
-// over every other k-step), sums the pairs in LDS and writes one fp32 slab [64][64];
-// vlp_stem1_wgrad_fold sums the slabs and replicates them over the 3 input
-// channels.  512 threads; LDS: W1 8 KB + P 2*Wo*128 + Y 2*Wo*128 + 1.25 KB.
-constexpr int kStemFusedPairs = 16;   // row pairs per workgroup
+// The stem's whole backward, y0 and dy never materialised.  With dy = k*g +
+// b*y0 + c (the folded BatchNorm backward, per-channel k, b, c) and y0 = W1 P
+// (P = the K = 64 patch of a conv-output pixel), the weight gradient is linear
+// in three batch sums:
+//   dW1[co][k] = k_co R[co][k] + b_co (W1 G)[co][k] + c_co S[k]
+//   R = sum_px g(px) P(px)^T   (g: the pooled gradient routed to its arg-max pixel)
+//   G = sum_px P(px) P(px)^T   (the 64 x 64 Gram matrix of the patches)
+//   S = sum_px P(px)
+// so the backward never recomputes y0 and never forms dy per pixel: it scatters
+// each pooled gradient once into a bf16 tile of routed gradients, and runs R, G
+// and S on MFMA over the patch tile (the y0 term is exact here -- W1 G in fp64 in
+// the fold -- where the per-pixel form rounds y0 and dy to bf16).
+//
+// Work split: a workgroup owns one image, a band of kGramBand pooled rows and a
+// column block of CW conv-output columns.  Iteration i (pooled row i):
+//   A. the patch tile P [2 rows][CW px][64 k] of conv rows 2i-1, 2i is stored
+//      (prefetched one iteration ahead in registers), and pooled row i's
+//      gradients are scattered into the routed-gradient ring: tap (dh, dw) of
+//      pooled (i, q) lands on conv pixel (2i-1+dh, 2q-1+dw) (ds_pk_add_bf16: the
+//      windows of q and q+1 share a column);
+//   B. conv rows 2i-1 and 2i are complete (no later pooled row reaches them):
+//      R += Gt^T P, G += P^T P, S += 1^T P on MFMA (operands read transposed from
+//      LDS, ds_read_b64_tr_b16), and the two ring rows the next iteration fills
+//      are cleared.
+// A band starting at i0 > 0 first scatters the dh = 2 taps of pooled row i0 - 1
+// (its row 2 i0 - 1); the last band also completes row Ho - 1.  Each workgroup
+// writes one fp32 slab [R | G | S]; vlp_stem1_bwd_fused's fold sums the slabs in
+// a fixed order (deterministic) and forms dW1.  512 threads; LDS 7 * CW * 128 B.
+constexpr int kGramBand = 32;                   // pooled rows per workgroup
+constexpr int kGramSlots = 5;                   // ring of conv-output rows (routed gradients)
+constexpr int kGramSlab = 64 * 64 * 2 + 64;     // R, G, S floats per workgroup
+constexpr int kGramGroups = 32;                 // first-level slab groups of the fold
+typedef __bf16 v2bf __attribute__((ext_vector_type(2)));
 
 // transposed fragment of a [px][64] tile (stile_off layout): lane (i, g) gets
 // column col0 + i of rows row0 + 8g .. +7 (the MFMA operand with k = px)
@@ -445,189 +465,257 @@ __device__ __forceinline__ v8bf tile_tr(const char* tile, int row0, int col0) {
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-template <int NA>
+template <int CW>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
-stem1_bwd_fused_kernel(Stem1Geom g, const bf16* __restrict__ xs, const bf16* __restrict__ wp1, int Hq, int Wq,
-                       const bf16* __restrict__ dp, const uint8_t* __restrict__ idx,
-                       const float* __restrict__ mean, const float* __restrict__ istd,
-                       const float* __restrict__ gamma, const double* __restrict__ sg,
-                       const double* __restrict__ sgx, float* __restrict__ slabs) {
+stem1_bwd_gram_kernel(Stem1Geom g, const bf16* __restrict__ xs, int Hq, int Wq, const bf16* __restrict__ dp,
+                      const uint8_t* __restrict__ idx, float* __restrict__ slabs) {
+  constexpr int RB = CW * 128;                          // bytes of one conv row in a [px][64] tile
+  constexpr int NP = 2 * CW * 8 / 512;                  // patch chunks per thread per iteration
+  constexpr int NQ = CW / 2 + 1;                        // pooled columns reaching the block
+  constexpr int NI = (NQ * 8 + 511) / 512;              // scatter items per thread
+  constexpr int KS = 2 * CW / 32;                       // 32-px k-steps per iteration
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int Ho = g.Ho, Wo = g.Wo;
-  const int tile_bytes = 2 * Wo * 128;                // two conv-output rows
-  char* wl = smem;
-  char* ptile = smem + 8192;
-  char* ytile = ptile + tile_bytes;
-  float* cl = reinterpret_cast<float*>(smem + 8192 + (2 * tile_bytes > 131072 ? 2 * tile_bytes : 131072));
-  const int HP = Ho / 2;
-  const int bands = (HP + kStemFusedPairs - 1) / kStemFusedPairs;
-  const int n = blockIdx.x / bands, band = blockIdx.x - n * bands;
-  const int a0 = band * kStemFusedPairs;
-  int a1 = a0 + kStemFusedPairs;
-  if (a1 > HP) a1 = HP;
+  char* ptile = smem;
+  char* gring = smem + 2 * RB;
+  const int Ho = g.Ho;
+  const int CB = g.Wo / CW;
+  const int bands = (Hq + kGramBand - 1) / kGramBand;
+  int bid = blockIdx.x;
+  const int cb = bid % CB;
+  bid /= CB;
+  const int band = bid % bands, n = bid / bands;
+  const int i0 = band * kGramBand;
+  const int i1 = i0 + kGramBand < Hq ? i0 + kGramBand : Hq;
+  const int iend = i1 == Hq ? Hq : i1 - 1;              // the last band also completes row Ho - 1
+  const int c0 = cb * CW, qlo = c0 / 2;
   const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
-  const int c = tid & 7;                               // routing: this thread's 8-channel chunk
-  const bf16* xn = xs + (size_t)n * g.Hp * g.Wp1;
+  const char* xb = reinterpret_cast<const char*>(xs + (size_t)n * g.Hp * g.Wp1);
   const bf16* dp_n = dp + (size_t)n * Hq * Wq * 64;
   const uint8_t* idx_n = idx + (size_t)n * Hq * Wq * 64;
-  const char* xb = reinterpret_cast<const char*>(xn);
 
-  // patch tile staging: item = (row r, pixel px, chunk kh) -> 16 B of xs
-  constexpr int NP = 2 * NA;                           // 2 rows * Wo * 8 chunks / 512 threads
+  // ---- patch staging: item (row r, pixel px, kh) -> 16 B of xs (zeros outside the conv rows)
   uint4 pf[NP];
-  auto p_load = [&](int pa) __attribute__((always_inline)) {
+  auto p_load = [&](int i) __attribute__((always_inline)) {
 #pragma unroll
     for (int it = 0; it < NP; ++it) {
       const int item = tid + 512 * it;
-      const int r = item / (Wo * 8), rem = item - r * Wo * 8;
+      const int r = item / (CW * 8), rem = item - r * (CW * 8);
       const int px = rem >> 3, kh = rem & 7;
-      const int sh = px & 3, ho = 2 * pa + r;
-      const unsigned e = (unsigned)sh * (unsigned)g.copy + (unsigned)(2 * ho + kh) * (unsigned)g.Wp1 +
-                         (unsigned)(2 * px - 2 * sh);
-      pf[it] = ldg16(xb + 2u * e);
+      const int rr = 2 * i - 1 + r, wo = c0 + px, sh = wo & 3;
+      if (rr >= 0 && rr < Ho) {
+        const unsigned e = (unsigned)sh * (unsigned)g.copy + (unsigned)(2 * rr + kh) * (unsigned)g.Wp1 +
+                           (unsigned)(2 * wo - 2 * sh);
+        pf[it] = ldg16(xb + 2u * e);
+      } else {
+        pf[it] = make_uint4(0u, 0u, 0u, 0u);
+      }
     }
   };
   auto p_store = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int it = 0; it < NP; ++it) {
       const int item = tid + 512 * it;
-      const int r = item / (Wo * 8), rem = item - r * Wo * 8;
-      *reinterpret_cast<uint4*>(ptile + r * (Wo * 128) + stile_off(rem >> 3, rem & 7)) = pf[it];
+      const int r = item / (CW * 8), rem = item - r * (CW * 8);
+      *reinterpret_cast<uint4*>(ptile + r * RB + stile_off(rem >> 3, rem & 7)) = pf[it];
     }
   };
-  p_load(a0);
-  stage_w(wp1, nullptr, wl);
-  if (tid < 64) {
-    const int co = tid;
-    const float inv_count = 1.f / (float)((double)g.N * Ho * Wo);
-    const float is = istd[co];
-    const float k = gamma[co] * is;
-    const float mg = (float)(sg[co] * (double)inv_count), mgx = (float)(sgx[co] * (double)inv_count);
-    cl[co] = k;
-    cl[64 + co] = -k * is * mgx;
-    cl[128 + co] = -k * mg + k * is * mgx * mean[co];
+  // ---- pooled-gradient items (column q = qlo + (item >> 3), chunk c = item & 7), prefetched
+  uint4 gv[NI];
+  uint2 tv[NI];
+  auto g_load = [&](int i) __attribute__((always_inline)) {
+#pragma unroll
+    for (int it = 0; it < NI; ++it) {
+      const int item = tid + 512 * it;
+      const int q = qlo + (item >> 3), c = item & 7;
+      if (item < NQ * 8 && q < Wq && i >= 0 && i < Hq) {
+        const unsigned po = ((unsigned)i * Wq + q) * 64 + 8 * c;
+        gv[it] = ldg16(dp_n + po);
+        tv[it] = *reinterpret_cast<const uint2*>(idx_n + po);
+      } else {
+        gv[it] = make_uint4(0u, 0u, 0u, 0u);
+        tv[it] = make_uint2(0xffffffffu, 0xffffffffu);   // tap 255: routes nowhere
+      }
+    }
+  };
+  // scatter pooled row i (taps with dh >= dhmin) into the ring
+  auto scatter = [&](int i, int dhmin) __attribute__((always_inline)) {
+    const int sbase = (2 * i) % kGramSlots;                 // slot of conv row 2i - 1 (+ dh)
+#pragma unroll
+    for (int it = 0; it < NI; ++it) {
+      const int item = tid + 512 * it;
+      const int q = qlo + (item >> 3), c = item & 7;
+      // LDS offsets of the pixel's chunk c for dw = 0, 1, 2 (local column 2q - 1 + dw - c0)
+      int off[3];
+      bool ok[3];
+#pragma unroll
+      for (int dw = 0; dw < 3; ++dw) {
+        const int px = 2 * q - 1 + dw - c0;
+        ok[dw] = px >= 0 && px < CW;
+        const int pc = ok[dw] ? px : 0;
+        off[dw] = stile_off(pc, c);
+      }
+      const uint32_t gw[4] = {gv[it].x, gv[it].y, gv[it].z, gv[it].w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t t = ((e < 4 ? tv[it].x : tv[it].y) >> (8 * (e & 3))) & 255u;
+        const uint32_t dh = (t * 11u) >> 5;                 // t / 3 for t <= 8
+        const uint32_t dw = t - 3u * dh;
+        const bool valid = t <= 8u && (int)dh >= dhmin && (dw == 0u ? ok[0] : dw == 1u ? ok[1] : ok[2]);
+        if (valid) {
+          int slot = sbase + (int)dh;
+          slot = slot >= kGramSlots ? slot - kGramSlots : slot;
+          const int o = dw == 0u ? off[0] : dw == 1u ? off[1] : off[2];
+          char* at = gring + slot * RB + o + (e & 6) * 2;
+          const uint32_t v = (e & 1) ? (gw[e >> 1] & 0xffff0000u) : (gw[e >> 1] & 0x0000ffffu);
+          __builtin_amdgcn_ds_atomic_fadd_v2bf16(
+              (__attribute__((address_space(3))) v2bf*)lds_addr_stem(at),
+              __builtin_bit_cast(v2bf, v));
+        }
+      }
+    }
+  };
+  auto zero_rows = [&](int slot_a, int slot_b) __attribute__((always_inline)) {
+    for (int q = tid; q < 2 * RB / 16; q += 512) {
+      const int slot = q < RB / 16 ? slot_a : slot_b;
+      const int o = (q < RB / 16 ? q : q - RB / 16) * 16;
+      *reinterpret_cast<uint4*>(gring + slot * RB + o) = make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+
+  // accumulators: wave (quadrant qd = wv & 3: rows 32a.., columns 32b..; k-step parity wv >> 2)
+  const int a = (wv >> 1) & 1, b = wv & 1, par = wv >> 2;
+  v4f accR[2][2], accG[2][2], accS[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    accS[j] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) accR[j][jj] = accG[j][jj] = v4f{0.f, 0.f, 0.f, 0.f};
   }
-  // dW1[co][k] split over the waves: wave wv owns the 32 x 32 quadrant (co half
-  // (wv >> 1) & 1, k half wv & 1) and every other 32-px k-step (parity wv >> 2)
-  const int qco = 32 * ((wv >> 1) & 1), qk = 32 * (wv & 1);
-  v4f dw[2][2];
+  v8bf ones;
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) dw[a][b] = v4f{0.f, 0.f, 0.f, 0.f};
-  // y0 recompute split: wave -> row (wv >> 2), columns 16*NA*(wv & 3) ..
-  const int yr = wv >> 2, yseg = 16 * NA * (wv & 3);
-  for (int pa = a0; pa < a1; ++pa) {
+  for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.f;
+
+  // ---- prologue
+  p_load(i0);
+  for (int q = tid; q < kGramSlots * RB / 16; q += 512)
+    *reinterpret_cast<uint4*>(gring + q * 16) = make_uint4(0u, 0u, 0u, 0u);
+  g_load(i0 - 1);
+  lds_barrier();
+  if (i0 > 0) scatter(i0 - 1, 2);                        // row 2 i0 - 1's dh = 2 taps
+  g_load(i0);
+  for (int i = i0; i <= iend; ++i) {
+    // ---- A: patches of rows 2i-1, 2i; scatter pooled row i
     p_store();
-    if (pa + 1 < a1) p_load(pa + 1);                   // the next pair's patches fly across this pair
+    if (i < iend) p_load(i + 1);
+    if (i < Hq) scatter(i, i == 0 ? 1 : 0);             // i = 0: row -1 does not exist
+    if (i < iend) g_load(i + 1);
     lds_barrier();
-    // ---- 2: y0 on MFMA (A = W1 from LDS, B = patch fragments from the P tile), one
-    //         16-px fragment at a time (16 accumulator registers live) ----
-    {
-      const char* prow = ptile + yr * (Wo * 128);
-      char* yrow = ytile + yr * (Wo * 128);
+    // ---- B: R, G, S over the two completed rows; clear the ring rows of 2i+2, 2i+3
 #pragma unroll 1
-      for (int a = 0; a < NA; ++a) {
-        const int px = yseg + 16 * a + (l & 15);
-        const v8bf p0 = *reinterpret_cast<const v8bf*>(prow + stile_off(px, l >> 4));
-        const v8bf p1 = *reinterpret_cast<const v8bf*>(prow + stile_off(px, 4 + (l >> 4)));
+    for (int ks = par; ks < KS; ks += 2) {
+      const int r = (32 * ks) / CW, px0 = 32 * ks - r * CW;
+      const char* gt = gring + ((2 * i + r) % kGramSlots) * RB;
+      const char* pt = ptile + r * RB;
+      v8bf fg[2], fp[2], fb[2];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const int co = 16 * b + (l & 15);
-          const v8bf w0 = *reinterpret_cast<const v8bf*>(wl + stile_off(co, l >> 4));
-          const v8bf w1 = *reinterpret_cast<const v8bf*>(wl + stile_off(co, 4 + (l >> 4)));
-          v4f t = v4f{0.f, 0.f, 0.f, 0.f};
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, p0, t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, p1, t, 0, 0, 0);
-          const int co0 = 16 * b + 4 * (l >> 4);
-          v4bf v;
-          v[0] = (bf16)t[0]; v[1] = (bf16)t[1]; v[2] = (bf16)t[2]; v[3] = (bf16)t[3];
-          *reinterpret_cast<v4bf*>(yrow + stile_off(px, co0 >> 3) + ((co0 >> 2) & 1) * 8) = v;
-        }
+      for (int j = 0; j < 2; ++j) {
+        fg[j] = tile_tr(gt, px0, 32 * a + 16 * j);
+        fp[j] = tile_tr(pt, px0, 32 * a + 16 * j);
+        fb[j] = tile_tr(pt, px0, 32 * b + 16 * j);
       }
-    }
-    lds_barrier();
-    // ---- 3: route the pooled gradient; dy = k*g + b*y0 + c over the Y tile ----
-    const bool v10 = pa + 1 < Hq;
-#pragma unroll 1
-    for (int item = tid; item < 4 * Wo; item += 512) {
-      const int q = item >> 3;                         // column pair 2q, 2q + 1 (chunk c = item & 7)
-      const bool v01 = q + 1 < Wq;
-      const int pa1 = v10 ? pa + 1 : pa, q1 = v01 ? q + 1 : q;
-      uint4 pv[4];
-      uint2 ib[4];
-#pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4) {
-        const int ho = (k4 >> 1) ? pa1 : pa, wo = (k4 & 1) ? q1 : q;
-        const unsigned po = ((unsigned)ho * Wq + wo) * 64 + 8 * c;
-        pv[k4] = ldg16(dp_n + po);
-        ib[k4] = *reinterpret_cast<const uint2*>(idx_n + po);
-      }
-      float ka[8], ba[8], ca[8];
-      ld8f_lds(cl + 8 * c, ka);
-      ld8f_lds(cl + 64 + 8 * c, ba);
-      ld8f_lds(cl + 128 + 8 * c, ca);
-      float f[4][8];
-#pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4) unpack8(pv[k4], f[k4]);
-      const bool v11 = v01 && v10;
-#pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4) {   // pixel (2pa + (k4 >> 1), 2q + (k4 & 1))
-        float yv[8], d[8];
-        const int px = 2 * q + (k4 & 1);
-        char* at = ytile + (k4 >> 1) * (Wo * 128) + stile_off(px, c);
-        unpack8(*reinterpret_cast<const uint4*>(at), yv);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          unsigned t[4];
-#pragma unroll
-          for (int m = 0; m < 4; ++m) t[m] = (((e >> 2) ? ib[m].y : ib[m].x) >> (8 * (e & 3))) & 255u;
-          float gsum;
-          if (k4 == 0) gsum = t[0] == 4u ? f[0][e] : 0.f;
-          else if (k4 == 1) gsum = (t[0] == 5u ? f[0][e] : 0.f) + ((v01 && t[1] == 3u) ? f[1][e] : 0.f);
-          else if (k4 == 2) gsum = (t[0] == 7u ? f[0][e] : 0.f) + ((v10 && t[2] == 1u) ? f[2][e] : 0.f);
-          else
-            gsum = (t[0] == 8u ? f[0][e] : 0.f) + ((v01 && t[1] == 6u) ? f[1][e] : 0.f) +
-                   ((v10 && t[2] == 2u) ? f[2][e] : 0.f) + ((v11 && t[3] == 0u) ? f[3][e] : 0.f);
-          d[e] = fmaf(ka[e], gsum, fmaf(ba[e], yv[e], ca[e]));
-        }
-        *reinterpret_cast<uint4*>(at) = Chunk<bf16>::pack(d);
-      }
-    }
-    lds_barrier();
-    // ---- 4: dW1 += dy^T P over this pair's 2*Wo pixels (k-steps of 32 px split over the waves) ----
-    for (int ks = wv >> 2; ks < Wo / 16; ks += 2) {
-      const int r = (32 * ks) / Wo, px0 = 32 * ks - r * Wo;
-      const char* yb = ytile + r * (Wo * 128);
-      const char* pb = ptile + r * (Wo * 128);
-      v8bf fa[2], fb[2];
-#pragma unroll
-      for (int a = 0; a < 2; ++a) fa[a] = tile_tr(yb, px0, qco + 16 * a);
-#pragma unroll
-      for (int b = 0; b < 2; ++b) fb[b] = tile_tr(pb, px0, qk + 16 * b);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the asm reads' results (hipcc does not track them)
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) dw[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[a], fb[b], dw[a][b], 0, 0, 0);
-    }
-    lds_barrier();                                     // P and Y are rewritten by the next pair
-  }
-  // ---- the two k-parity waves of each quadrant summed through LDS: one fp32 slab per workgroup ----
-  float* red = reinterpret_cast<float*>(ptile);        // [2 parities][64 co][64 k]
+        for (int jj = 0; jj < 2; ++jj) {
+          accR[j][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fg[j], fb[jj], accR[j][jj], 0, 0, 0);
+          accG[j][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fp[j], fb[jj], accG[j][jj], 0, 0, 0);
+        }
+      if (a == 0) {
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = qco + 16 * a + 4 * (l >> 4) + r, k = qk + 16 * b + (l & 15);
-        red[((wv >> 2) * 64 + co) * 64 + k] = dw[a][b][r];
+        for (int jj = 0; jj < 2; ++jj) accS[jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, fb[jj], accS[jj], 0, 0, 0);
       }
+    }
+    zero_rows((2 * i + 3) % kGramSlots, (2 * i + 4) % kGramSlots);
+    lds_barrier();
+  }
+  // ---- the two k-parity halves summed through LDS: one slab [R | G | S] per workgroup
+  float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    if (par == pass) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = 32 * a + 16 * j + 4 * (l >> 4) + r, k = 32 * b + 16 * jj + (l & 15);
+            float* pr = red + m * 64 + k;
+            float* pg = red + 4096 + m * 64 + k;
+            if (pass == 0) { *pr = accR[j][jj][r]; *pg = accG[j][jj][r]; }
+            else { *pr += accR[j][jj][r]; *pg += accG[j][jj][r]; }
+          }
+      if (a == 0 && l < 16) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          float* ps = red + 8192 + 32 * b + 16 * jj + l;
+          if (pass == 0) *ps = accS[jj][0];
+          else *ps += accS[jj][0];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* slab = slabs + (size_t)blockIdx.x * kGramSlab;
+  for (int e = tid; e < kGramSlab; e += 512) slab[e] = red[e];
+}
+
+// fold, level 1: part[grp][e] = sum of slabs grp, grp + G, ... (fixed order)
+__global__ void __launch_bounds__(256) stem1_gram_part_kernel(int ns, const float* __restrict__ slabs,
+                                                              float* __restrict__ part) {
+  const int e = blockIdx.x * 256 + threadIdx.x, grp = blockIdx.y;
+  if (e >= kGramSlab) return;
+  float acc0 = 0.f, acc1 = 0.f;
+  int s = grp;
+  for (; s + kGramGroups < ns; s += 2 * kGramGroups) {
+    acc0 += slabs[(size_t)s * kGramSlab + e];
+    acc1 += slabs[(size_t)(s + kGramGroups) * kGramSlab + e];
+  }
+  if (s < ns) acc0 += slabs[(size_t)s * kGramSlab + e];
+  part[(size_t)grp * kGramSlab + e] = acc0 + acc1;
+}
+// fold, level 2: tot[e] = sum over the groups in fp64 (fixed order)
+__global__ void __launch_bounds__(256) stem1_gram_tot_kernel(const float* __restrict__ part, double* __restrict__ tot) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= kGramSlab) return;
+  double s = 0.0;
+  for (int grp = 0; grp < kGramGroups; ++grp) s += (double)part[(size_t)grp * kGramSlab + e];
+  tot[e] = s;
+}
+// fold, level 3: dW1[co][k] = k R + b (W1 G) + c S in fp64, replicated over the 3
+// input channels ([64][3][7][7]).  One workgroup per co, one thread per k.
+__global__ void __launch_bounds__(64) stem1_gram_grad_kernel(const double* __restrict__ tot, const bf16* __restrict__ wp1,
+                                                             const float* __restrict__ mean, const float* __restrict__ istd,
+                                                             const float* __restrict__ gamma, const double* __restrict__ sg,
+                                                             const double* __restrict__ sgx, double inv_count,
+                                                             float* __restrict__ grad) {
+  __shared__ double w1[64];
+  const int co = blockIdx.x, k = threadIdx.x;
+  w1[k] = (double)(float)wp1[co * 64 + k];
   __syncthreads();
-  float* slab = slabs + (size_t)blockIdx.x * 4096;
-  for (int e = tid; e < 4096; e += 512) slab[e] = red[e] + red[4096 + e];
+  double wg = 0.0;
+  for (int k2 = 0; k2 < 64; ++k2) wg += w1[k2] * tot[4096 + k2 * 64 + k];
+  const double is = istd[co], kk = (double)gamma[co] * is;
+  const double mg = sg[co] * inv_count, mgx = sgx[co] * inv_count;
+  const double bco = -kk * is * mgx, cco = -kk * mg + kk * is * mgx * (double)mean[co];
+  const double v = kk * tot[co * 64 + k] + bco * wg + cco * tot[8192 + k];
+  const int kh = k >> 3, kw = k & 7;
+  if (kh < 7 && kw < 7) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) grad[((co * 3 + c) * 7 + kh) * 7 + kw] = (float)v;
+  }
 }
 
 }  // namespace vlp
@@ -694,41 +782,54 @@ VLP_EXPORT int vlp_stem1_route_bwd(const void* xs, const void* wp1, const void* 
   return (int)hipGetLastError();
 }
 
+static int stem1_gram_cw(int Wo) { return Wo % 128 == 0 ? 128 : 64; }
 static int stem1_bwd_fused_wgs(int N, int H, int W) {
   const Stem1Geom g = make_stem1(N, H, W);
-  return N * ((g.Ho / 2 + kStemFusedPairs - 1) / kStemFusedPairs);
+  const int Hq = g.Ho / 2;
+  return N * ((Hq + kGramBand - 1) / kGramBand) * (g.Wo / stem1_gram_cw(g.Wo));
 }
-// Number of fp32 [64][64] slabs vlp_stem1_bwd_fused writes (one per workgroup).
-VLP_EXPORT int vlp_stem1_bwd_fused_slabs(int N, int H, int W, int* nslabs) {
-  *nslabs = stem1_bwd_fused_wgs(N, H, W);
+// fp32 workspace of vlp_stem1_bwd_fused: one [R | G | S] slab per workgroup + the fold's partials
+VLP_EXPORT int vlp_stem1_bwd_fused_ws_floats(int N, int H, int W, long long* n) {
+  if (!n || N < 1) return (int)hipErrorInvalidValue;
+  *n = ((long long)stem1_bwd_fused_wgs(N, H, W) + kGramGroups + 2) * kGramSlab;
   return 0;
 }
 
-// The whole stem backward (route + BN backward + weight gradient), y0 and dy
-// never materialised: slabs [vlp_stem1_bwd_fused_slabs][64][64] -> vlp_stem1_wgrad_fold.
+// The whole stem backward (routing + BN backward + weight gradient), y0 and dy never
+// materialised: grad [64][3][7][7] (overwritten).  ws >= vlp_stem1_bwd_fused_ws_floats.
 VLP_EXPORT int vlp_stem1_bwd_fused(const void* xs, const void* wp1, const void* dp, const uint8_t* idx,
                                    const float* mean, const float* istd, const float* gamma, const double* sum_g,
-                                   const double* sum_gx, float* slabs, long long slab_floats, int N, int H, int W,
-                                   void* stream) {
-  if (!vlp_stem1_fused_ok(H, W) || N < 1) return (int)hipErrorInvalidValue;
+                                   const double* sum_gx, float* ws, long long ws_floats, float* grad, int N, int H,
+                                   int W, void* stream) {
+  if (!vlp_stem1_fused_ok(H, W) || N < 1 || !ws || !grad) return (int)hipErrorInvalidValue;
   const Stem1Geom g = make_stem1(N, H, W);
   if (!stem1_offsets_fit(g)) return (int)hipErrorInvalidValue;
   const int nwg = stem1_bwd_fused_wgs(N, H, W);
-  if ((long long)nwg * 4096 > slab_floats) return (int)hipErrorInvalidValue;
-  const int Hq = (g.Ho + 2 - 3) / 2 + 1, Wq = (g.Wo + 2 - 3) / 2 + 1;
-  // the P and Y tiles (4 * Wo * 128 B), at least the 8 x 16 KB of the final cross-wave sum
-  const size_t tiles = 4 * (size_t)g.Wo * 128 > 131072 ? 4 * (size_t)g.Wo * 128 : 131072;
-  const size_t lds = 8192 + tiles + 3 * 64 * sizeof(float);
+  if (((long long)nwg + kGramGroups + 2) * kGramSlab > ws_floats) return (int)hipErrorInvalidValue;
+  const int Hq = g.Ho / 2, Wq = g.Wo / 2;
   hipStream_t st = (hipStream_t)stream;
-  VLP_STEM_NA_SWITCH(g.Wo / 64, {
+  float* part = ws + (size_t)nwg * kGramSlab;
+  const int cw = stem1_gram_cw(g.Wo);
+  if (cw == 128) {
+    constexpr size_t lds = 7 * 128 * 128;
     static bool attr = false;
     if (!attr) {
-      (void)hipFuncSetAttribute((const void*)&stem1_bwd_fused_kernel<NAC>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 8192 + 4 * 256 * 128 + 3 * 64 * 4);
+      (void)hipFuncSetAttribute((const void*)&stem1_bwd_gram_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds);
       attr = true;
     }
-    hipLaunchKernelGGL(stem1_bwd_fused_kernel<NAC>, dim3(nwg), dim3(512), lds, st, g, (const bf16*)xs,
-                       (const bf16*)wp1, Hq, Wq, (const bf16*)dp, idx, mean, istd, gamma, sum_g, sum_gx, slabs);
-  });
+    hipLaunchKernelGGL(stem1_bwd_gram_kernel<128>, dim3(nwg), dim3(512), lds, st, g, (const bf16*)xs, Hq, Wq,
+                       (const bf16*)dp, idx, ws);
+  } else {
+    constexpr size_t lds = 7 * 64 * 128;
+    hipLaunchKernelGGL(stem1_bwd_gram_kernel<64>, dim3(nwg), dim3(512), lds, st, g, (const bf16*)xs, Hq, Wq,
+                       (const bf16*)dp, idx, ws);
+  }
+  hipLaunchKernelGGL(stem1_gram_part_kernel, dim3((kGramSlab + 255) / 256, kGramGroups), dim3(256), 0, st, nwg,
+                     (const float*)ws, part);
+  double* tot = reinterpret_cast<double*>(part + (size_t)kGramGroups * kGramSlab);   // 8-B aligned: slabs are even
+  hipLaunchKernelGGL(stem1_gram_tot_kernel, dim3((kGramSlab + 255) / 256), dim3(256), 0, st, (const float*)part, tot);
+  hipLaunchKernelGGL(stem1_gram_grad_kernel, dim3(64), dim3(64), 0, st, (const double*)tot, (const bf16*)wp1, mean,
+                     istd, gamma, sum_g, sum_gx, 1.0 / ((double)N * g.Ho * g.Wo), grad);
   return (int)hipGetLastError();
 }

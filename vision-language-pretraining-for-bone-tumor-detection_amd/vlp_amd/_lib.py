@@ -63,6 +63,11 @@ _FAMILY_TIMED = {"vlp_conv_fwd", "vlp_conv_dgrad", "vlp_conv_dgrad_relu", "vlp_c
                  "vlp_nest_attn_fwd", "vlp_nest_attn_bwd"}
 
 
+# host-side queries (no GPU work): never timed
+_QUERIES = {"vlp_linear_wgrad_ws_floats", "vlp_clip_loss_ws_floats", "vlp_stem1_bwd_fused_ws_floats",
+            "vlp_stem1_fused_ok"}
+
+
 class HipError(RuntimeError):
     pass
 
@@ -96,7 +101,7 @@ class _Lib:
             return fn
 
         from . import ktimer
-        timed_here = name not in _FAMILY_TIMED
+        timed_here = name not in _FAMILY_TIMED and name not in _QUERIES
 
         def call(*args):
             tk = ktimer.begin(name[4:]) if timed_here and ktimer._ENABLED else None

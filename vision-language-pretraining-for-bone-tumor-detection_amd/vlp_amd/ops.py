@@ -222,17 +222,17 @@ def stem1_route_bwd(xs, wp1, dp, idx, sc, sh, mean, istd, gamma, sum_g, sum_gx, 
 
 def stem1_bwd_fused_into(xs, wp1, dp, idx, mean, istd, gamma, sum_g, sum_gx, N, H, W, grad):
     """grad[64][3][7][7] = the stem weight gradient from the pooled gradient dp
-    (ReLU-masked): routing, BN backward and the weight-gradient GEMM in one pass
-    (y0 and dy never written), per-workgroup slabs folded by vlp_stem1_wgrad_fold."""
+    (ReLU-masked): routing, BN backward and the weight gradient in one pass
+    through the batch sums R = sum g P^T, G = sum P P^T, S = sum P (y0 and dy
+    never formed); per-workgroup slabs folded in a fixed order."""
     import ctypes
-    ns = ctypes.c_int(0)
-    lib().vlp_stem1_bwd_fused_slabs(N, H, W, ctypes.addressof(ns))
-    ws = wgrad_ws(dp.device)
-    tk = ktimer.begin("stem_bwd_fused", 4.0 * N * (H // 2) * (W // 2) * 64 * 64)
+    n = ctypes.c_longlong(0)
+    lib().vlp_stem1_bwd_fused_ws_floats(N, H, W, ctypes.byref(n))
+    ws = _stream_ws("wgrad", dp.device, max(n.value, WGRAD_WS_FLOATS))
+    tk = ktimer.begin("stem_bwd_fused", 6.0 * N * (H // 2) * (W // 2) * 64 * 64)
     lib().vlp_stem1_bwd_fused(ptr(xs), ptr(wp1), ptr(dp), ptr(idx), ptr(mean), ptr(istd), ptr(gamma), ptr(sum_g),
-                              ptr(sum_gx), ptr(ws), ws.numel(), N, H, W, _s())
+                              ptr(sum_gx), ptr(ws), ws.numel(), ptr(grad), N, H, W, _s())
     ktimer.end(tk)
-    lib().vlp_stem1_wgrad_fold(ns.value, ptr(ws), ptr(grad), _s())
     return grad
 
 
@@ -379,7 +379,10 @@ def linear_wgrad(dy, x, dw, M, Nout, Kin, lddy=None, ldx=None):
     workspace folded by one reduction pass; fp32: atomic split-K."""
     tk = ktimer.begin("linear_wgrad/wide", 2.0 * M * Nout * Kin)
     if dy.dtype == torch.bfloat16 and Kin % 4 == 0:
-        ws = _linw_ws(dy.device, 16 * Nout * Kin)
+        import ctypes
+        n = ctypes.c_longlong(0)
+        lib().vlp_linear_wgrad_ws_floats(M, Nout, Kin, ctypes.byref(n))
+        ws = _linw_ws(dy.device, max(n.value, 16 * Nout * Kin))
         lib().vlp_linear_wgrad_ws(dcode(dy), M, Nout, Kin, ptr(dy), lddy or Nout, ptr(x), ldx or Kin,
                                   ptr(dw), ptr(ws), ws.numel(), _s())
     else:
