@@ -54,6 +54,19 @@ _USE_STEM1 = os.environ.get("VLP_STEM1", "1") != "0"
 # bf16: stem conv + BN sums + max-pool fused (stem_ops.hip); False keeps the
 # conv -> y0 -> max-pool kernels (tests compare the two)
 _USE_STEM_FUSED = True
+# bf16 training forward as two image halves on two streams (_run_blocks_split):
+# each half's BN/ReLU passes run beside the other half's convolutions.  The
+# side stream is the weight-gradient stream (idle during the forward), so the
+# process stays within the box's 4 hardware queues (main, text, side, copy).
+_SPLIT_FWD = True
+_SPLIT_LAYERS = (1, 2, 3, 4)
+
+
+def _side_stream(dev):
+    s = _WG_STREAMS.get(dev)
+    if s is None:
+        s = _WG_STREAMS[dev] = torch.cuda.Stream(device=dev)
+    return s
 
 
 STAGES = ("stem", "layer1", "layer2", "layer3", "layer4")
@@ -362,35 +375,130 @@ class ResNet34Tower(ArenaModule):
         return self._run_blocks(ws, T, dev, N, p, pm, saved, training)
 
     def _run_blocks(self, ws, T, dev, N, p, pm, saved, training):
+        if (_SPLIT_FWD and training and T == torch.bfloat16 and dev.type == "cuda" and N % 2 == 0
+                and N >= 2):
+            return self._run_blocks_split(ws, T, dev, N, p, pm, saved)
         bits = training and T == torch.bfloat16
         xmask = pm
         xcur = p
         blocks = []
         for pre, has_ds in self._blocks:
+            blk, xcur, xmask = self._block_fwd(ws, T, dev, pre, has_ds, xcur, xmask, training, bits)
+            blocks.append(blk)
+        feat = torch.empty(N, 512, dtype=T, device=dev)
+        ops.avgpool_fwd(xcur, feat)
+        saved["blocks"] = blocks
+        return feat, saved
+
+    def _block_fwd(self, ws, T, dev, pre, has_ds, xcur, xmask, training, bits):
+        """One BasicBlock forward on the current stream -> (saved dict, out, ReLU bits)."""
+        c1, c2 = self._convs[pre + ".conv1"], self._convs[pre + ".conv2"]
+        s, ss = self._fstat(ws, pre + ".bn1", full=True)
+        y1 = ops.conv_fwd(xcur, ws[c1.key + ".wp"], c1.Co, 3, 3, c1.S, 1, stat_sum=s, stat_sumsq=ss,
+                          stat_rep=STAT_REP)
+        Mb = y1.numel() // y1.shape[-1]
+        sc1, sh1 = self._bn_finalize(ws, pre + ".bn1", Mb, training)
+        a1 = torch.empty_like(y1)    # relu(bn1(y1)), materialised once: conv2 fwd + wgrad stream it
+        ops.bn_add_relu(y1, sc1, sh1, None, None, None, a1)
+        s, ss = self._fstat(ws, pre + ".bn2", full=True)
+        y2 = ops.conv_fwd(a1, ws[c2.key + ".wp"], c2.Co, 3, 3, 1, 1, stat_sum=s, stat_sumsq=ss,
+                          stat_rep=STAT_REP)
+        sc2, sh2 = self._bn_finalize(ws, pre + ".bn2", Mb, training)
+        yd = scd = shd = None
+        if has_ds:
+            cd = self._convs[pre + ".downsample.0"]
+            s, ss = self._fstat(ws, pre + ".downsample.1", full=True)
+            yd = ops.conv_fwd(xcur, ws[cd.key + ".wp"], cd.Co, 1, 1, cd.S, 0, stat_sum=s,
+                              stat_sumsq=ss, stat_rep=STAT_REP)
+            scd, shd = self._bn_finalize(ws, pre + ".downsample.1", Mb, training)
+        out = torch.empty_like(y2)
+        om = torch.empty(out.numel() // 8, dtype=torch.uint8, device=dev) if bits else None
+        ops.bn_add_relu(y2, sc2, sh2, yd if has_ds else xcur, scd, shd, out, relu_mask=om)
+        blk = {"x": xcur, "xmask": xmask, "y1": y1, "a1": a1, "y2": y2, "yd": yd, "out": out}
+        return blk, out, om
+
+    def _run_blocks_split(self, ws, T, dev, N, p, pm, saved):
+        """Training forward with the batch as two image halves: half A on the
+        current stream, half B on a side stream, one pass behind.
+
+        Train-mode BN needs the whole batch's statistics before any element can
+        be normalised, so every BN/ReLU pass (HBM-bound, copy rate) sits between
+        two convolutions (MFMA-bound).  Per statistics barrier:
+            A: pass(A) -> conv(A)
+            B:            pass(B) -> conv(B)      (pass(B) starts after pass(A))
+        so pass(B) runs beside conv(A) and only pass(A) is exposed.  Both halves
+        accumulate into the same fp64 statistic replicas; the finalize runs once
+        on the current stream after joining the side stream.  Results equal the
+        unsplit forward up to the order of the fp64 atomic adds."""
+        main = torch.cuda.current_stream(dev)
+        side = _side_stream(dev)
+        h = N // 2
+        xcur, xmask = p, pm
+        blocks = []
+        b_on_side = False      # xcur's B half was produced on the side stream
+        for pre, has_ds in self._blocks:
             c1, c2 = self._convs[pre + ".conv1"], self._convs[pre + ".conv2"]
-            s, ss = self._fstat(ws, pre + ".bn1", full=True)
-            y1 = ops.conv_fwd(xcur, ws[c1.key + ".wp"], c1.Co, 3, 3, c1.S, 1, stat_sum=s, stat_sumsq=ss,
-                              stat_rep=STAT_REP)
-            Mb = y1.numel() // y1.shape[-1]
-            sc1, sh1 = self._bn_finalize(ws, pre + ".bn1", Mb, training)
-            a1 = torch.empty_like(y1)    # relu(bn1(y1)), materialised once: conv2 fwd + wgrad stream it
-            ops.bn_add_relu(y1, sc1, sh1, None, None, None, a1)
-            s, ss = self._fstat(ws, pre + ".bn2", full=True)
-            y2 = ops.conv_fwd(a1, ws[c2.key + ".wp"], c2.Co, 3, 3, 1, 1, stat_sum=s, stat_sumsq=ss,
-                              stat_rep=STAT_REP)
-            sc2, sh2 = self._bn_finalize(ws, pre + ".bn2", Mb, training)
-            yd = scd = shd = None
+            if int(pre[5]) not in _SPLIT_LAYERS:
+                if b_on_side:
+                    main.wait_stream(side)
+                    b_on_side = False
+                blk, xcur, xmask = self._block_fwd(ws, T, dev, pre, has_ds, xcur, xmask, True, True)
+                blocks.append(blk)
+                continue
+            if not b_on_side:
+                side.wait_stream(main)
+            N_, Hi, Wi, _ = xcur.shape
+            Ho, Wo = ops.conv_out_hw(Hi, Wi, 3, 3, c1.S, 1)
+            y1 = torch.empty(N, Ho, Wo, c1.Co, dtype=T, device=dev)
+            a1, y2, out = torch.empty_like(y1), torch.empty_like(y1), torch.empty_like(y1)
+            yd = torch.empty_like(y1) if has_ds else None
+            om = torch.empty(out.numel() // 8, dtype=torch.uint8, device=dev)
+            oh = om.numel() // 2
+            Mb = N * Ho * Wo
+            k1, k2, kd = pre + ".bn1", pre + ".bn2", pre + ".downsample.1"
+            s1, ss1 = self._fstat(ws, k1, full=True)
+            s2, ss2 = self._fstat(ws, k2, full=True)
+            sd = ssd = None
             if has_ds:
                 cd = self._convs[pre + ".downsample.0"]
-                s, ss = self._fstat(ws, pre + ".downsample.1", full=True)
-                yd = ops.conv_fwd(xcur, ws[cd.key + ".wp"], cd.Co, 1, 1, cd.S, 0, stat_sum=s,
-                                  stat_sumsq=ss, stat_rep=STAT_REP)
-                scd, shd = self._bn_finalize(ws, pre + ".downsample.1", Mb, training)
-            out = torch.empty_like(y2)
-            om = torch.empty(out.numel() // 8, dtype=torch.uint8, device=dev) if bits else None
-            ops.bn_add_relu(y2, sc2, sh2, yd if has_ds else xcur, scd, shd, out, relu_mask=om)
+                sd, ssd = self._fstat(ws, kd, full=True)
+
+            def conv1(lo, hi):
+                ops.conv_fwd(xcur[lo:hi], ws[c1.key + ".wp"], c1.Co, 3, 3, c1.S, 1, stat_sum=s1,
+                             stat_sumsq=ss1, out=y1[lo:hi], stat_rep=STAT_REP)
+
+            def pass1_conv2(lo, hi):
+                ops.bn_add_relu(y1[lo:hi], sc1, sh1, None, None, None, a1[lo:hi])
+                ops.conv_fwd(a1[lo:hi], ws[c2.key + ".wp"], c2.Co, 3, 3, 1, 1, stat_sum=s2, stat_sumsq=ss2,
+                             out=y2[lo:hi], stat_rep=STAT_REP)
+                if has_ds:
+                    ops.conv_fwd(xcur[lo:hi], ws[cd.key + ".wp"], cd.Co, 1, 1, cd.S, 0, stat_sum=sd,
+                                 stat_sumsq=ssd, out=yd[lo:hi], stat_rep=STAT_REP)
+
+            conv1(0, h)
+            with torch.cuda.stream(side):
+                conv1(h, N)
+            main.wait_stream(side)
+            sc1, sh1 = self._bn_finalize(ws, k1, Mb, True)
+            pass1_conv2(0, h)
+            side.wait_stream(main)           # finalize + pass(A) queued before pass(B)
+            with torch.cuda.stream(side):
+                pass1_conv2(h, N)
+            main.wait_stream(side)
+            sc2, sh2 = self._bn_finalize(ws, k2, Mb, True)
+            scd = shd = None
+            if has_ds:
+                scd, shd = self._bn_finalize(ws, kd, Mb, True)
+            idt = yd if has_ds else xcur
+            ops.bn_add_relu(y2[:h], sc2, sh2, idt[:h], scd, shd, out[:h], relu_mask=om[:oh])
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                ops.bn_add_relu(y2[h:], sc2, sh2, idt[h:], scd, shd, out[h:], relu_mask=om[oh:])
+            b_on_side = True
             blocks.append({"x": xcur, "xmask": xmask, "y1": y1, "a1": a1, "y2": y2, "yd": yd, "out": out})
             xcur, xmask = out, om
+        if b_on_side:
+            main.wait_stream(side)
         feat = torch.empty(N, 512, dtype=T, device=dev)
         ops.avgpool_fwd(xcur, feat)
         saved["blocks"] = blocks
