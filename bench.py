@@ -72,6 +72,8 @@ def parse():
                     help="steps timed with the batch copied from pinned host memory (0: skip)")
     ap.add_argument("--split-fwd", type=int, default=1, choices=[0, 1],
                     help="ResNet34 training forward as two image halves on two streams (BN passes beside convs)")
+    ap.add_argument("--split-bwd", type=int, default=0, choices=[0, 1],
+                    help="ResNet34 backward BN passes / data gradients in two image halves on two streams")
     ap.add_argument("--wgrad-stream", type=int, default=1, choices=[0, 1],
                     help="ResNet34 weight gradients on a side stream beside the data-gradient chain (default 1)")
     ap.add_argument("--roofline-steps", type=int, default=5,
@@ -302,6 +304,10 @@ def mfma_peak_measured(dev):
     return round(best, 1)
 
 
+def rank_of():
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
 def pcie_inclusive(args, model, opt, world, dev):
     """The SURVEY §8(d) step including the batch's H2D copy: the batch starts in
     pinned host memory each step (as the reference's pin_memory DataLoader
@@ -359,6 +365,36 @@ def pcie_inclusive(args, model, opt, world, dev):
         el = el.item()
         out[form + "_prefetched"] = {"value": round(world * args.batch * args.pcie_steps / el, 2),
                                      "ms_per_step": round(el / args.pcie_steps * 1e3, 3)}
+    # the training loop's default (disable_augmentations=False): the uint8 upload
+    # through the reference's augmentations on the device (PretrainDataModule.
+    # device_augment -> vlp_aug_warp), which hands the step the fp32 3-channel
+    # batch (independent per-channel noise), i.e. the 3-channel stem path
+    from vlp_amd.augment import Augmenter
+    aug = Augmenter(seed=7 + rank_of())
+    host = {"x-ray-u8": b["x-ray-u8"].pin_memory(), "caption_tokenized": caps, "label": b["label"],
+            "caption": b["caption"]}
+
+    def steps_augmented(n):
+        for dbatch in DevicePrefetcher((host for _ in range(n)), dev):
+            xb = aug(dbatch["x-ray-u8"], channels=3, mean=127.5, std=73.9)
+            opt.zero_grad()
+            loss = model.training_step({"x-ray": xb, "caption_tokenized": dbatch["caption_tokenized"],
+                                        "label": dbatch["label"]})
+            loss.backward()
+            opt.step()
+    steps_augmented(2)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    steps_augmented(args.pcie_steps)
+    torch.cuda.synchronize()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    el = el.item()
+    out["u8_1ch_augmented_prefetched"] = {"value": round(world * args.batch * args.pcie_steps / el, 2),
+                                          "ms_per_step": round(el / args.pcie_steps * 1e3, 3)}
     out["unit"] = "image-text pairs/s"
     out["steps"] = args.pcie_steps
     return out
@@ -422,6 +458,7 @@ def main():
         if resnet:
             _r34._USE_WG_STREAM = bool(on) and args.wgrad_stream
             _r34._SPLIT_FWD = bool(on) and args.split_fwd
+            _r34._SPLIT_BWD = bool(on) and args.split_bwd
     set_wgrad_stream(True)
 
     for _ in range(args.warmup):

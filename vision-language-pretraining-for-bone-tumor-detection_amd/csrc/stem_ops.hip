@@ -433,8 +433,9 @@ stem1_route_bwd_kernel(Stem1Geom g, const bf16* __restrict__ xs, const bf16* __r
 //   A. the patch tile P [2 rows][CW px][64 k] of conv rows 2i-1, 2i is stored
 //      (prefetched one iteration ahead in registers), and pooled row i's
 //      gradients are scattered into the routed-gradient ring: tap (dh, dw) of
-//      pooled (i, q) lands on conv pixel (2i-1+dh, 2q-1+dw) (ds_pk_add_bf16: the
-//      windows of q and q+1 share a column);
+//      pooled (i, q) lands on conv pixel (2i-1+dh, 2q-1+dw) (ds_pk_add_bf16; the
+//      windows of q and q+1 share a column, so even and odd q scatter in two
+//      passes: a fixed summation order, bit-identical runs);
 //   B. conv rows 2i-1 and 2i are complete (no later pooled row reaches them):
 //      R += Gt^T P, G += P^T P, S += 1^T P on MFMA (operands read transposed from
 //      LDS, ds_read_b64_tr_b16), and the two ring rows the next iteration fills
@@ -537,13 +538,18 @@ stem1_bwd_gram_kernel(Stem1Geom g, const bf16* __restrict__ xs, int Hq, int Wq, 
       }
     }
   };
-  // scatter pooled row i (taps with dh >= dhmin) into the ring
-  auto scatter = [&](int i, int dhmin) __attribute__((always_inline)) {
+  // scatter the pooled columns q of parity qpar of pooled row i (taps with dh >=
+  // dhmin) into the ring.  Windows q and q + 1 share conv column 2q + 1, so the
+  // two parities run in separate passes (a barrier apart): every routed-gradient
+  // sum then forms in a fixed order (row 2i - 1's earlier-row part, then the even,
+  // then the odd column's window) and the bf16 result is the same on every run.
+  auto scatter_par = [&](int i, int dhmin, int qpar) __attribute__((always_inline)) {
     const int sbase = (2 * i) % kGramSlots;                 // slot of conv row 2i - 1 (+ dh)
 #pragma unroll
     for (int it = 0; it < NI; ++it) {
       const int item = tid + 512 * it;
       const int q = qlo + (item >> 3), c = item & 7;
+      if ((q & 1) != qpar) continue;
       // LDS offsets of the pixel's chunk c for dw = 0, 1, 2 (local column 2q - 1 + dw - c0)
       int off[3];
       bool ok[3];
@@ -573,6 +579,11 @@ stem1_bwd_gram_kernel(Stem1Geom g, const bf16* __restrict__ xs, int Hq, int Wq, 
         }
       }
     }
+  };
+  auto scatter = [&](int i, int dhmin) __attribute__((always_inline)) {
+    scatter_par(i, dhmin, 0);
+    lds_barrier();
+    scatter_par(i, dhmin, 1);
   };
   auto zero_rows = [&](int slot_a, int slot_b) __attribute__((always_inline)) {
     for (int q = tid; q < 2 * RB / 16; q += 512) {

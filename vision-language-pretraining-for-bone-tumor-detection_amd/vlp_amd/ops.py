@@ -76,12 +76,12 @@ def conv_dgrad(dy, wt, H, W, C, KH, KW, S, P, addend=None, y_bn=None, bn=None, s
 
 
 def conv_dgrad_relu(dy, wt, H, W, C, KH, KW, S, P, relu_out, y, mean, invstd, stat1, stat2,
-                    addend=None, stat_rep=1):
+                    addend=None, stat_rep=1, out=None):
     """g = (dgrad(dy) + addend) * (relu_out > 0), plus the BN backward sums of g
     against y (the next block's bn2 input).  relu_out may be the activation or
     its uint8 sign-bit mask (bn_add_relu / maxpool_fwd relu_mask)."""
     N, Ho, Wo, Co = dy.shape
-    g = torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
+    g = out if out is not None else torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
     bits = relu_out.dtype == torch.uint8
     tk = ktimer.begin(f"conv_dgrad[relu]{_tile_auto(C)}", 2.0 * N * Ho * Wo * Co * C * KH * KW)
     lib().vlp_conv_dgrad_relu(dcode(dy), ptr(dy), ptr(wt), ptr(g), N, H, W, C, Co, KH, KW, S, P,
