@@ -70,10 +70,6 @@ def parse():
     ap.add_argument("--kernel-report", default="")
     ap.add_argument("--pcie-steps", type=int, default=5,
                     help="steps timed with the batch copied from pinned host memory (0: skip)")
-    ap.add_argument("--split-fwd", type=int, default=1, choices=[0, 1],
-                    help="ResNet34 training forward as two image halves on two streams (BN passes beside convs)")
-    ap.add_argument("--split-bwd", type=int, default=0, choices=[0, 1],
-                    help="ResNet34 backward BN passes / data gradients in two image halves on two streams")
     ap.add_argument("--wgrad-stream", type=int, default=1, choices=[0, 1],
                     help="ResNet34 weight gradients on a side stream beside the data-gradient chain (default 1)")
     ap.add_argument("--roofline-steps", type=int, default=5,
@@ -457,8 +453,6 @@ def main():
     def set_wgrad_stream(on):
         if resnet:
             _r34._USE_WG_STREAM = bool(on) and args.wgrad_stream
-            _r34._SPLIT_FWD = bool(on) and args.split_fwd
-            _r34._SPLIT_BWD = bool(on) and args.split_bwd
     set_wgrad_stream(True)
 
     for _ in range(args.warmup):

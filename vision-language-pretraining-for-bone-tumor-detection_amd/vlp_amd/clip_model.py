@@ -195,10 +195,7 @@ class ClipStepFn(torch.autograd.Function):
                 txt_t.run_backward(sv_txt, dcls)
                 reducer.reduce([txt_t.arena])
             reducer.reduce([head.arena])
-            # the split image backward queues its weight gradients behind the text
-            # backward on the text stream (three compute streams in all)
-            kw = {"wg_stream": s_txt} if hasattr(img_t, "_stem_backward") else {}
-            img_t.run_backward(sv_img, dfeat_img, on_stage_done=on_stage, **kw)
+            img_t.run_backward(sv_img, dfeat_img, on_stage_done=on_stage)
             main.wait_stream(s_txt)
         else:
             txt_t.run_backward(sv_txt, dcls)

@@ -54,30 +54,12 @@ _USE_STEM1 = os.environ.get("VLP_STEM1", "1") != "0"
 # bf16: stem conv + BN sums + max-pool fused (stem_ops.hip); False keeps the
 # conv -> y0 -> max-pool kernels (tests compare the two)
 _USE_STEM_FUSED = True
-# training forward as two image halves on two streams (_run_blocks_split):
-# each half's BN/ReLU passes run beside the other half's convolutions.  The
-# side stream is the weight-gradient stream (idle during the forward), so the
-# process stays within the box's 4 hardware queues (main, text, side, copy).
-_SPLIT_FWD = True
-_SPLIT_LAYERS = (1, 2, 3, 4)
-# the same two-half schedule for the backward's BN-backward passes and data
-# gradients (_run_backward_split); the weight gradients then go to a third
-# stream (the caller's text stream in the CLIP step)
-_SPLIT_BWD = False
-_AUX_STREAMS = {}
 
 
 def _side_stream(dev):
     s = _WG_STREAMS.get(dev)
     if s is None:
         s = _WG_STREAMS[dev] = torch.cuda.Stream(device=dev)
-    return s
-
-
-def _aux_stream(dev):
-    s = _AUX_STREAMS.get(dev)
-    if s is None:
-        s = _AUX_STREAMS[dev] = torch.cuda.Stream(device=dev)
     return s
 
 
@@ -387,8 +369,6 @@ class ResNet34Tower(ArenaModule):
         return self._run_blocks(ws, T, dev, N, p, pm, saved, training)
 
     def _run_blocks(self, ws, T, dev, N, p, pm, saved, training):
-        if _SPLIT_FWD and training and dev.type == "cuda" and N % 2 == 0 and N >= 2:
-            return self._run_blocks_split(ws, T, dev, N, p, pm, saved)
         bits = training and T == torch.bfloat16
         xmask = pm
         xcur = p
@@ -428,126 +408,24 @@ class ResNet34Tower(ArenaModule):
         blk = {"x": xcur, "xmask": xmask, "y1": y1, "a1": a1, "y2": y2, "yd": yd, "out": out}
         return blk, out, om
 
-    def _run_blocks_split(self, ws, T, dev, N, p, pm, saved):
-        """Training forward with the batch as two image halves: half A on the
-        current stream, half B on a side stream, one pass behind.
-
-        Train-mode BN needs the whole batch's statistics before any element can
-        be normalised, so every BN/ReLU pass (HBM-bound, copy rate) sits between
-        two convolutions (MFMA-bound).  Per statistics barrier:
-            A: pass(A) -> conv(A)
-            B:            pass(B) -> conv(B)      (pass(B) starts after pass(A))
-        so pass(B) runs beside conv(A) and only pass(A) is exposed.  Both halves
-        accumulate into the same fp64 statistic replicas; the finalize runs once
-        on the current stream after joining the side stream.  Results equal the
-        unsplit forward up to the order of the fp64 atomic adds."""
-        main = torch.cuda.current_stream(dev)
-        side = _side_stream(dev)
-        h = N // 2
-        xcur, xmask = p, pm
-        blocks = []
-        b_on_side = False      # xcur's B half was produced on the side stream
-        for pre, has_ds in self._blocks:
-            c1, c2 = self._convs[pre + ".conv1"], self._convs[pre + ".conv2"]
-            if int(pre[5]) not in _SPLIT_LAYERS:
-                if b_on_side:
-                    main.wait_stream(side)
-                    b_on_side = False
-                blk, xcur, xmask = self._block_fwd(ws, T, dev, pre, has_ds, xcur, xmask, True,
-                                                   T == torch.bfloat16)
-                blocks.append(blk)
-                continue
-            if not b_on_side:
-                side.wait_stream(main)
-            N_, Hi, Wi, _ = xcur.shape
-            Ho, Wo = ops.conv_out_hw(Hi, Wi, 3, 3, c1.S, 1)
-            y1 = torch.empty(N, Ho, Wo, c1.Co, dtype=T, device=dev)
-            a1, y2, out = torch.empty_like(y1), torch.empty_like(y1), torch.empty_like(y1)
-            yd = torch.empty_like(y1) if has_ds else None
-            bits = T == torch.bfloat16     # ReLU sign bits of the block output (bf16 backward)
-            om = torch.empty(out.numel() // 8, dtype=torch.uint8, device=dev) if bits else None
-            oh = out.numel() // 16
-            Mb = N * Ho * Wo
-            k1, k2, kd = pre + ".bn1", pre + ".bn2", pre + ".downsample.1"
-            s1, ss1 = self._fstat(ws, k1, full=True)
-            s2, ss2 = self._fstat(ws, k2, full=True)
-            sd = ssd = None
-            if has_ds:
-                cd = self._convs[pre + ".downsample.0"]
-                sd, ssd = self._fstat(ws, kd, full=True)
-
-            def conv1(lo, hi):
-                ops.conv_fwd(xcur[lo:hi], ws[c1.key + ".wp"], c1.Co, 3, 3, c1.S, 1, stat_sum=s1,
-                             stat_sumsq=ss1, out=y1[lo:hi], stat_rep=STAT_REP)
-
-            def pass1_conv2(lo, hi):
-                ops.bn_add_relu(y1[lo:hi], sc1, sh1, None, None, None, a1[lo:hi])
-                ops.conv_fwd(a1[lo:hi], ws[c2.key + ".wp"], c2.Co, 3, 3, 1, 1, stat_sum=s2, stat_sumsq=ss2,
-                             out=y2[lo:hi], stat_rep=STAT_REP)
-                if has_ds:
-                    ops.conv_fwd(xcur[lo:hi], ws[cd.key + ".wp"], cd.Co, 1, 1, cd.S, 0, stat_sum=sd,
-                                 stat_sumsq=ssd, out=yd[lo:hi], stat_rep=STAT_REP)
-
-            conv1(0, h)
-            with torch.cuda.stream(side):
-                conv1(h, N)
-            main.wait_stream(side)
-            sc1, sh1 = self._bn_finalize(ws, k1, Mb, True)
-            pass1_conv2(0, h)
-            side.wait_stream(main)           # finalize + pass(A) queued before pass(B)
-            with torch.cuda.stream(side):
-                pass1_conv2(h, N)
-            main.wait_stream(side)
-            sc2, sh2 = self._bn_finalize(ws, k2, Mb, True)
-            scd = shd = None
-            if has_ds:
-                scd, shd = self._bn_finalize(ws, kd, Mb, True)
-            idt = yd if has_ds else xcur
-            ops.bn_add_relu(y2[:h], sc2, sh2, idt[:h], scd, shd, out[:h], relu_mask=om[:oh] if bits else None)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                ops.bn_add_relu(y2[h:], sc2, sh2, idt[h:], scd, shd, out[h:], relu_mask=om[oh:] if bits else None)
-            b_on_side = True
-            blocks.append({"x": xcur, "xmask": xmask, "y1": y1, "a1": a1, "y2": y2, "yd": yd, "out": out})
-            xcur, xmask = out, om
-        if b_on_side:
-            main.wait_stream(side)
-        feat = torch.empty(N, 512, dtype=T, device=dev)
-        ops.avgpool_fwd(xcur, feat)
-        saved["blocks"] = blocks
-        return feat, saved
-
     # ---------------- backward ----------------
     def stage_span(self, stage):
         """(offset, length) of one stage's parameters in the arena."""
         return self.arena.span(self._stage_names[stage])
 
-    def run_backward(self, saved, dfeat: torch.Tensor, on_stage_done=None, wg_stream=None):
+    def run_backward(self, saved, dfeat: torch.Tensor, on_stage_done=None):
         """dfeat: [N,512] fp32 gradient of the pooled features.  Writes every
         parameter gradient into the grad arena (overwriting).  on_stage_done(off,
         n) is called (in backward order: layer4, layer3, layer2, layer1 + stem)
         once the arena range [off, off+n) holds its final gradients, with every
         kernel writing it already queued on the current stream -- the data-
-        parallel all-reduce of that bucket is launched there.  wg_stream: the
-        stream the split backward queues the weight gradients on (the caller's
-        text-tower stream, so the process keeps to three compute streams); None
-        takes a dedicated one."""
+        parallel all-reduce of that bucket is launched there."""
         ws = self._workspace()
         T = self.tdtype
         dev = self.arena.data.device
-        self._sw = None
-        N = saved["N"]
-        split = (_SPLIT_BWD and saved["training"] and dev.type == "cuda" and N % 2 == 0 and N >= 2
-                 and not _USE_DYT)
-        if split:
-            self._sw = wg_stream if wg_stream is not None else _aux_stream(dev)
-        elif _USE_WG_STREAM and dev.type == "cuda":
-            self._sw = _side_stream(dev)
+        self._sw = _side_stream(dev) if (_USE_WG_STREAM and dev.type == "cuda") else None
         try:
-            if split:
-                self._run_backward_split(saved, dfeat, ws, T, dev, on_stage_done)
-            else:
-                self._run_backward(saved, dfeat, ws, T, dev, on_stage_done)
+            self._run_backward(saved, dfeat, ws, T, dev, on_stage_done)
         finally:
             if self._sw is not None:   # join: every weight gradient is in the arena
                 torch.cuda.current_stream(dev).wait_stream(self._sw)
@@ -702,148 +580,6 @@ class ResNet34Tower(ArenaModule):
             ops.stem_wgrad_into(dy0, saved["xp"], saved["N"], saved["H"], saved["W"],
                                 self.arena.gview("conv1.weight"))
         self._stage_done(["layer1", "stem"], on_stage_done, dev)
-
-    def _run_backward_split(self, saved, dfeat, ws, T, dev, on_stage_done=None):
-        """_run_backward with each block's BN-backward passes and data gradients
-        in two image halves (A on the current stream, B on the side stream, one
-        pass behind), as the split forward: the pass of half B runs beside the
-        data-gradient GEMM of half A.  The statistics barriers (the BN backward
-        sums every pass needs) join the two streams; both halves' epilogues add
-        into the same fp64 replicas.  The weight gradients take the full-batch
-        operands on self._sw once both halves of their dy are written."""
-        main = torch.cuda.current_stream(dev)
-        side = _side_stream(dev)
-        ws["bstat"].zero_()
-        dfeat = dfeat.float().contiguous()
-        blocks = saved["blocks"]
-        N = saved["N"]
-        h = N // 2
-        side.wait_stream(main)
-        dout = None
-        dout_masked = False
-
-        def both(fn):
-            """fn(lo, hi) for half A on main, then half B on the side stream after it."""
-            fn(0, h)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                fn(h, N)
-
-        def join():
-            main.wait_stream(side)
-
-        def wgrad(c, dy, x):
-            self._sw.wait_stream(main)          # main has joined the side stream before every call
-            with torch.cuda.stream(self._sw):
-                ops.conv_wgrad_into(dy, x, c.KH, c.KW, c.S, c.P, self.arena.gview(c.key + ".weight"))
-            dy.record_stream(self._sw)
-            x.record_stream(self._sw)
-
-        for bi in range(len(self._blocks) - 1, -1, -1):
-            pre, has_ds = self._blocks[bi]
-            B = blocks[bi]
-            x, y1, y2, yd, out = B["x"], B["y1"], B["y2"], B["yd"], B["out"]
-            _, Hh, Ww, C = out.shape
-            Cin = x.shape[-1]
-            M = N * Hh * Ww
-            mh = h * Hh * Ww                     # rows of one half
-            last = dout is None
-            dbc = dfeat if last else None
-            c1, c2 = self._convs[pre + ".conv1"], self._convs[pre + ".conv2"]
-            k1, k2, kd = pre + ".bn1", pre + ".bn2", pre + ".downsample.1"
-            _, _, mu2, is2 = self._coef(ws, k2)
-            sg2f, sgx2f = self._bstat(ws, k2, full=True)
-            mud = isd = sgxdf = None
-            if has_ds:
-                _, _, mud, isd = self._coef(ws, kd)
-                sgxdf = self._bstat_ds(ws, k2, full=True)
-            # ---- statistics barrier 1: the bn2 (+ bnd) backward sums of the whole batch
-            join()
-            if not dout_masked:
-                ops.bn_bwd_reduce(M, C, dout, dbc, Hh * Ww, out, y2, mu2, is2, yd, mud, isd, sg2f, sgx2f, sgxdf,
-                                  out, stat_rep=STAT_REP)
-            ops.bn_grad_rep(STAT_REP, C, sg2f, sgx2f, self.arena.gview(k2 + ".weight"),
-                            self.arena.gview(k2 + ".bias"), sgxdf,
-                            self.arena.gview(kd + ".weight") if has_ds else None,
-                            self.arena.gview(kd + ".bias") if has_ds else None)
-            sg2, sgx2 = sg2f[:C], sgx2f[:C]
-            sgxd = sgxdf[:C] if has_ds else None
-            dy2 = torch.empty_like(y2)
-            dyd = torch.empty_like(yd) if has_ds else None
-            g_id = None if has_ds else (dout if dout_masked else torch.empty_like(out))
-            sc1, sh1, mu1, is1 = self._coef(ws, k1)
-            sg1f, sgx1f = self._bstat(ws, k1, full=True)
-            g1 = torch.empty_like(y1)
-
-            def apply2_dgrad2(lo, hi):
-                A = (y2[lo:hi], mu2, is2, self.arena.view(k2 + ".weight"), sg2, sgx2, dy2[lo:hi])
-                Bs = ((yd[lo:hi], mud, isd, self.arena.view(kd + ".weight"), sg2, sgxd, dyd[lo:hi])
-                      if has_ds else None)
-                ops.bn_bwd_apply((hi - lo) * Hh * Ww, C, None if last else dout[lo:hi],
-                                 dbc[lo:hi] if last else None, Hh * Ww, None if dout_masked else out[lo:hi], A, Bs,
-                                 None if (dout_masked or has_ds) else g_id[lo:hi], out)
-                ops.conv_dgrad(dy2[lo:hi], ws[c2.key + ".wt"], Hh, Ww, C, 3, 3, 1, 1, y_bn=y1[lo:hi],
-                               bn=(sc1, sh1, mu1, is1), stat1=sg1f, stat2=sgx1f, out=g1[lo:hi], stat_rep=STAT_REP)
-
-            both(apply2_dgrad2)
-            # ---- statistics barrier 2: the bn1 backward sums
-            join()
-            ops.bn_grad_rep(STAT_REP, C, sg1f, sgx1f, self.arena.gview(k1 + ".weight"),
-                            self.arena.gview(k1 + ".bias"))
-            wgrad(c2, dy2, B["a1"])
-            sg1, sgx1 = sg1f[:C], sgx1f[:C]
-            dy1 = torch.empty_like(y1)
-            Hi, Wi = x.shape[1], x.shape[2]
-            addend = g_id
-            if has_ds:
-                cd = self._convs[pre + ".downsample.0"]
-                addend = torch.empty_like(x)
-            prev = self._blocks[bi - 1] if bi > 0 else None
-            stem_sums = bi == 0 and saved.get("yarg") is not None
-            xm = B.get("xmask")
-            xmh = x.numel() // 16                # ReLU-bit bytes of one half
-            dx = torch.empty_like(x)
-            if stem_sums:
-                _, _, mu0, is0 = self._coef(ws, "bn1")
-                sgpf, sgxpf = self._bstat(ws, "bn1", full=True)
-                mup, isp, yprev = mu0, is0, saved["yarg"]
-                use_bits = xm is not None
-            elif prev is not None and not prev[1]:
-                kp = prev[0] + ".bn2"
-                _, _, mup, isp = self._coef(ws, kp)
-                sgpf, sgxpf = self._bstat(ws, kp, full=True)
-                yprev = blocks[bi - 1]["y2"]
-                use_bits = xm is not None and c1.S == 1
-            else:
-                yprev = None
-
-            def apply1_dgrad1(lo, hi):
-                ops.bn_bwd_apply((hi - lo) * Hh * Ww, C, g1[lo:hi], None, 1, None,
-                                 (y1[lo:hi], mu1, is1, self.arena.view(k1 + ".weight"), sg1, sgx1, dy1[lo:hi]),
-                                 None, None, y1)
-                add = addend[lo:hi] if addend is not None else None
-                if has_ds:
-                    ops.conv_dgrad(dyd[lo:hi], ws[cd.key + ".wt"], Hi, Wi, Cin, 1, 1, cd.S, 0, out=add)
-                if yprev is not None:
-                    rm = xm[lo * xmh // h:hi * xmh // h] if use_bits else x[lo:hi]
-                    ops.conv_dgrad_relu(dy1[lo:hi], ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, rm,
-                                        yprev[lo:hi], mup, isp, sgpf, sgxpf, addend=add, stat_rep=STAT_REP,
-                                        out=dx[lo:hi])
-                else:
-                    ops.conv_dgrad(dy1[lo:hi], ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, addend=add,
-                                   out=dx[lo:hi])
-
-            both(apply1_dgrad1)
-            dout_masked = yprev is not None
-            join()
-            if has_ds:
-                wgrad(cd, dyd, x)
-            wgrad(c1, dy1, x)
-            dout = dx
-            stage = pre.split(".", 1)[0]
-            if pre.endswith(".0") and stage != "layer1":
-                self._stage_done([stage], on_stage_done, dev)
-        self._stem_backward(saved, dout, ws, dev, on_stage_done)
 
     def _tbuf(self, ws, name, C, M):
         """[C][M] bf16 scratch for a transposed output gradient (the weight-gradient
