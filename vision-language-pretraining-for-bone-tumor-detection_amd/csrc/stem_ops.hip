@@ -423,32 +423,34 @@ stem1_route_bwd_kernel(Stem1Geom g, const bf16* __restrict__ xs, const bf16* __r
 //   R = sum_px g(px) P(px)^T   (g: the pooled gradient routed to its arg-max pixel)
 //   G = sum_px P(px) P(px)^T   (the 64 x 64 Gram matrix of the patches)
 //   S = sum_px P(px)
-// so the backward never recomputes y0 and never forms dy per pixel: it scatters
-// each pooled gradient once into a bf16 tile of routed gradients, and runs R, G
-// and S on MFMA over the patch tile (the y0 term is exact here -- W1 G in fp64 in
-// the fold -- where the per-pixel form rounds y0 and dy to bf16).
+// so the backward never recomputes y0 and never forms dy per pixel: it routes
+// each pooled gradient to its arg-max pixel once into a bf16 tile of routed
+// gradients, and runs R, G and S on MFMA over the patch tile (the y0 term is
+// exact here -- W1 G in fp64 in the fold -- where the per-pixel form rounds y0
+// and dy to bf16).
 //
 // Work split: a workgroup owns one image, a band of kGramBand pooled rows and a
-// column block of CW conv-output columns.  Iteration i (pooled row i):
-//   A. the patch tile P [2 rows][CW px][64 k] of conv rows 2i-1, 2i is stored
-//      (prefetched one iteration ahead in registers), and pooled row i's
-//      gradients are scattered into the routed-gradient ring: tap (dh, dw) of
-//      pooled (i, q) lands on conv pixel (2i-1+dh, 2q-1+dw) (ds_pk_add_bf16; the
-//      windows of q and q+1 share a column, so even and odd q scatter in two
-//      passes: a fixed summation order, bit-identical runs);
-//   B. conv rows 2i-1 and 2i are complete (no later pooled row reaches them):
-//      R += Gt^T P, G += P^T P, S += 1^T P on MFMA (operands read transposed from
-//      LDS, ds_read_b64_tr_b16), and the two ring rows the next iteration fills
-//      are cleared.
-// A band starting at i0 > 0 first scatters the dh = 2 taps of pooled row i0 - 1
-// (its row 2 i0 - 1); the last band also completes row Ho - 1.  Each workgroup
-// writes one fp32 slab [R | G | S]; vlp_stem1_bwd_fused's fold sums the slabs in
-// a fixed order (deterministic) and forms dW1.  512 threads; LDS 7 * CW * 128 B.
+// column block of CW conv-output columns.  Iteration a (pooled row a = conv rows
+// 2a, 2a + 1, which only the windows of pooled rows a and a + 1 reach):
+//   A. the patch tile P [2 rows][CW px][64 k] of conv rows 2a, 2a + 1 is stored
+//      (prefetched one iteration ahead in registers), and the routed-gradient
+//      tile Gt [2 rows][CW px][64] is GATHERED: one thread per (column pair
+//      {2q, 2q + 1}, 8-channel chunk) reads the four windows (a|a+1, q|q+1) and
+//      sums, per pixel and channel, the windows whose arg-max tap is that pixel
+//      (pixel (2a, 2q): window (a, q) tap 4; (2a, 2q+1): (a, q) tap 5 + (a, q+1)
+//      tap 3; (2a+1, 2q): (a, q) 7 + (a+1, q) 1; (2a+1, 2q+1): (a, q) 8 +
+//      (a, q+1) 6 + (a+1, q) 2 + (a+1, q+1) 0), in fp32, in that fixed order,
+//      rounded once to bf16: no LDS atomics, bit-identical runs.  Pooled row
+//      a + 1's windows are kept in registers for the next iteration, so every
+//      window is read from HBM once per column block;
+//   B. R += Gt^T P, G += P^T P, S += 1^T P on MFMA (operands read transposed from
+//      LDS, ds_read_b64_tr_b16).
+// Each workgroup writes one fp32 slab [R | G | S]; vlp_stem1_bwd_fused's fold
+// sums the slabs in a fixed order (deterministic) and forms dW1.  512 threads;
+// LDS 4 * CW * 128 B (P and Gt, two conv rows each).
 constexpr int kGramBand = 32;                   // pooled rows per workgroup
-constexpr int kGramSlots = 5;                   // ring of conv-output rows (routed gradients)
 constexpr int kGramSlab = 64 * 64 * 2 + 64;     // R, G, S floats per workgroup
 constexpr int kGramGroups = 32;                 // first-level slab groups of the fold
-typedef __bf16 v2bf __attribute__((ext_vector_type(2)));
 
 // transposed fragment of a [px][64] tile (stile_off layout): lane (i, g) gets
 // column col0 + i of rows row0 + 8g .. +7 (the MFMA operand with k = px)
@@ -466,19 +468,24 @@ __device__ __forceinline__ v8bf tile_tr(const char* tile, int row0, int col0) {
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+// one pooled window's 8-channel chunk: pooled gradient and arg-max taps
+struct GramWin { uint4 pv; uint2 ib; };
+
+#ifndef VLP_GRAM_WPE
+#define VLP_GRAM_WPE 2   // waves per SIMD the Gram kernel is compiled for (4: <= 128 VGPRs, two workgroups per CU)
+#endif
 template <int CW>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(VLP_GRAM_WPE)))
 stem1_bwd_gram_kernel(Stem1Geom g, const bf16* __restrict__ xs, int Hq, int Wq, const bf16* __restrict__ dp,
                       const uint8_t* __restrict__ idx, float* __restrict__ slabs) {
   constexpr int RB = CW * 128;                          // bytes of one conv row in a [px][64] tile
   constexpr int NP = 2 * CW * 8 / 512;                  // patch chunks per thread per iteration
-  constexpr int NQ = CW / 2 + 1;                        // pooled columns reaching the block
-  constexpr int NI = (NQ * 8 + 511) / 512;              // scatter items per thread
+  constexpr int NG = CW / 2 * 8;                        // routing items (column pair, chunk) <= 512
   constexpr int KS = 2 * CW / 32;                       // 32-px k-steps per iteration
+  static_assert(NG <= 512 && NP >= 1, "CW in {64, 128}");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* ptile = smem;
-  char* gring = smem + 2 * RB;
-  const int Ho = g.Ho;
+  char* gtile = smem + 2 * RB;
   const int CB = g.Wo / CW;
   const int bands = (Hq + kGramBand - 1) / kGramBand;
   int bid = blockIdx.x;
@@ -487,29 +494,24 @@ stem1_bwd_gram_kernel(Stem1Geom g, const bf16* __restrict__ xs, int Hq, int Wq, 
   const int band = bid % bands, n = bid / bands;
   const int i0 = band * kGramBand;
   const int i1 = i0 + kGramBand < Hq ? i0 + kGramBand : Hq;
-  const int iend = i1 == Hq ? Hq : i1 - 1;              // the last band also completes row Ho - 1
-  const int c0 = cb * CW, qlo = c0 / 2;
+  const int c0 = cb * CW;
   const int tid = threadIdx.x, l = tid & 63, wv = tid >> 6;
   const char* xb = reinterpret_cast<const char*>(xs + (size_t)n * g.Hp * g.Wp1);
   const bf16* dp_n = dp + (size_t)n * Hq * Wq * 64;
   const uint8_t* idx_n = idx + (size_t)n * Hq * Wq * 64;
 
-  // ---- patch staging: item (row r, pixel px, kh) -> 16 B of xs (zeros outside the conv rows)
+  // ---- patch staging: item (row r, pixel px, kh) -> 16 B of xs
   uint4 pf[NP];
-  auto p_load = [&](int i) __attribute__((always_inline)) {
+  auto p_load = [&](int a) __attribute__((always_inline)) {
 #pragma unroll
     for (int it = 0; it < NP; ++it) {
       const int item = tid + 512 * it;
       const int r = item / (CW * 8), rem = item - r * (CW * 8);
       const int px = rem >> 3, kh = rem & 7;
-      const int rr = 2 * i - 1 + r, wo = c0 + px, sh = wo & 3;
-      if (rr >= 0 && rr < Ho) {
-        const unsigned e = (unsigned)sh * (unsigned)g.copy + (unsigned)(2 * rr + kh) * (unsigned)g.Wp1 +
-                           (unsigned)(2 * wo - 2 * sh);
-        pf[it] = ldg16(xb + 2u * e);
-      } else {
-        pf[it] = make_uint4(0u, 0u, 0u, 0u);
-      }
+      const int rr = 2 * a + r, wo = c0 + px, sh = wo & 3;
+      const unsigned e = (unsigned)sh * (unsigned)g.copy + (unsigned)(2 * rr + kh) * (unsigned)g.Wp1 +
+                         (unsigned)(2 * wo - 2 * sh);
+      pf[it] = ldg16(xb + 2u * e);
     }
   };
   auto p_store = [&]() __attribute__((always_inline)) {
@@ -520,81 +522,46 @@ stem1_bwd_gram_kernel(Stem1Geom g, const bf16* __restrict__ xs, int Hq, int Wq, 
       *reinterpret_cast<uint4*>(ptile + r * RB + stile_off(rem >> 3, rem & 7)) = pf[it];
     }
   };
-  // ---- pooled-gradient items (column q = qlo + (item >> 3), chunk c = item & 7), prefetched
-  uint4 gv[NI];
-  uint2 tv[NI];
-  auto g_load = [&](int i) __attribute__((always_inline)) {
-#pragma unroll
-    for (int it = 0; it < NI; ++it) {
-      const int item = tid + 512 * it;
-      const int q = qlo + (item >> 3), c = item & 7;
-      if (item < NQ * 8 && q < Wq && i >= 0 && i < Hq) {
-        const unsigned po = ((unsigned)i * Wq + q) * 64 + 8 * c;
-        gv[it] = ldg16(dp_n + po);
-        tv[it] = *reinterpret_cast<const uint2*>(idx_n + po);
-      } else {
-        gv[it] = make_uint4(0u, 0u, 0u, 0u);
-        tv[it] = make_uint2(0xffffffffu, 0xffffffffu);   // tap 255: routes nowhere
-      }
+  // ---- routing item of this thread: column pair q (local pixels 2q', 2q' + 1), chunk c
+  const bool router = tid < NG;
+  const int qq = tid >> 3, c = tid & 7;
+  const int q = c0 / 2 + qq;
+  auto ldwin = [&](int i, int qw, GramWin& w) __attribute__((always_inline)) {
+    if (router && i < Hq && qw < Wq) {
+      const unsigned po = ((unsigned)i * Wq + qw) * 64 + 8 * c;
+      w.pv = ldg16(dp_n + po);
+      w.ib = *reinterpret_cast<const uint2*>(idx_n + po);
+    } else {
+      w.pv = make_uint4(0u, 0u, 0u, 0u);
+      w.ib = make_uint2(0xffffffffu, 0xffffffffu);    // tap 255: routes nowhere
     }
   };
-  // scatter the pooled columns q of parity qpar of pooled row i (taps with dh >=
-  // dhmin) into the ring.  Windows q and q + 1 share conv column 2q + 1, so the
-  // two parities run in separate passes (a barrier apart): every routed-gradient
-  // sum then forms in a fixed order (row 2i - 1's earlier-row part, then the even,
-  // then the odd column's window) and the bf16 result is the same on every run.
-  auto scatter_par = [&](int i, int dhmin, int qpar) __attribute__((always_inline)) {
-    const int sbase = (2 * i) % kGramSlots;                 // slot of conv row 2i - 1 (+ dh)
+  auto route = [&](const GramWin& w0, const GramWin& w1, const GramWin& w2, const GramWin& w3)
+      __attribute__((always_inline)) {
+    float f0[8], f1[8], f2[8], f3[8], o[4][8];
+    unpack8(w0.pv, f0); unpack8(w1.pv, f1); unpack8(w2.pv, f2); unpack8(w3.pv, f3);
 #pragma unroll
-    for (int it = 0; it < NI; ++it) {
-      const int item = tid + 512 * it;
-      const int q = qlo + (item >> 3), c = item & 7;
-      if ((q & 1) != qpar) continue;
-      // LDS offsets of the pixel's chunk c for dw = 0, 1, 2 (local column 2q - 1 + dw - c0)
-      int off[3];
-      bool ok[3];
-#pragma unroll
-      for (int dw = 0; dw < 3; ++dw) {
-        const int px = 2 * q - 1 + dw - c0;
-        ok[dw] = px >= 0 && px < CW;
-        const int pc = ok[dw] ? px : 0;
-        off[dw] = stile_off(pc, c);
-      }
-      const uint32_t gw[4] = {gv[it].x, gv[it].y, gv[it].z, gv[it].w};
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const uint32_t t = ((e < 4 ? tv[it].x : tv[it].y) >> (8 * (e & 3))) & 255u;
-        const uint32_t dh = (t * 11u) >> 5;                 // t / 3 for t <= 8
-        const uint32_t dw = t - 3u * dh;
-        const bool valid = t <= 8u && (int)dh >= dhmin && (dw == 0u ? ok[0] : dw == 1u ? ok[1] : ok[2]);
-        if (valid) {
-          int slot = sbase + (int)dh;
-          slot = slot >= kGramSlots ? slot - kGramSlots : slot;
-          const int o = dw == 0u ? off[0] : dw == 1u ? off[1] : off[2];
-          char* at = gring + slot * RB + o + (e & 6) * 2;
-          const uint32_t v = (e & 1) ? (gw[e >> 1] & 0xffff0000u) : (gw[e >> 1] & 0x0000ffffu);
-          __builtin_amdgcn_ds_atomic_fadd_v2bf16(
-              (__attribute__((address_space(3))) v2bf*)lds_addr_stem(at),
-              __builtin_bit_cast(v2bf, v));
-        }
-      }
+    for (int e = 0; e < 8; ++e) {
+      const int sh = 8 * (e & 3);
+      const unsigned t0 = (((e >> 2) ? w0.ib.y : w0.ib.x) >> sh) & 255u;
+      const unsigned t1 = (((e >> 2) ? w1.ib.y : w1.ib.x) >> sh) & 255u;
+      const unsigned t2 = (((e >> 2) ? w2.ib.y : w2.ib.x) >> sh) & 255u;
+      const unsigned t3 = (((e >> 2) ? w3.ib.y : w3.ib.x) >> sh) & 255u;
+      o[0][e] = t0 == 4u ? f0[e] : 0.f;
+      o[1][e] = (t0 == 5u ? f0[e] : 0.f) + (t1 == 3u ? f1[e] : 0.f);
+      o[2][e] = (t0 == 7u ? f0[e] : 0.f) + (t2 == 1u ? f2[e] : 0.f);
+      o[3][e] = (t0 == 8u ? f0[e] : 0.f) + (t1 == 6u ? f1[e] : 0.f) + (t2 == 2u ? f2[e] : 0.f) +
+                (t3 == 0u ? f3[e] : 0.f);
     }
-  };
-  auto scatter = [&](int i, int dhmin) __attribute__((always_inline)) {
-    scatter_par(i, dhmin, 0);
-    lds_barrier();
-    scatter_par(i, dhmin, 1);
-  };
-  auto zero_rows = [&](int slot_a, int slot_b) __attribute__((always_inline)) {
-    for (int q = tid; q < 2 * RB / 16; q += 512) {
-      const int slot = q < RB / 16 ? slot_a : slot_b;
-      const int o = (q < RB / 16 ? q : q - RB / 16) * 16;
-      *reinterpret_cast<uint4*>(gring + slot * RB + o) = make_uint4(0u, 0u, 0u, 0u);
+    if (router) {
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4)
+        *reinterpret_cast<uint4*>(gtile + (k4 >> 1) * RB + stile_off(2 * qq + (k4 & 1), c)) = Chunk<bf16>::pack(o[k4]);
     }
   };
 
   // accumulators: wave (quadrant qd = wv & 3: rows 32a.., columns 32b..; k-step parity wv >> 2)
-  const int a = (wv >> 1) & 1, b = wv & 1, par = wv >> 2;
+  const int a_ = (wv >> 1) & 1, b = wv & 1, par = wv >> 2;
   v4f accR[2][2], accG[2][2], accS[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -606,32 +573,32 @@ stem1_bwd_gram_kernel(Stem1Geom g, const bf16* __restrict__ xs, int Hq, int Wq, 
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.f;
 
-  // ---- prologue
+  // ---- prologue: patches of pair i0, windows of pooled rows i0 and i0 + 1
   p_load(i0);
-  for (int q = tid; q < kGramSlots * RB / 16; q += 512)
-    *reinterpret_cast<uint4*>(gring + q * 16) = make_uint4(0u, 0u, 0u, 0u);
-  g_load(i0 - 1);
-  lds_barrier();
-  if (i0 > 0) scatter(i0 - 1, 2);                        // row 2 i0 - 1's dh = 2 taps
-  g_load(i0);
-  for (int i = i0; i <= iend; ++i) {
-    // ---- A: patches of rows 2i-1, 2i; scatter pooled row i
+  GramWin wa0, wa1, wb0, wb1, wn0, wn1;                  // rows a, a + 1 (columns q, q + 1); a + 2 ahead
+  ldwin(i0, q, wa0);
+  ldwin(i0, q + 1, wa1);
+  ldwin(i0 + 1, q, wb0);
+  ldwin(i0 + 1, q + 1, wb1);
+  for (int a = i0; a < i1; ++a) {
+    // ---- A: patches of rows 2a, 2a + 1; the routed gradients of the same rows
     p_store();
-    if (i < iend) p_load(i + 1);
-    if (i < Hq) scatter(i, i == 0 ? 1 : 0);             // i = 0: row -1 does not exist
-    if (i < iend) g_load(i + 1);
+    if (a + 1 < i1) p_load(a + 1);
+    ldwin(a + 2, q, wn0);                                // next iteration's row a + 1 + 1
+    ldwin(a + 2, q + 1, wn1);
+    route(wa0, wa1, wb0, wb1);
     lds_barrier();
-    // ---- B: R, G, S over the two completed rows; clear the ring rows of 2i+2, 2i+3
+    // ---- B: R, G, S over the two rows
 #pragma unroll 1
     for (int ks = par; ks < KS; ks += 2) {
       const int r = (32 * ks) / CW, px0 = 32 * ks - r * CW;
-      const char* gt = gring + ((2 * i + r) % kGramSlots) * RB;
+      const char* gt = gtile + r * RB;
       const char* pt = ptile + r * RB;
       v8bf fg[2], fp[2], fb[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        fg[j] = tile_tr(gt, px0, 32 * a + 16 * j);
-        fp[j] = tile_tr(pt, px0, 32 * a + 16 * j);
+        fg[j] = tile_tr(gt, px0, 32 * a_ + 16 * j);
+        fp[j] = tile_tr(pt, px0, 32 * a_ + 16 * j);
         fb[j] = tile_tr(pt, px0, 32 * b + 16 * j);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the asm reads' results (hipcc does not track them)
@@ -643,13 +610,13 @@ stem1_bwd_gram_kernel(Stem1Geom g, const bf16* __restrict__ xs, int Hq, int Wq, 
           accR[j][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fg[j], fb[jj], accR[j][jj], 0, 0, 0);
           accG[j][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fp[j], fb[jj], accG[j][jj], 0, 0, 0);
         }
-      if (a == 0) {
+      if (a_ == 0) {
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) accS[jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, fb[jj], accS[jj], 0, 0, 0);
       }
     }
-    zero_rows((2 * i + 3) % kGramSlots, (2 * i + 4) % kGramSlots);
-    lds_barrier();
+    lds_barrier();                                       // P and Gt are rewritten by the next pair
+    wa0 = wb0; wa1 = wb1; wb0 = wn0; wb1 = wn1;
   }
   // ---- the two k-parity halves summed through LDS: one slab [R | G | S] per workgroup
   float* red = reinterpret_cast<float*>(smem);
@@ -662,13 +629,13 @@ stem1_bwd_gram_kernel(Stem1Geom g, const bf16* __restrict__ xs, int Hq, int Wq, 
         for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int m = 32 * a + 16 * j + 4 * (l >> 4) + r, k = 32 * b + 16 * jj + (l & 15);
+            const int m = 32 * a_ + 16 * j + 4 * (l >> 4) + r, k = 32 * b + 16 * jj + (l & 15);
             float* pr = red + m * 64 + k;
             float* pg = red + 4096 + m * 64 + k;
             if (pass == 0) { *pr = accR[j][jj][r]; *pg = accG[j][jj][r]; }
             else { *pr += accR[j][jj][r]; *pg += accG[j][jj][r]; }
           }
-      if (a == 0 && l < 16) {
+      if (a_ == 0 && l < 16) {
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj) {
           float* ps = red + 8192 + 32 * b + 16 * jj + l;
@@ -793,7 +760,10 @@ VLP_EXPORT int vlp_stem1_route_bwd(const void* xs, const void* wp1, const void* 
   return (int)hipGetLastError();
 }
 
-static int stem1_gram_cw(int Wo) { return Wo % 128 == 0 ? 128 : 64; }
+#ifndef VLP_GRAM_CW
+#define VLP_GRAM_CW 128   // widest column block the Gram backward takes (64 or 128)
+#endif
+static int stem1_gram_cw(int Wo) { return (VLP_GRAM_CW == 128 && Wo % 128 == 0) ? 128 : 64; }
 static int stem1_bwd_fused_wgs(int N, int H, int W) {
   const Stem1Geom g = make_stem1(N, H, W);
   const int Hq = g.Ho / 2;
@@ -822,7 +792,7 @@ VLP_EXPORT int vlp_stem1_bwd_fused(const void* xs, const void* wp1, const void* 
   float* part = ws + (size_t)nwg * kGramSlab;
   const int cw = stem1_gram_cw(g.Wo);
   if (cw == 128) {
-    constexpr size_t lds = 7 * 128 * 128;
+    constexpr size_t lds = 4 * 128 * 128;
     static bool attr = false;
     if (!attr) {
       (void)hipFuncSetAttribute((const void*)&stem1_bwd_gram_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -832,7 +802,7 @@ VLP_EXPORT int vlp_stem1_bwd_fused(const void* xs, const void* wp1, const void* 
     hipLaunchKernelGGL(stem1_bwd_gram_kernel<128>, dim3(nwg), dim3(512), lds, st, g, (const bf16*)xs, Hq, Wq,
                        (const bf16*)dp, idx, ws);
   } else {
-    constexpr size_t lds = 7 * 64 * 128;
+    constexpr size_t lds = 4 * 64 * 128 > kGramSlab * 4 ? 4 * 64 * 128 : kGramSlab * 4;   // the slab reduction reuses it
     hipLaunchKernelGGL(stem1_bwd_gram_kernel<64>, dim3(nwg), dim3(512), lds, st, g, (const bf16*)xs, Hq, Wq,
                        (const bf16*)dp, idx, ws);
   }
