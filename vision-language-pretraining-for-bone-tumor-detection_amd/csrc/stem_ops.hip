@@ -471,6 +471,9 @@ __device__ __forceinline__ v8bf tile_tr(const char* tile, int row0, int col0) {
 // one pooled window's 8-channel chunk: pooled gradient and arg-max taps
 struct GramWin { uint4 pv; uint2 ib; };
 
+#ifndef VLP_GRAM_PF
+#define VLP_GRAM_PF 1    // patch prefetch distance of the Gram backward, in row pairs (1 or 2)
+#endif
 #ifndef VLP_GRAM_WPE
 #define VLP_GRAM_WPE 2   // waves per SIMD the Gram kernel is compiled for (4: <= 128 VGPRs, two workgroups per CU)
 #endif
@@ -501,8 +504,9 @@ stem1_bwd_gram_kernel(Stem1Geom g, const bf16* __restrict__ xs, int Hq, int Wq, 
   const uint8_t* idx_n = idx + (size_t)n * Hq * Wq * 64;
 
   // ---- patch staging: item (row r, pixel px, kh) -> 16 B of xs
-  uint4 pf[NP];
-  auto p_load = [&](int a) __attribute__((always_inline)) {
+  // patch prefetch distance VLP_GRAM_PF pairs (2: two register sets, the loop unrolled by 2)
+  uint4 pf0[NP], pf1[NP];
+  auto p_load = [&](int a, uint4 (&pf)[NP]) __attribute__((always_inline)) {
 #pragma unroll
     for (int it = 0; it < NP; ++it) {
       const int item = tid + 512 * it;
@@ -514,7 +518,7 @@ stem1_bwd_gram_kernel(Stem1Geom g, const bf16* __restrict__ xs, int Hq, int Wq, 
       pf[it] = ldg16(xb + 2u * e);
     }
   };
-  auto p_store = [&]() __attribute__((always_inline)) {
+  auto p_store = [&](const uint4 (&pf)[NP]) __attribute__((always_inline)) {
 #pragma unroll
     for (int it = 0; it < NP; ++it) {
       const int item = tid + 512 * it;
@@ -573,50 +577,76 @@ stem1_bwd_gram_kernel(Stem1Geom g, const bf16* __restrict__ xs, int Hq, int Wq, 
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.f;
 
-  // ---- prologue: patches of pair i0, windows of pooled rows i0 and i0 + 1
-  p_load(i0);
-  GramWin wa0, wa1, wb0, wb1, wn0, wn1;                  // rows a, a + 1 (columns q, q + 1); a + 2 ahead
+  // ---- one pair: A (patch tile + gathered routed gradients), B (R, G, S on MFMA).
+  // The fragment reads of k-step ks + 2 are issued before the MFMAs of ks (12
+  // ds_read_b64_tr per k-step, waited for with a counted lgkmcnt).
+  auto frags = [&](int ks, v8bf (&fg)[2], v8bf (&fp)[2], v8bf (&fb)[2]) __attribute__((always_inline)) {
+    const int r = (32 * ks) / CW, px0 = 32 * ks - r * CW;
+    const char* gt = gtile + r * RB;
+    const char* pt = ptile + r * RB;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      fg[j] = tile_tr(gt, px0, 32 * a_ + 16 * j);
+      fp[j] = tile_tr(pt, px0, 32 * a_ + 16 * j);
+      fb[j] = tile_tr(pt, px0, 32 * b + 16 * j);
+    }
+  };
+  auto mfmas = [&](const v8bf (&fg)[2], const v8bf (&fp)[2], const v8bf (&fb)[2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        accR[j][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fg[j], fb[jj], accR[j][jj], 0, 0, 0);
+        accG[j][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fp[j], fb[jj], accG[j][jj], 0, 0, 0);
+      }
+    if (a_ == 0) {
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) accS[jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, fb[jj], accS[jj], 0, 0, 0);
+    }
+  };
+  static_assert(KS % 4 == 0, "k-steps per wave even");
+  GramWin wa0, wa1, wb0, wb1, wn0, wn1;                  // pooled rows a, a + 1 (columns q, q + 1); a + 2 ahead
+  auto pair = [&](int a, uint4 (&pf)[NP]) __attribute__((always_inline)) {
+    p_store(pf);
+    if (a + VLP_GRAM_PF < i1) p_load(a + VLP_GRAM_PF, pf);
+    ldwin(a + 2, q, wn0);
+    ldwin(a + 2, q + 1, wn1);
+    route(wa0, wa1, wb0, wb1);
+    lds_barrier();
+    v8bf g0[2], p0[2], b0[2], g1[2], p1[2], b1[2];
+    frags(par, g0, p0, b0);
+#pragma unroll
+    for (int ks = par; ks < KS; ks += 4) {
+      frags(ks + 2, g1, p1, b1);
+      asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");   // k-step ks's 12 reads (LDS returns in order)
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(g0, p0, b0);
+      if (ks + 4 < KS) {
+        frags(ks + 4, g0, p0, b0);
+        asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(g1, p1, b1);
+    }
+    lds_barrier();                                       // P and Gt are rewritten by the next pair
+    wa0 = wb0; wa1 = wb1; wb0 = wn0; wb1 = wn1;
+  };
+  // ---- prologue: patches of pairs i0, i0 + 1; windows of pooled rows i0, i0 + 1
+  p_load(i0, pf0);
+  if (VLP_GRAM_PF == 2 && i0 + 1 < i1) p_load(i0 + 1, pf1);
   ldwin(i0, q, wa0);
   ldwin(i0, q + 1, wa1);
   ldwin(i0 + 1, q, wb0);
   ldwin(i0 + 1, q + 1, wb1);
-  for (int a = i0; a < i1; ++a) {
-    // ---- A: patches of rows 2a, 2a + 1; the routed gradients of the same rows
-    p_store();
-    if (a + 1 < i1) p_load(a + 1);
-    ldwin(a + 2, q, wn0);                                // next iteration's row a + 1 + 1
-    ldwin(a + 2, q + 1, wn1);
-    route(wa0, wa1, wb0, wb1);
-    lds_barrier();
-    // ---- B: R, G, S over the two rows
-#pragma unroll 1
-    for (int ks = par; ks < KS; ks += 2) {
-      const int r = (32 * ks) / CW, px0 = 32 * ks - r * CW;
-      const char* gt = gtile + r * RB;
-      const char* pt = ptile + r * RB;
-      v8bf fg[2], fp[2], fb[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        fg[j] = tile_tr(gt, px0, 32 * a_ + 16 * j);
-        fp[j] = tile_tr(pt, px0, 32 * a_ + 16 * j);
-        fb[j] = tile_tr(pt, px0, 32 * b + 16 * j);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the asm reads' results (hipcc does not track them)
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-          accR[j][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fg[j], fb[jj], accR[j][jj], 0, 0, 0);
-          accG[j][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fp[j], fb[jj], accG[j][jj], 0, 0, 0);
-        }
-      if (a_ == 0) {
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) accS[jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, fb[jj], accS[jj], 0, 0, 0);
-      }
+  if constexpr (VLP_GRAM_PF == 2) {
+    for (int a = i0; a < i1; a += 2) {
+      pair(a, pf0);
+      if (a + 1 < i1) pair(a + 1, pf1);
     }
-    lds_barrier();                                       // P and Gt are rewritten by the next pair
-    wa0 = wb0; wa1 = wb1; wb0 = wn0; wb1 = wn1;
+  } else {
+    for (int a = i0; a < i1; ++a) pair(a, pf0);
   }
   // ---- the two k-parity halves summed through LDS: one slab [R | G | S] per workgroup
   float* red = reinterpret_cast<float*>(smem);
