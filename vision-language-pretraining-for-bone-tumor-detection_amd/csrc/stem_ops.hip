@@ -36,6 +36,10 @@
 namespace vlp {
 
 constexpr int kStemBand = 8;      // pooled rows per workgroup (forward)
+#ifndef VLP_STEM_PK
+#define VLP_STEM_PK 1                 // forward BN sums in packed fp32 (two channels per instruction)
+#endif
+typedef float v2f __attribute__((ext_vector_type(2)));
 constexpr int kStemPairs = 8;     // conv-output row pairs per workgroup (backward)
 
 // byte offset of 16-B chunk `chunk` of pixel px in a [px][64] bf16 tile: rows of 128 B
@@ -189,6 +193,11 @@ stem1_pool_fwd_kernel(Stem1Geom g, const bf16* __restrict__ xs, const bf16* __re
   float s1[8], s2[8];   // sum and sum of squares of s*y0 over this thread's pixels, chunk c
 #pragma unroll
   for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+#if VLP_STEM_PK
+  v2f s1p[4], s2p[4];
+#pragma unroll
+  for (int e2 = 0; e2 < 4; ++e2) s1p[e2] = s2p[e2] = v2f{0.f, 0.f};
+#endif
   // running window maxima of s*y0 per item (column j = item >> 3) and their taps
   float best[NI][8];
   uint32_t tap[NI][2];
@@ -221,11 +230,21 @@ stem1_pool_fwd_kernel(Stem1Geom g, const bf16* __restrict__ xs, const bf16* __re
         const bool left = j > 0;
         unpack8(*reinterpret_cast<const uint4*>(tile + stile_off(left ? 2 * j - 1 : 0, c)), vl);
         if (stats && rr >= 1) {
+#if VLP_STEM_PK
+          // packed fp32 (v_pk_add_f32 / v_pk_fma_f32: two channels per instruction)
+#pragma unroll
+          for (int e2 = 0; e2 < 4; ++e2) {
+            const v2f c2 = {vc[2 * e2], vc[2 * e2 + 1]}, r2 = {vr[2 * e2], vr[2 * e2 + 1]};
+            s1p[e2] += c2 + r2;
+            s2p[e2] = __builtin_elementwise_fma(c2, c2, __builtin_elementwise_fma(r2, r2, s2p[e2]));
+          }
+#else
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             s1[e] += vc[e] + vr[e];
             s2[e] = fmaf(vc[e], vc[e], fmaf(vr[e], vr[e], s2[e]));
           }
+#endif
         }
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
@@ -275,6 +294,13 @@ stem1_pool_fwd_kernel(Stem1Geom g, const bf16* __restrict__ xs, const bf16* __re
     }
   }
   if (!stats) return;
+#if VLP_STEM_PK
+#pragma unroll
+  for (int e2 = 0; e2 < 4; ++e2) {
+    s1[2 * e2] = s1p[e2][0]; s1[2 * e2 + 1] = s1p[e2][1];
+    s2[2 * e2] = s2p[e2][0]; s2[2 * e2 + 1] = s2p[e2][1];
+  }
+#endif
   // statistics: each thread summed its columns {2j, 2j + 1} of chunk c over the owned
   // rows; the 32 threads sharing a chunk meet in LDS
   __syncthreads();
