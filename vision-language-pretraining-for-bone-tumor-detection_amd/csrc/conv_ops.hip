@@ -1223,18 +1223,42 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
       else if (i == 1) wait_vmcnt<2 + S>();     // row 2 (row 3, row-0 stores in flight)
       else wait_vmcnt<2 + 2 * S>();             // row i+1 (rows i+2, stores of i-2, i-1)
       raw_barrier();                            // all waves: ring rows landed, row i-1 done
-      fetch(n, i + 3);
-      // epilogue operands of this row: issued now, consumed after the MFMAs
+      // epilogue operands of this row (row-chunk epilogues): issued now, consumed
+      // after the MFMAs, and BEFORE the ring fetch of row i+3 -- vmcnt retires in
+      // issue order, so the epilogue's wait for them leaves that fetch in flight
+      // (issued after the fetch, the wait drained it within the row: layer-1
+      // data gradient with the ReLU epilogue 641 -> 561 us, tools/conv_bench.py)
+      constexpr bool kRowEpi = RowTrait<EP>::value;
+      if constexpr (!kRowEpi) fetch(n, i + 3);
       RowPre pre[2];
-      if constexpr (RowTrait<EP>::value) {
+      if constexpr (kRowEpi) {
 #pragma unroll
         for (int h2 = 0; h2 < 2; ++h2) ep.pre8((n * H + i) * kRcW + (tid >> 3) + 64 * h2, (tid & 7) * 8, pre[h2]);
+        __builtin_amdgcn_sched_barrier(0);      // keep the issue order
+        fetch(n, i + 3);
       }
       v4f acc[2][2];
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[a][b] = v4f{0.f, 0.f, 0.f, 0.f};
+      // row-chunk epilogues: the lane's ring offsets of its (kw, s) fragments
+      // (kc_off of ring row 32pq + kw + li, chunk 4s + lg; the a = 1 fragment is
+      // +16 rows = +2 KiB, same swizzle) are recomputed per row from an opaque
+      // seed -- hoisted out of the row loop they were ~35 loop-invariant VGPRs
+      // that spilled beside the epilogue operands, and every scratch reload's
+      // vmcnt(0) drained the ring prefetch.  (The forward, with no epilogue
+      // operands, keeps the hoisted form: 362 vs 383 us.)
+      int seed = pq * 32 + li;
+      if constexpr (kRowEpi) asm volatile("" : "+v"(seed));
+      int foff[3][2];
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int r = seed + kw;
+          foff[kw][s] = r * 128 + (((4 * s + lg) ^ ((r >> 1) & 7)) << 4);
+        }
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
         const char* sl = ring + ((i + kh) % kRcRing) * kRcSlot;   // input row i - 1 + kh
@@ -1244,7 +1268,10 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
 #pragma unroll
           for (int s = 0; s < 2; ++s)
 #pragma unroll
-            for (int a = 0; a < 2; ++a) fa[s][a] = frag_bf16<true, 128, true>(sl, pq * 32 + a * 16 + kw, s);
+            for (int a = 0; a < 2; ++a) {
+              if constexpr (kRowEpi) fa[s][a] = *reinterpret_cast<const v8bf*>(sl + foff[kw][s] + a * 2048);
+              else fa[s][a] = frag_bf16<true, 128, true>(sl, pq * 32 + a * 16 + kw, s);
+            }
 #pragma unroll
           for (int s = 0; s < 2; ++s)
 #pragma unroll
