@@ -1553,6 +1553,9 @@ __global__ void wgrad_fold_kernel(int Co, int C, int T, int ks, size_t slab, con
   g[((size_t)co * C + c) * T + t] = (a0 + a1) + (a2 + a3);
 }
 
+#ifndef VLP_WGRAD_SLOT_DIV
+#define VLP_WGRAD_SLOT_DIV 1   // weight-gradient split count sized for 1/DIV of the chip's slots
+#endif
 template <typename T>
 static int conv_wgrad_ws_t(const void* dy, const void* x, float* ws, long long ws_floats, int* ks_out, ConvGeom g,
                            hipStream_t st) {
@@ -1576,8 +1579,10 @@ static int conv_wgrad_ws_t(const void* dy, const void* x, float* ws, long long w
       MNMat<bf16> la{(const bf16*)dy, g.Co, g.Co, g.M};
       ConvWgradB<bf16, false> lb{g, (const bf16*)x, nullptr, nullptr, g.K, make_pixstep(g, Elem<bf16>::BK)};
       EpiSplitStore ep{nullptr, nullptr, ws, g.K, slab};
+      ksplit_slot_div() = VLP_WGRAD_SLOT_DIV;
       const int r = g.Co <= 64 ? gemm_short<bf16>(g.Co, g.K, g.M, -mink, la, lb, ep, st)
                                : gemm_conv_wide<bf16>(g.Co, g.K, g.M, -mink, la, lb, ep, st);
+      ksplit_slot_div() = 1;
       if (r) return r;
       ks = last_ksplit();
       if (ks > max_ks) return (int)hipErrorInvalidValue;   // would have overrun the workspace

@@ -1521,7 +1521,15 @@ inline int& last_ksplit() {
   static thread_local int v = 1;
   return v;
 }
+// fraction of the chip's workgroup slots an auto-split launch is sized for
+// (1: all; the weight gradients on their side stream may take fewer, see
+// conv_wgrad_ws_t)
+inline int& ksplit_slot_div() {
+  static thread_local int v = 1;
+  return v;
+}
 inline int balanced_ksplit(int tiles, int K, int slots, int min_k) {
+  slots = slots / ksplit_slot_div() > 0 ? slots / ksplit_slot_div() : 1;
   if (tiles >= slots) return 1;
   int best = 1;
   double best_eff = 0.0;
