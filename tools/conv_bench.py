@@ -49,6 +49,10 @@ def main():
         for op in args.ops.split(","):
             if op == "fwd":
                 fn = lambda: ops.conv_fwd(x, wp, Co, KH, KW, S, P, stat_sum=s1, stat_sumsq=s2, stat_rep=64)  # noqa: E731
+            elif op == "fwd_bn":       # BN-apply + ReLU of the input on load (in_scale / in_shift)
+                xsc, xsh = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
+                fn = lambda: ops.conv_fwd(x, wp, Co, KH, KW, S, P, in_scale=xsc, in_shift=xsh,  # noqa: E731
+                                          stat_sum=s1, stat_sumsq=s2, stat_rep=64)
             elif op == "dgrad":
                 fn = lambda: ops.conv_dgrad(dy, wt, H, W, C, KH, KW, S, P)  # noqa: E731
             elif op == "dgrad_bn":     # + ReLU-mask of bn(y), BN backward sums (EpiDgradBN)

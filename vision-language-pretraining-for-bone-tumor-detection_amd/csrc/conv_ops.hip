@@ -142,6 +142,18 @@ struct ConvFwdA {
     return ((s.mask >> st.tap) & 1u) ? s.base + st.delta : kOOB;
   }
 };
+// BN-apply + ReLU on load for the ping-pong kernel (gemm_pp_kernel applies
+// relu(sc*a + sh) to its A fragments; C <= 512 channels in its LDS table)
+struct ConvFwdABn : ConvFwdA<bf16, false> {
+  static constexpr bool kXformA = true;
+  __device__ int xchannels() const { return g.C; }
+  __device__ unsigned xrow_mask(int m) const { return bstart(m, 0, 0).mask; }
+  __device__ unsigned xtap(int k0, int& ci0) const {
+    const int tap = fdiv(k0, g.fd_c);
+    ci0 = k0 - tap * g.C;
+    return (unsigned)tap;
+  }
+};
 // the same operand through register staging only (per-chunk filter tap): for
 // channel counts the one-tap-per-K-step LDS-DMA / direct loaders cannot take
 template <typename T>
@@ -1390,6 +1402,9 @@ static int launch_rows_c64(const ConvGeom& g, const void* x, const void* w, int 
   return (int)hipGetLastError();
 }
 
+#ifndef VLP_FWD_BN_PP
+#define VLP_FWD_BN_PP 1   // bf16 BN-on-load forward on the ping-pong kernel (fragment transform)
+#endif
 template <typename T>
 static int conv_fwd_t(const void* x, const void* wp, void* y, ConvGeom g, const float* sc,
                       const float* sh, double* s1, double* s2, int rep, hipStream_t st) {
@@ -1398,6 +1413,14 @@ static int conv_fwd_t(const void* x, const void* wp, void* y, ConvGeom g, const 
   KMat<T> lb{(const T*)wp, g.K, g.Co, g.K};
   EpiConvFwd<T> ep{s1, s2, rep, (T*)y, g.Co};
   if (sc) {
+#if VLP_FWD_BN_PP
+    if constexpr (std::is_same<T, bf16>::value) {
+      if (g.C % 64 == 0 && g.C <= 512 && g.M >= 256 && g.Co >= 256) {
+        ConvFwdABn la{{g, (const bf16*)x, sc, sh}};
+        return launch_gemm_pp<256, 256, 2, 4>(g.M, g.Co, g.K, 1, la, lb, ep, st);
+      }
+    }
+#endif
     ConvFwdA<T, true> la{g, (const T*)x, sc, sh};
     return gemm_auto<T>(g.M, g.Co, g.K, 1, la, lb, ep, st);
   }

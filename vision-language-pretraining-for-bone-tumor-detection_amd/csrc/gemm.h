@@ -934,6 +934,20 @@ __device__ __forceinline__ void dma16(rsrc_t r, unsigned voff, char* lds) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, (int)voff, 0, 0, 0);
 }
 
+// A operand loaders that ask the ping-pong kernel to apply relu(sc[c]*a + sh[c])
+// to the A fragments in registers (BN-apply + ReLU on load; padding taps and
+// rows past M masked to zero from the loader's tap-validity mask)
+template <class L, class = void> struct XformTrait { static constexpr bool value = false; };
+template <class L> struct XformTrait<L, std::void_t<decltype(L::kXformA)>> { static constexpr bool value = L::kXformA; };
+__device__ __forceinline__ v8bf bn_relu_frag(v8bf v, v4f s0, v4f s1, v4f h0, v4f h1, bool ok) {
+  v8bf r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[j] = (bf16)fmaxf(fmaf((float)v[j], s0[j], h0[j]), 0.f);
+    r[4 + j] = (bf16)fmaxf(fmaf((float)v[4 + j], s1[j], h1[j]), 0.f);
+  }
+  return ok ? r : v8bf{};
+}
 template <class L, class = void> struct BufTrait { static constexpr bool value = false; };
 template <class L> struct BufTrait<L, std::void_t<decltype(L::kBuf)>> { static constexpr bool value = L::kBuf; };
 
@@ -1267,6 +1281,13 @@ gemm_big_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   }
 }
 
+template <int BM, int BN, class EP>
+constexpr int big_lds_bytes() {
+  constexpr int ring = 2 * (BM + BN) * 128;
+  constexpr int stg = StageTrait<EP>::value ? 4096 + BM * BN * 2 : 4096;
+  return ring > stg ? ring : stg;
+}
+
 // ---------------- ping-pong large-tile kernel (bf16, K-contig operands) ----------------
 // The two wave groups of a 2 x WGN workgroup (M halves; one wave of each per
 // SIMD) run one barrier interval apart, so that on every SIMD one wave issues
@@ -1391,6 +1412,23 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   const int lane = threadIdx.x & 63;
   const int fi = lane & 15, fg = lane >> 4;
   const char* fbase = smem + fi * 64 + (pp_chunk(fi, fg) << 4);
+  // BN-apply on the A fragments: per-channel (scale, shift) table in LDS past
+  // the ring / epilogue staging, one tap-validity mask per fragment row
+  constexpr bool XA = XformTrait<LA>::value;
+  float* const xtab = reinterpret_cast<float*>(smem + big_lds_bytes<BM, BN, EP>());
+  unsigned xm[XA ? (MB + 2) / 3 : 1];   // three 9-bit row masks per register
+  if constexpr (XA) {
+    const int C = la.xchannels();
+    for (int i = threadIdx.x; i < C; i += NT) {
+      xtab[i] = la.sc[i];
+      xtab[512 + i] = la.sh[i];
+    }
+#pragma unroll
+    for (int a = 0; a < (MB + 2) / 3; ++a) xm[a] = 0;
+#pragma unroll
+    for (int a = 0; a < MB; ++a) xm[a / 3] |= la.xrow_mask(row0 + wm * WTM + a * 16 + fi) << (9 * (a % 3));
+    __syncthreads();
+  }
   // MN-contig operands: one transposing-read address per (slot pair, fragment column)
   constexpr int QA = MB < 4 ? MB : 4, QB = NB < 4 ? NB : 4;
   unsigned abase[2][LA::kKContig ? 1 : QA], bbase[2][LB::kKContig ? 1 : QB];
@@ -1453,6 +1491,17 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
         else
           fb[b] = frag_tr_at<SO + (b >> 2) * 1024>(bbase[SL >> 1][b & 3]);
       });
+      v4f xs0, xs1, xh0, xh1;
+      unsigned xtap = 0;
+      if constexpr (XA) {
+        int ci0;
+        xtap = la.xtap(kb + (q >> 1) * BK, ci0);
+        const float* t = xtab + ci0 + (SL & 1) * 32 + fg * 8;
+        xs0 = *reinterpret_cast<const v4f*>(t);
+        xs1 = *reinterpret_cast<const v4f*>(t + 4);
+        xh0 = *reinterpret_cast<const v4f*>(t + 512);
+        xh1 = *reinterpret_cast<const v4f*>(t + 516);
+      }
       if constexpr (G == 0) {
         fetch(std::integral_constant<int, SL & 1>{}, q + 2, smem + ((SL + 2) & 3) * SLOT);
       } else {
@@ -1466,6 +1515,10 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
 #if VLP_PP_PRIO
       __builtin_amdgcn_s_setprio(1);
 #endif
+      if constexpr (XA) {
+#pragma unroll
+        for (int a = 0; a < MB; ++a) fa[a] = bn_relu_frag(fa[a], xs0, xs1, xh0, xh1, (xm[a / 3] >> (xtap + 9 * (a % 3))) & 1u);
+      }
 #pragma unroll
       for (int a = 0; a < MB; ++a)
 #pragma unroll
@@ -1503,12 +1556,6 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   }
 }
 
-template <int BM, int BN, class EP>
-constexpr int big_lds_bytes() {
-  constexpr int ring = 2 * (BM + BN) * 128;
-  constexpr int stg = StageTrait<EP>::value ? 4096 + BM * BN * 2 : 4096;
-  return ring > stg ? ring : stg;
-}
 
 // Split-K count for a reduction of K over `tiles` output tiles, given the
 // number of workgroups the chip holds at once (`slots`).  Workgroups of one
@@ -1727,7 +1774,7 @@ inline int launch_gemm_pp(int M, int N, int K, int ksplit, const LA& la, const L
   sh.M = M; sh.N = N; sh.K = K;
   sh.tiles_m = (M + BM - 1) / BM;
   sh.tiles_n = (N + BN - 1) / BN;
-  constexpr int lds = big_lds_bytes<BM, BN, EP>();
+  constexpr int lds = big_lds_bytes<BM, BN, EP>() + (XformTrait<LA>::value ? 4096 : 0);
   static_assert(lds <= 160 * 1024, "LDS budget");
   if (ksplit <= 0) {   // auto: fill whole rounds of resident workgroups (one per CU)
     static int occ = 0;
