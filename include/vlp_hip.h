@@ -55,6 +55,20 @@ int vlp_conv_fwd(int dtype, const void* x, const void* wp, void* y, int N, int H
                  int Co, int KH, int KW, int S, int P, const float* in_scale,
                  const float* in_shift, double* stat_sum, double* stat_sumsq, int stat_rep,
                  void* stream);
+/* Conv forward with BN-apply + ReLU of its input fused (timm BasicBlock
+ * act1(bn1(conv1(x))) -> conv2, VisionLanguageModule.py:30-32): x is the raw
+ * output of the previous conv; each input element becomes
+ * relu(in_scale[c]*x + in_shift[c]) once, and that activation is also written to
+ * x_act (what this conv's weight gradient reads), so no separate BN pass runs.
+ * Bit-identical to vlp_bn_add_relu (no residual) followed by vlp_conv_fwd.
+ * Layer-1 geometry only: vlp_conv_fwd_act_ok(...) = 1 when the shape is taken
+ * (bf16, C = Co = 64, 3x3, stride 1, pad 1, W = 128); otherwise
+ * vlp_conv_fwd_act returns hipErrorInvalidValue. */
+int vlp_conv_fwd_act_ok(int dtype, int N, int H, int W, int C, int Co, int KH, int KW, int S, int P);
+int vlp_conv_fwd_act(int dtype, const void* x, const void* wp, void* y, void* x_act, int N, int H, int W,
+                     int C, int Co, int KH, int KW, int S, int P, const float* in_scale,
+                     const float* in_shift, double* stat_sum, double* stat_sumsq, int stat_rep,
+                     void* stream);
 /* dx[N][H][W][C] = conv^T(dy, w).  If y_bn != NULL: dx := dx * (bn_scale*y_bn +
  * bn_shift > 0) (ReLU mask of the producing BN+ReLU) and stat1 += sum(dx),
  * stat2 += sum(dx * (y_bn - bn_mean) * bn_invstd); else if addend != NULL:

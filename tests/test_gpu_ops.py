@@ -101,6 +101,44 @@ def test_conv_fwd(ops, dt, case, xform):
     assert rel(s2.cpu(), (ref * ref).sum((0, 2, 3))) < 1e-4
 
 
+@pytest.mark.parametrize("N,H", [(3, 5), (2, 128), (300, 4)])
+def test_conv_fwd_act_matches_pass_then_conv(ops, N, H):
+    """vlp_conv_fwd_act (bn1 + ReLU in the layer-1 rows kernel's ring) against the
+    separate bn_add_relu pass + conv_fwd: a1 and y bit-identical, BN sums equal up
+    to fp64 atomic order; N = 300 > CUs puts two images on some workgroups."""
+    torch.manual_seed(11)
+    C = 64
+    dev = torch.device("cuda")
+    y1 = torch.randn(N, H, 128, C, device=dev).to(torch.bfloat16)
+    sc = (torch.rand(C, device=dev) + 0.5) * torch.where(torch.arange(C, device=dev) % 5 == 0, -1.0, 1.0)
+    sh = torch.randn(C, device=dev) * 0.3
+    w = (torch.randn(C, C, 3, 3) * (9 * C) ** -0.5).to(torch.bfloat16).float()
+    wp = torch.empty(C, 3, 3, C, dtype=torch.bfloat16, device=dev)
+    ops.pack_conv(w.cuda(), wp, None)
+    assert ops.conv_fwd_act_ok(y1, C, 3, 3, 1, 1)
+    a_ref = torch.empty_like(y1)
+    ops.bn_add_relu(y1, sc, sh, None, None, None, a_ref)
+    r1, r2 = (torch.zeros(4 * C, dtype=torch.float64, device=dev) for _ in range(2))
+    y_ref = ops.conv_fwd(a_ref, wp, C, 3, 3, 1, 1, stat_sum=r1, stat_sumsq=r2, stat_rep=4)
+    a = torch.full_like(y1, float("nan"))
+    t1, t2 = (torch.zeros(4 * C, dtype=torch.float64, device=dev) for _ in range(2))
+    y = ops.conv_fwd_act(y1, wp, C, 3, 3, 1, 1, sc, sh, a, t1, t2, stat_rep=4)
+    torch.cuda.synchronize()
+    assert torch.equal(a, a_ref)
+    assert torch.equal(y, y_ref)
+    assert torch.allclose(t1.view(4, C).sum(0), r1.view(4, C).sum(0), rtol=1e-9, atol=1e-9)
+    assert torch.allclose(t2.view(4, C).sum(0), r2.view(4, C).sum(0), rtol=1e-9, atol=1e-9)
+    # against torch: conv2d(relu(bn(y1))) in fp32 on the bf16 activation
+    xin = nchw(a_ref.float().cpu())
+    ref = F.conv2d(xin, w, padding=1)
+    assert rel(nchw(y.float().cpu()), ref) < tol(torch.bfloat16)
+    # other shapes are refused, not silently rerouted
+    assert not ops.conv_fwd_act_ok(y1[:, :, :64].contiguous(), C, 3, 3, 1, 1)
+    with pytest.raises(RuntimeError):
+        ops.conv_fwd_act(y1[:, :, :64].contiguous(), wp, C, 3, 3, 1, 1, sc, sh, a[:, :, :64].contiguous(),
+                         t1, t2, stat_rep=4)
+
+
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_dgrad_wgrad(ops, dt, case):

@@ -12,8 +12,9 @@ for f in conv_ops stem_ops bn_ops bert_ops head_ops optim_ops probe_ops retrieva
   [ $f = prep_ops ] && EXTRA="-ffp-contract=off"
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -fvisibility=hidden \
     -Wno-unused-result $EXTRA $FLAGS -c $CSRC/$f.hip -o $OUT/obj/$f.o &
+  PIDS="$PIDS $!"
 done
-wait
+for p in $PIDS; do wait $p || { echo "variant $NAME: compile failed"; exit 1; }; done
 /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $OUT/libvlp_hip.so $OUT/obj/*.o
 rm -rf $OUT/obj
 echo built $OUT/libvlp_hip.so

@@ -53,6 +53,17 @@ def main():
                 xsc, xsh = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
                 fn = lambda: ops.conv_fwd(x, wp, Co, KH, KW, S, P, in_scale=xsc, in_shift=xsh,  # noqa: E731
                                           stat_sum=s1, stat_sumsq=s2, stat_rep=64)
+            elif op == "fwd_act":      # layer 1: bn + ReLU in the rows kernel's ring, activation written out
+                xsc, xsh = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
+                xa = torch.empty_like(x)
+                fn = lambda: ops.conv_fwd_act(x, wp, Co, KH, KW, S, P, xsc, xsh, xa, s1, s2, stat_rep=64)  # noqa: E731
+            elif op == "pass_fwd":     # the unfused pair: bn_add_relu pass, then the forward
+                xsc, xsh = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1
+                xa = torch.empty_like(x)
+
+                def fn():
+                    ops.bn_add_relu(x, xsc, xsh, None, None, None, xa)
+                    ops.conv_fwd(xa, wp, Co, KH, KW, S, P, stat_sum=s1, stat_sumsq=s2, stat_rep=64)
             elif op == "dgrad":
                 fn = lambda: ops.conv_dgrad(dy, wt, H, W, C, KH, KW, S, P)  # noqa: E731
             elif op == "dgrad_bn":     # + ReLU-mask of bn(y), BN backward sums (EpiDgradBN)

@@ -1148,17 +1148,27 @@ constexpr int kRcW = 128;                        // image width handled
 constexpr int kRcSlot = (kRcW + 2) * 128;        // one ring row (bytes)
 constexpr int kRcWeights = 9 * 64 * 128;         // 73728
 constexpr int kRcRing = 5;
-constexpr int kRcLds = kRcWeights + kRcRing * kRcSlot + 2048;
+constexpr int kRcXtab = kRcWeights + kRcRing * kRcSlot + 2048;   // BN (scale, shift) table, 512 B
+constexpr int kRcLds = kRcXtab + 512;
 
-template <class EP>
+#ifndef VLP_ACT_NT
+#define VLP_ACT_NT 0   // non-temporal stores of the transformed input rows
+#endif
+// XF: the input is the raw output of the previous conv; every input row is
+// turned into relu(sc[c]*x + sh[c]) once, in place in the ring right after it
+// lands (padding rows stay zero), and written to xout (the activation the
+// weight gradient reads) -- BN-apply + ReLU without a separate pass
+template <class EP, bool XF = false>
 __global__ void __launch_bounds__(512)
 conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __restrict__ w, int flip,
-                        EP ep, int M) {
+                        EP ep, int M, const float* __restrict__ xsc = nullptr,
+                        const float* __restrict__ xsh = nullptr, bf16* __restrict__ xout = nullptr) {
   // 8 waves: wave w computes pixels 32*(w&3) .. +31 and channels 32*(w>>2) .. +31
   // of each output row; its 9 taps x 2 k-substeps x 2 column blocks of filter
   // fragments (144 VGPRs) stay in registers, so the row loop reads only the
   // input ring (4 ds_read_b128 per tap) and two waves share each SIMD.
   constexpr int S = RowTrait<EP>::value ? 2 : 4;  // global stores per lane per output row
+  static_assert(!XF || !RowTrait<EP>::value, "input transform with the direct epilogue only");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* wlds = smem;
   char* ring = smem + kRcWeights;
@@ -1225,15 +1235,51 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
     for (int q = tid; q < NCF * 64; q += 512) cfl[q] = ep.coef(q >> 6)[q & 63];
     __syncthreads();
   }
+  float* xtab = reinterpret_cast<float*>(smem + kRcXtab);
+  if constexpr (XF) {
+    if (tid < 128) xtab[tid] = tid < 64 ? xsc[tid] : xsh[tid - 64];
+    __syncthreads();
+  }
+  // ring row r (0 <= r < H) of image n -> relu(sc*x + sh), in place and to xout;
+  // thread t takes the fixed channel chunk t%8 of pixels t/8 and t/8 + 64
+  auto xrow = [&](int n, int r) __attribute__((always_inline)) {
+    char* slot = ring + ((r + 1) % kRcRing) * kRcSlot + 128;
+    const int cc = tid & 7;
+    const v4f s0 = *reinterpret_cast<const v4f*>(xtab + cc * 8), s1 = *reinterpret_cast<const v4f*>(xtab + cc * 8 + 4);
+    const v4f h0 = *reinterpret_cast<const v4f*>(xtab + 64 + cc * 8), h1 = *reinterpret_cast<const v4f*>(xtab + 68 + cc * 8);
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const int px = (tid >> 3) + 64 * h2;
+      uint4* p = reinterpret_cast<uint4*>(slot + px * 128 + ((cc ^ (((px + 1) >> 1) & 7)) << 4));
+      float f[8];
+      Chunk<bf16>::unpack(*p, f);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f[j] = fmaxf(fmaf(f[j], s0[j], h0[j]), 0.f);
+        f[4 + j] = fmaxf(fmaf(f[4 + j], s1[j], h1[j]), 0.f);
+      }
+      const uint4 v = Chunk<bf16>::pack(f);
+      *p = v;
+#if VLP_ACT_NT
+      typedef unsigned v4u_nt __attribute__((ext_vector_type(4)));
+      __builtin_nontemporal_store(v4u_nt{v.x, v.y, v.z, v.w},
+                                  reinterpret_cast<v4u_nt*>(xout + (((size_t)n * H + r) * kRcW + px) * 64 + cc * 8));
+#else
+      stg16(xout + (((size_t)n * H + r) * kRcW + px) * 64 + cc * 8, v);
+#endif
+    }
+  };
 
   for (int n = blockIdx.x; n < N; n += gridDim.x) {
     wait_vmcnt<0>();
     __syncthreads();
     fetch(n, -1); fetch(n, 0); fetch(n, 1); fetch(n, 2);
     for (int i = 0; i < H; ++i) {
-      if (i == 0) wait_vmcnt<2>();              // rows -1..1 landed (row 2 in flight)
-      else if (i == 1) wait_vmcnt<2 + S>();     // row 2 (row 3, row-0 stores in flight)
-      else wait_vmcnt<2 + 2 * S>();             // row i+1 (rows i+2, stores of i-2, i-1)
+      // XF adds the xout stores (2 per row, rows 0 and 1 both in row 0) after
+      // each row's ring fetch; i == 2 waits two more than it must
+      if (i == 0) wait_vmcnt<2>();                           // rows -1..1 landed (row 2 in flight)
+      else if (i == 1) wait_vmcnt<2 + S + (XF ? 4 : 0)>();   // row 2 (row 3, row-0 stores in flight)
+      else wait_vmcnt<2 + 2 * S + (XF ? 4 : 0)>();           // row i+1 (rows i+2, stores of i-2, i-1)
       raw_barrier();                            // all waves: ring rows landed, row i-1 done
       // epilogue operands of this row (row-chunk epilogues): issued now, consumed
       // after the MFMAs, and BEFORE the ring fetch of row i+3 -- vmcnt retires in
@@ -1242,6 +1288,12 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
       // data gradient with the ReLU epilogue 641 -> 561 us, tools/conv_bench.py)
       constexpr bool kRowEpi = RowTrait<EP>::value;
       if constexpr (!kRowEpi) fetch(n, i + 3);
+      if constexpr (XF) {
+        if (i == 0) { xrow(n, 0); xrow(n, 1); }
+        else if (i + 1 < H) xrow(n, i + 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        raw_barrier();                          // transformed rows visible to every wave
+      }
       RowPre pre[2];
       if constexpr (kRowEpi) {
 #pragma unroll
@@ -1386,19 +1438,20 @@ static bool rows_c64_ok(const ConvGeom& g) {
   return !off && g.C == 64 && g.Co == 64 && g.KH == 3 && g.KW == 3 && g.S == 1 && g.P == 1 && g.W == kRcW &&
          g.H >= 3 && (size_t)g.N * g.H * kRcW * 128 < (1ull << 31);
 }
-template <class EP>
+template <class EP, bool XF = false>
 static int launch_rows_c64(const ConvGeom& g, const void* x, const void* w, int flip, const EP& ep,
-                           hipStream_t st) {
+                           hipStream_t st, const float* xsc = nullptr, const float* xsh = nullptr,
+                           void* xout = nullptr) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)&conv3x3_c64_rows_kernel<EP>,
+    (void)hipFuncSetAttribute((const void*)&conv3x3_c64_rows_kernel<EP, XF>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, kRcLds);
     attr = true;
   }
   int grid = device_cus();
   if (grid > g.N) grid = g.N;
-  hipLaunchKernelGGL((conv3x3_c64_rows_kernel<EP>), dim3(grid), dim3(512), kRcLds, st, g.N, g.H,
-                     (const bf16*)x, (const bf16*)w, flip, ep, g.N * g.H * g.W);
+  hipLaunchKernelGGL((conv3x3_c64_rows_kernel<EP, XF>), dim3(grid), dim3(512), kRcLds, st, g.N, g.H,
+                     (const bf16*)x, (const bf16*)w, flip, ep, g.N * g.H * g.W, xsc, xsh, (bf16*)xout);
   return (int)hipGetLastError();
 }
 
@@ -1752,6 +1805,26 @@ VLP_EXPORT int vlp_conv_fwd(int dtype, const void* x, const void* wp, void* y, i
   if (dtype == VLP_BF16)
     return conv_fwd_t<bf16>(x, wp, y, g, in_scale, in_shift, stat_sum, stat_sumsq, stat_rep, st);
   return conv_fwd_t<float>(x, wp, y, g, in_scale, in_shift, stat_sum, stat_sumsq, stat_rep, st);
+}
+
+VLP_EXPORT int vlp_conv_fwd_act_ok(int dtype, int N, int H, int W, int C, int Co, int KH, int KW, int S,
+                                  int P) {
+  return dtype == VLP_BF16 && N >= 1 && rows_c64_ok(make_geom(N, H, W, C, Co, KH, KW, S, P)) ? 1 : 0;
+}
+
+VLP_EXPORT int vlp_conv_fwd_act(int dtype, const void* x, const void* wp, void* y, void* x_act, int N,
+                                int H, int W, int C, int Co, int KH, int KW, int S, int P,
+                                const float* in_scale, const float* in_shift, double* stat_sum,
+                                double* stat_sumsq, int stat_rep, void* stream) {
+  if (!vlp_conv_fwd_act_ok(dtype, N, H, W, C, Co, KH, KW, S, P) || !in_scale || !in_shift || !x_act ||
+      !stat_sum || !stat_sumsq)
+    return (int)hipErrorInvalidValue;
+  ConvGeom g = make_geom(N, H, W, C, Co, KH, KW, S, P);
+  g.M = g.N * g.Ho * g.Wo;
+  g.K = g.KH * g.KW * g.C;
+  EpiConvFwd<bf16> ep{stat_sum, stat_sumsq, stat_rep, (bf16*)y, g.Co};
+  return launch_rows_c64<EpiConvFwd<bf16>, true>(g, x, wp, 0, ep, (hipStream_t)stream, in_scale, in_shift,
+                                                 x_act);
 }
 
 VLP_EXPORT int vlp_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, int N, int H,

@@ -58,6 +58,24 @@ def conv_fwd(x, wp, Co, KH, KW, S, P, in_scale=None, in_shift=None, stat_sum=Non
     return y
 
 
+def conv_fwd_act_ok(x, Co, KH, KW, S, P):
+    N, H, W, C = x.shape
+    return bool(lib()._dll.vlp_conv_fwd_act_ok(dcode(x), N, H, W, C, Co, KH, KW, S, P))
+
+
+def conv_fwd_act(x, wp, Co, KH, KW, S, P, in_scale, in_shift, x_act, stat_sum, stat_sumsq, stat_rep=1, out=None):
+    """conv(relu(in_scale*x + in_shift)) with that activation also written to x_act
+    (vlp_conv_fwd_act: BN-apply + ReLU fused into the layer-1 rows kernel)."""
+    N, H, W, C = x.shape
+    Ho, Wo = conv_out_hw(H, W, KH, KW, S, P)
+    y = out if out is not None else torch.empty((N, Ho, Wo, Co), dtype=x.dtype, device=x.device)
+    tk = ktimer.begin("conv_fwd[act]/narrow", 2.0 * N * Ho * Wo * Co * C * KH * KW)
+    lib().vlp_conv_fwd_act(dcode(x), ptr(x), ptr(wp), ptr(y), ptr(x_act), N, H, W, C, Co, KH, KW, S, P,
+                           ptr(in_scale), ptr(in_shift), ptr(stat_sum), ptr(stat_sumsq), int(stat_rep), _s())
+    ktimer.end(tk)
+    return y
+
+
 def conv_dgrad(dy, wt, H, W, C, KH, KW, S, P, addend=None, y_bn=None, bn=None, stat1=None,
                stat2=None, out=None, stat_rep=1):
     """bn = (scale, shift, mean, invstd) of the BN+ReLU producing the conv input."""

@@ -54,6 +54,9 @@ _USE_STEM1 = os.environ.get("VLP_STEM1", "1") != "0"
 # bf16: stem conv + BN sums + max-pool fused (stem_ops.hip); False keeps the
 # conv -> y0 -> max-pool kernels (tests compare the two)
 _USE_STEM_FUSED = True
+# bf16 layer 1: bn1 + ReLU applied in conv2's input ring (vlp_conv_fwd_act), a1
+# written by that kernel; False keeps the separate bn_add_relu pass
+_USE_ACT_FUSED = True
 
 
 def _side_stream(dev):
@@ -390,10 +393,15 @@ class ResNet34Tower(ArenaModule):
         Mb = y1.numel() // y1.shape[-1]
         sc1, sh1 = self._bn_finalize(ws, pre + ".bn1", Mb, training)
         a1 = torch.empty_like(y1)    # relu(bn1(y1)), materialised once: conv2 fwd + wgrad stream it
-        ops.bn_add_relu(y1, sc1, sh1, None, None, None, a1)
         s, ss = self._fstat(ws, pre + ".bn2", full=True)
-        y2 = ops.conv_fwd(a1, ws[c2.key + ".wp"], c2.Co, 3, 3, 1, 1, stat_sum=s, stat_sumsq=ss,
-                          stat_rep=STAT_REP)
+        if _USE_ACT_FUSED and ops.conv_fwd_act_ok(y1, c2.Co, 3, 3, 1, 1):
+            # layer 1: conv2 applies bn1 + ReLU to each input row once in its ring and writes a1
+            y2 = ops.conv_fwd_act(y1, ws[c2.key + ".wp"], c2.Co, 3, 3, 1, 1, sc1, sh1, a1, s, ss,
+                                  stat_rep=STAT_REP)
+        else:
+            ops.bn_add_relu(y1, sc1, sh1, None, None, None, a1)
+            y2 = ops.conv_fwd(a1, ws[c2.key + ".wp"], c2.Co, 3, 3, 1, 1, stat_sum=s, stat_sumsq=ss,
+                              stat_rep=STAT_REP)
         sc2, sh2 = self._bn_finalize(ws, pre + ".bn2", Mb, training)
         yd = scd = shd = None
         if has_ds:
