@@ -1241,16 +1241,17 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
     __syncthreads();
   }
   // ring row r (0 <= r < H) of image n -> relu(sc*x + sh), in place and to xout;
-  // thread t takes the fixed channel chunk t%8 of pixels t/8 and t/8 + 64
+  // each thread transforms the two 16-B chunks its own ring fetch wrote, so
+  // its vmcnt wait alone makes them readable (no barrier before the transform)
   auto xrow = [&](int n, int r) __attribute__((always_inline)) {
     char* slot = ring + ((r + 1) % kRcRing) * kRcSlot + 128;
-    const int cc = tid & 7;
-    const v4f s0 = *reinterpret_cast<const v4f*>(xtab + cc * 8), s1 = *reinterpret_cast<const v4f*>(xtab + cc * 8 + 4);
-    const v4f h0 = *reinterpret_cast<const v4f*>(xtab + 64 + cc * 8), h1 = *reinterpret_cast<const v4f*>(xtab + 68 + cc * 8);
 #pragma unroll
-    for (int h2 = 0; h2 < 2; ++h2) {
-      const int px = (tid >> 3) + 64 * h2;
-      uint4* p = reinterpret_cast<uint4*>(slot + px * 128 + ((cc ^ (((px + 1) >> 1) & 7)) << 4));
+    for (int jj = 0; jj < 2; ++jj) {
+      const int q = (wv * 2 + jj) * 64 + lane;
+      const int px = q >> 3, cc = (q & 7) ^ (((px + 1) >> 1) & 7);
+      const v4f s0 = *reinterpret_cast<const v4f*>(xtab + cc * 8), s1 = *reinterpret_cast<const v4f*>(xtab + cc * 8 + 4);
+      const v4f h0 = *reinterpret_cast<const v4f*>(xtab + 64 + cc * 8), h1 = *reinterpret_cast<const v4f*>(xtab + 68 + cc * 8);
+      uint4* p = reinterpret_cast<uint4*>(slot + q * 16);
       float f[8];
       Chunk<bf16>::unpack(*p, f);
 #pragma unroll
@@ -1275,12 +1276,17 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
     __syncthreads();
     fetch(n, -1); fetch(n, 0); fetch(n, 1); fetch(n, 2);
     for (int i = 0; i < H; ++i) {
-      // XF adds the xout stores (2 per row, rows 0 and 1 both in row 0) after
-      // each row's ring fetch; i == 2 waits two more than it must
+      // XF adds the xout stores (2 per row, rows 0 and 1 both in row 0) before
+      // each row's ring fetch
       if (i == 0) wait_vmcnt<2>();                           // rows -1..1 landed (row 2 in flight)
       else if (i == 1) wait_vmcnt<2 + S + (XF ? 4 : 0)>();   // row 2 (row 3, row-0 stores in flight)
-      else wait_vmcnt<2 + 2 * S + (XF ? 4 : 0)>();           // row i+1 (rows i+2, stores of i-2, i-1)
-      raw_barrier();                            // all waves: ring rows landed, row i-1 done
+      else wait_vmcnt<2 + 2 * S + (XF ? 2 : 0)>();           // row i+1 (rows i+2, stores of i-2, i-1)
+      if constexpr (XF) {
+        if (i == 0) { xrow(n, 0); xrow(n, 1); }
+        else if (i + 1 < H) xrow(n, i + 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+      raw_barrier();                            // all waves: ring rows landed (and transformed), row i-1 done
       // epilogue operands of this row (row-chunk epilogues): issued now, consumed
       // after the MFMAs, and BEFORE the ring fetch of row i+3 -- vmcnt retires in
       // issue order, so the epilogue's wait for them leaves that fetch in flight
@@ -1288,12 +1294,6 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
       // data gradient with the ReLU epilogue 641 -> 561 us, tools/conv_bench.py)
       constexpr bool kRowEpi = RowTrait<EP>::value;
       if constexpr (!kRowEpi) fetch(n, i + 3);
-      if constexpr (XF) {
-        if (i == 0) { xrow(n, 0); xrow(n, 1); }
-        else if (i + 1 < H) xrow(n, i + 1);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        raw_barrier();                          // transformed rows visible to every wave
-      }
       RowPre pre[2];
       if constexpr (kRowEpi) {
 #pragma unroll
