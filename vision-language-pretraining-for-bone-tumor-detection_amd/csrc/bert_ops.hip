@@ -506,14 +506,14 @@ struct AttnGeom {
 
 template <typename T>
 __device__ __forceinline__ void zero_lds(T* p, int n) {
-  for (int e = threadIdx.x & 63; e < n; e += 64) p[e] = from_f<T>(0.f);
+  for (int e = threadIdx.x; e < n; e += blockDim.x) p[e] = from_f<T>(0.f);
 }
 
 // rows t < Tn, channels d < dh of one head slice -> LDS image (row-major or transposed)
 template <typename T>
 __device__ __forceinline__ void load_head(T* dst, int ld, bool transpose, const T* src, size_t src_ld, int Tn,
                                           int dh) {
-  for (int e = threadIdx.x & 63; e < Tn * dh; e += 64) {
+  for (int e = threadIdx.x; e < Tn * dh; e += blockDim.x) {
     const int t = e / dh, d = e - t * dh;
     const T v = src[(size_t)t * src_ld + d];
     if (transpose) dst[d * ld + t] = v;
@@ -521,8 +521,17 @@ __device__ __forceinline__ void load_head(T* dst, int ld, bool transpose, const 
   }
 }
 
+// VLP_ATTN_MW: one wave per 16-query block of the (b, h) (TB waves per
+// workgroup: loads, the score/softmax rows and the output rows split across
+// them); 0 = the whole (b, h) on one wave
+#ifndef VLP_ATTN_MW
+#define VLP_ATTN_MW 1
+#endif
+template <int TB>
+constexpr int attn_waves() { return VLP_ATTN_MW ? TB : 1; }
+
 template <typename T, int TB>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(256)
 attn_fwd_kernel(int B, int Tn, int H, int dh, const T* __restrict__ qkv, const int64_t* __restrict__ amask,
                 T* __restrict__ ctx, float* __restrict__ P, float scale, float p, uint64_t seed) {
   using G = AttnGeom<T, TB>;
@@ -554,8 +563,9 @@ attn_fwd_kernel(int B, int Tn, int H, int dh, const T* __restrict__ qkv, const i
       const int j = jb * 16 + 4 * lg + r;
       kb[jb][r] = j >= Tn ? -INFINITY : (amask && amask[(size_t)b * Tn + j] == 0 ? -3.402823466e38f : 0.f);
     }
-#pragma unroll
-  for (int ib = 0; ib < TB; ++ib) {
+  constexpr int NW = attn_waves<TB>();
+  const int wv = NW > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
+  for (int ib = wv; ib < TB; ib += NW) {
     // S[i][j] for the 16 queries of block ib: lane holds query ib*16 + li, keys 4lg+r of each key block
     v4f s[TB];
 #pragma unroll
@@ -601,8 +611,7 @@ attn_fwd_kernel(int B, int Tn, int H, int dh, const T* __restrict__ qkv, const i
   }
   __syncthreads();
   // ctx[i][d] = sum_j P'[i][j] V[j][d]: X = V^T (rows d), Y = P' (rows i)
-#pragma unroll
-  for (int ib = 0; ib < TB; ++ib) {
+  for (int ib = wv; ib < TB; ib += NW) {
     const int i = ib * 16 + li;
 #pragma unroll
     for (int db = 0; db < 2; ++db) {
@@ -625,7 +634,7 @@ attn_fwd_kernel(int B, int Tn, int H, int dh, const T* __restrict__ qkv, const i
 //   dP' = dctx V^T ; dP = dP' * dropout mask ; dS = P (dP - rowsum(P dP))
 //   dq = scale * dS K ;  dk = scale * dS^T Q ;  dv = P'^T dctx
 template <typename T, int TB>
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(256)
 attn_bwd_kernel(int B, int Tn, int H, int dh, const T* __restrict__ qkv, const float* __restrict__ P,
                 const T* __restrict__ dctx, T* __restrict__ dqkv, float scale, float p, uint64_t seed) {
   using G = AttnGeom<T, TB>;
@@ -660,8 +669,9 @@ attn_bwd_kernel(int B, int Tn, int H, int dh, const T* __restrict__ qkv, const f
   load_head(sdOt, G::LT, true, dbase, Dm, Tn, dh);
   __syncthreads();
   const float* Pb = P + ((size_t)b * H + h) * Tn * Tn;
-#pragma unroll
-  for (int ib = 0; ib < TB; ++ib) {
+  constexpr int NW = attn_waves<TB>();
+  const int wv = NW > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
+  for (int ib = wv; ib < TB; ib += NW) {
     const int i = ib * 16 + li;
     // dP'[i][j] = sum_d dO[i][d] V[j][d]: X = V (rows j), Y = dO (rows i)
     v4f dp[TB];
@@ -698,8 +708,7 @@ attn_bwd_kernel(int B, int Tn, int H, int dh, const T* __restrict__ qkv, const f
       }
   }
   __syncthreads();
-#pragma unroll
-  for (int nb = 0; nb < TB; ++nb) {
+  for (int nb = wv; nb < TB; nb += NW) {
     const int t = nb * 16 + li;
 #pragma unroll
     for (int db = 0; db < 2; ++db) {
@@ -1067,13 +1076,13 @@ VLP_EXPORT int vlp_layernorm_bwd_add_rs(int dtype, int M, int D, const void* dy,
 template <typename T, int TB>
 static void launch_attn_fwd(int B, int Tn, int H, int dh, const void* qkv, const long long* amask, void* ctx,
                             float* P, float scale, float p, unsigned long long seed, hipStream_t st) {
-  hipLaunchKernelGGL((attn_fwd_kernel<T, TB>), dim3(B * H), dim3(64), 0, st, B, Tn, H, dh, (const T*)qkv,
+  hipLaunchKernelGGL((attn_fwd_kernel<T, TB>), dim3(B * H), dim3(64 * attn_waves<TB>()), 0, st, B, Tn, H, dh, (const T*)qkv,
                      (const int64_t*)amask, (T*)ctx, P, scale, p, (uint64_t)seed);
 }
 template <typename T, int TB>
 static void launch_attn_bwd(int B, int Tn, int H, int dh, const void* qkv, const float* P, const void* dctx,
                             void* dqkv, float scale, float p, unsigned long long seed, hipStream_t st) {
-  hipLaunchKernelGGL((attn_bwd_kernel<T, TB>), dim3(B * H), dim3(64), 0, st, B, Tn, H, dh, (const T*)qkv, P,
+  hipLaunchKernelGGL((attn_bwd_kernel<T, TB>), dim3(B * H), dim3(64 * attn_waves<TB>()), 0, st, B, Tn, H, dh, (const T*)qkv, P,
                      (const T*)dctx, (T*)dqkv, scale, p, (uint64_t)seed);
 }
 
