@@ -287,8 +287,8 @@ layernorm_fwd_kernel(int M, int D, const T* __restrict__ x, const float* __restr
 // strided over a capped grid so the gamma/beta partials stay in registers,
 // meet across the wave's four rows by shuffles and across the block in LDS,
 // then one atomic per column and block.
-template <typename T, int NCH>
-__global__ void __launch_bounds__(256)
+template <typename T, int NCH, int NW = 4>
+__global__ void __launch_bounds__(NW * 64)
 layernorm_bwd_kernel(int M, int D, const T* __restrict__ dy, float p_out, uint64_t seed_out,
                      const T* __restrict__ x, const float* __restrict__ mean,
                      const float* __restrict__ rstd, const float* __restrict__ gamma,
@@ -296,7 +296,7 @@ layernorm_bwd_kernel(int M, int D, const T* __restrict__ dy, float p_out, uint64
                      float* dgamma, float* dbeta, const T* __restrict__ addend,
                      const float* __restrict__ rscale, int rps) {
   constexpr int E = Chunk<T>::N;
-  __shared__ float part[4][2][512];
+  __shared__ float part[NW][2][512];
   const int j = threadIdx.x & 15, w = threadIdx.x >> 6;
   const int nch = D / E;
   float pg[NCH][E], pb[NCH][E], gm[NCH][E];
@@ -309,7 +309,7 @@ layernorm_bwd_kernel(int M, int D, const T* __restrict__ dy, float p_out, uint64
       gm[k][e] = c < nch ? gamma[c * E + e] : 0.f;
     }
   }
-  for (int row = blockIdx.x * 16 + (threadIdx.x >> 4); row < M; row += gridDim.x * 16) {
+  for (int row = blockIdx.x * (NW * 4) + (threadIdx.x >> 4); row < M; row += gridDim.x * (NW * 4)) {
     const T* xr = x + (size_t)row * D;
     const T* dyr = dy + (size_t)row * D;
     const float mu = mean[row], rs = rstd[row];
@@ -378,8 +378,11 @@ layernorm_bwd_kernel(int M, int D, const T* __restrict__ dy, float p_out, uint64
     }
   __syncthreads();
   for (int c = threadIdx.x; c < D; c += blockDim.x) {
-    atomicAdd(dgamma + c, part[0][0][c] + part[1][0][c] + part[2][0][c] + part[3][0][c]);
-    atomicAdd(dbeta + c, part[0][1][c] + part[1][1][c] + part[2][1][c] + part[3][1][c]);
+    float sg = 0.f, sb = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) { sg += part[q][0][c]; sb += part[q][1][c]; }
+    atomicAdd(dgamma + c, sg);
+    atomicAdd(dbeta + c, sb);
   }
 }
 
@@ -1017,6 +1020,9 @@ VLP_EXPORT int vlp_layernorm_fwd(int dtype, int M, int D, const void* x, const f
   return (int)hipGetLastError();
 }
 
+#ifndef VLP_LNB_TEXT_WAVES
+#define VLP_LNB_TEXT_WAVES 8   // waves per LayerNorm-backward block at text-sized M (4 = the NesT block)
+#endif
 template <typename T, int NCH>
 static void ln_bwd_t(int M, int D, const void* dy, float p_out, unsigned long long seed_out, const void* x,
                      const float* mean, const float* rstd, const float* gamma, void* dx, void* dxd, float p_in,
@@ -1028,6 +1034,17 @@ static void ln_bwd_t(int M, int D, const void* dy, float p_out, unsigned long lo
   // the cap applies to text-sized M only: NesT's 0.1-2 M token rows need the
   // wide grid for bandwidth (a 160 or M/2048 cap there: -3 % per NesT step)
   constexpr int cap = 160;   // LayerNorm-backward grid cap for text-sized M (atomic fan-in)
+  if (M <= 65536 && VLP_LNB_TEXT_WAVES > 4) {
+    // text-sized M: the capped grid with 8-wave blocks (32 rows per pass, twice the
+    // loads in flight per CU at the same atomic fan-in)
+    constexpr int NW = VLP_LNB_TEXT_WAVES;
+    int blocks = (M + NW * 4 - 1) / (NW * 4);
+    if (blocks > cap) blocks = cap;
+    hipLaunchKernelGGL((layernorm_bwd_kernel<T, NCH, NW>), dim3(blocks), dim3(NW * 64), 0, st, M, D, (const T*)dy,
+                       p_out, (uint64_t)seed_out, (const T*)x, mean, rstd, gamma, (T*)dx, (T*)dxd, p_in,
+                       (uint64_t)seed_in, dgamma, dbeta, (const T*)addend, rscale, rps);
+    return;
+  }
   int blocks = (M + 15) / 16;
   const int lim = M <= 65536 ? cap : 4096;
   if (blocks > lim) blocks = lim;
