@@ -1732,23 +1732,28 @@ __global__ void stem_prep_u8_kernel(const uint8_t* __restrict__ x, T* __restrict
 template <typename T>
 __global__ void stem1_prep_u8_kernel(const uint8_t* __restrict__ x, T* __restrict__ xs, Stem1Geom g, int H, int W,
                                      float mean, float inv_std) {
-  const size_t rows = 4 * (size_t)g.N * g.Hp;
-  const int cpr = g.Wp1 / 8;
-  const size_t total = rows * cpr;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int c = (int)(i % cpr);
-    const size_t row = i / cpr;
-    const int hp = (int)(row % g.Hp);
-    const size_t t = row / g.Hp;
-    const int n = (int)(t % g.N), sh = (int)(t / g.N);
+  // 32-bit index math (the host bounds 4 * copy elements below 2^31): the 64-bit
+  // divisions of a size_t grid-stride loop dominated this copy-rate kernel
+  const unsigned rows = 4u * (unsigned)g.N * (unsigned)g.Hp;
+  const unsigned cpr = (unsigned)g.Wp1 / 8u;
+  const unsigned total = rows * cpr;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const unsigned row = i / cpr;
+    const int c = (int)(i - row * cpr);
+    const unsigned t = row / (unsigned)g.Hp;
+    const int hp = (int)(row - t * (unsigned)g.Hp);
+    const unsigned sh = t / (unsigned)g.N;
+    const int n = (int)(t - sh * (unsigned)g.N);
     const int h = hp - 3;
+    const bool hin = h >= 0 && h < H;
+    const uint8_t* xr = x + ((size_t)n * H + (hin ? h : 0)) * W;
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int w = c * 8 + j + 2 * sh - 3;
-      v[j] = (h >= 0 && h < H && w >= 0 && w < W) ? ((float)x[((size_t)n * H + h) * W + w] - mean) * inv_std : 0.f;
+      const int w = c * 8 + j + 2 * (int)sh - 3;
+      v[j] = (hin && w >= 0 && w < W) ? ((float)xr[w] - mean) * inv_std : 0.f;
     }
-    T* dst = xs + row * g.Wp1 + c * 8;
+    T* dst = xs + (size_t)row * g.Wp1 + c * 8;
     if constexpr (sizeof(T) == 2) {
       stg16(dst, Chunk<bf16>::pack(v));
     } else {
