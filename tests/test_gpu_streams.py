@@ -16,6 +16,10 @@ noise of two stream-off steps when that is not 0 (an fp64 BN-sum atomic landing
 on a rounding boundary).
 Test B: bf16 NesT + TinyBERT step at 64^2, text stream on vs off: every
 gradient within max(1e-6, 4 x run-to-run noise of either schedule) rel-L2.
+Test C: bf16 ResNet34 + TinyBERT step at 512^2 (layer-1 width 128), layer-1
+bn1 + ReLU fused into conv2's ring (resnet34._USE_ACT_FUSED) vs the separate
+pass: the activation and conv2 output are bit-identical by construction, so
+every gradient and the loss stay within 4x the run-to-run noise.
 """
 import functools
 
@@ -113,3 +117,36 @@ def test_text_stream_matches_serial_nest_bf16():
     worst.sort()
     print("text stream on vs off, worst (excess, name, rel, tol):", worst[-3:])
     assert worst[-1][0] <= 0, worst[-3:]
+
+
+def test_layer1_act_fused_matches_pass_bf16():
+    from src.models.pretrain.VisionLanguageModule import VisionLanguageModule
+    from vlp_amd import resnet34 as r34
+    torch.manual_seed(2)
+    m = VisionLanguageModule("resnet34", "tinybert", functools.partial(torch.optim.AdamW, lr=5e-5), False, False,
+                             512, 312, 128, compute_dtype="bf16", text_dropout=0.0)
+    m.train()
+    with torch.no_grad():
+        for k, p in m.named_parameters():
+            if k.endswith("bn2.weight"):
+                p.fill_(0.5)
+    b = synth_batch(2, 512, 16, 7, with_u8=True)
+    b = {"x-ray-u8": b["x-ray-u8"].cuda(), "label": b["label"], "caption": b["caption"],
+         "caption_tokenized": {k: v.cuda() for k, v in b["caption_tokenized"].items()}}
+    was = r34._USE_ACT_FUSED
+    try:
+        r34._USE_ACT_FUSED = False
+        l0, g0 = _grads(m, b)
+        l1, g1 = _grads(m, b)
+        r34._USE_ACT_FUSED = True
+        l2, g2 = _grads(m, b)
+        l3, g3 = _grads(m, b)
+    finally:
+        r34._USE_ACT_FUSED = was
+    img = [k for k in g0 if k.startswith("image_encoder.")]
+    assert len(img) > 100
+    for k in img:
+        noise = max((g0[k] - g1[k]).abs().max().item(), (g2[k] - g3[k]).abs().max().item())
+        d = (g2[k] - g0[k]).abs().max().item()
+        assert d <= 4 * noise + 1e-30, (k, d, noise)
+    assert abs(l2 - l0) <= 4 * max(abs(l1 - l0), abs(l3 - l2)) + 1e-7, (l0, l1, l2, l3)
