@@ -877,6 +877,18 @@ struct EpiConvFwd {
 };
 // data gradient through the producer's ReLU (mask from BN-applied y), plus
 // that BN's backward statistics: sum(g), sum(g * xhat).
+// 16-B store of a row-chunk epilogue (VLP_ROW_NT: non-temporal, streaming past the caches)
+#ifndef VLP_ROW_NT
+#define VLP_ROW_NT 0
+#endif
+__device__ __forceinline__ void stg16_row(void* p, const uint4& v) {
+#if VLP_ROW_NT
+  typedef unsigned v4u_nt __attribute__((ext_vector_type(4)));
+  __builtin_nontemporal_store(v4u_nt{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u_nt*>(p));
+#else
+  stg16(p, v);
+#endif
+}
 template <typename T>
 struct EpiDgradBN {
   static constexpr bool kStats = true;
@@ -937,7 +949,7 @@ struct EpiDgradBN {
         s2[j] += g[j] * ((yv[j] - mu[jj]) * is[jj]);
       }
     }
-    stg16(g_out + o, Chunk<bf16>::pack(g));
+    stg16_row(g_out + o, Chunk<bf16>::pack(g));
   }
   static constexpr bool kStage = false;
   __device__ v4f value(int row, int col, v4f v, v4f& s1, v4f& s2) const {
@@ -982,7 +994,7 @@ struct EpiDgradAdd {
 #pragma unroll
       for (int j = 0; j < 8; ++j) d[j] += a[j];
     }
-    stg16(dx + o, Chunk<bf16>::pack(d));
+    stg16_row(dx + o, Chunk<bf16>::pack(d));
   }
   static constexpr bool kStage = false;
   __device__ v4f value(int row, int col, v4f v, v4f&, v4f&) const {
@@ -1083,7 +1095,7 @@ struct EpiDgradRelu {
       s1[j] += g[j];
       s2[j] += g[j] * ((yv[j] - mu[j]) * is[j]);
     }
-    stg16(g_out + o, Chunk<bf16>::pack(g));
+    stg16_row(g_out + o, Chunk<bf16>::pack(g));
   }
   static constexpr bool kStage = false;
   __device__ v4f value(int row, int col, v4f v, v4f& s1, v4f& s2) const { return grad(row, col, v, s1, s2); }
