@@ -31,6 +31,8 @@
 extern "C" {
 #endif
 
+/* 2 since r4 (r3 added ws / ws_floats to vlp_clip_loss_fused and made it write its
+ * outputs); the Python binding refuses any other value. */
 int vlp_abi_version(void);
 /* Diagnostic: register-only v_mfma_f32_16x16x32_bf16 chains (8 independent
  * accumulators per wave, 4 waves per block) to measure the card's dense bf16
@@ -248,7 +250,9 @@ int vlp_avgpool_fwd(int dtype, int N, int HW, int C, const void* x, void* feat, 
 /* ---------------- text tower (TinyBERT) ----------------
  * Replace the cuBLAS/ATen kernels of HF BertModel (VisionLanguageModule.py:45, :57-60). */
 /* y = x W^T + bias; mode 0 plain, 1 aux = pre-activation & y = gelu(aux),
- * 2 y = dropout_p(x W^T + bias) + res */
+ * 2 y = dropout_p(x W^T + bias) + res.  bf16 (also _rs and vlp_linear_dgrad): the
+ * output width and every output/operand leading dimension a multiple of 8 and the
+ * rows 16-byte aligned (8-column epilogue groups), else hipErrorInvalidValue. */
 int vlp_linear_fwd(int dtype, int M, int N, int K, const void* x, int ldx, const void* w,
                    const float* bias, void* y, int ldy, int mode, void* aux, const void* res,
                    int ldr, float p, unsigned long long seed, void* stream);
@@ -362,12 +366,13 @@ int vlp_clip_loss_finish(const float* parts, int N, float* out, void* stream);
 /* Fused global-batch symmetric InfoNCE, forward + backward (replaces the
  * logits matmul and the two F.cross_entropy calls of VisionLanguageModule.py
  * :456-459 / :550-552 with their autograd backward).  img_all/txt_all: [N][E]
- * gathered normalised embeddings (E <= 128); this rank owns rows
+ * gathered normalised embeddings (E <= 256, E % 4 == 0); this rank owns rows
  * [offset, offset+B).  Written (not accumulated): g_img_all/g_txt_all, d loss /
  * d embeddings for all N rows; d_logit_scale; loss_parts[0] the sum of the
  * image->text CE terms of the local rows, loss_parts[1] text->image; lse_out
  * (optional) [2][B].  ws: vlp_clip_loss_ws_floats(B, N, E) floats of scratch
- * (split-key partials and gradient slabs; no atomics, bitwise reproducible). */
+ * (cosines / softmax weights, split-key partials, dq slabs; every product on fp32
+ * MFMA; no atomics, bitwise reproducible).  ABI 2 (vlp_abi_version). */
 int vlp_clip_loss_ws_floats(int B, int N, int E, long long* n);
 int vlp_clip_loss_fused(int B, int N, int E, int offset, const float* img_all,
                         const float* txt_all, const float* logit_scale, float* g_img_all,

@@ -45,7 +45,7 @@ def test_library_loads_with_typed_bindings():
         fn = L._fns[name]
         assert len(fn.argtypes) == len(p["args"]), name
     # pure-host entry point: no device work
-    assert L._dll.vlp_abi_version() >= 1
+    assert L._dll.vlp_abi_version() == 2
 
 
 def test_every_declaration_cites_the_reference():

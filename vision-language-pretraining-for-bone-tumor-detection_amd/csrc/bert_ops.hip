@@ -818,6 +818,8 @@ VLP_EXPORT int vlp_linear_fwd(int dtype, int M, int N, int K, const void* x, int
                               void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (dtype == VLP_BF16) {
+    // the bf16 row-chunk epilogue moves 8-column groups with 16-B accesses
+    if (N % 8 || ldy % 8 || (res && ldr % 8)) return (int)hipErrorInvalidValue;
     KMat<bf16> la{(const bf16*)x, ldx, M, K};
     KMat<bf16> lb{(const bf16*)w, K, N, K};
     EpiLinear<bf16> ep{nullptr, nullptr, (bf16*)y, ldy, bias, mode, (bf16*)aux, (const bf16*)res, ldr, p, seed, N};
@@ -837,6 +839,7 @@ VLP_EXPORT int vlp_linear_fwd_rs(int dtype, int M, int N, int K, const void* x, 
   hipStream_t st = (hipStream_t)stream;
   if (!rscale || rps < 1) return (int)hipErrorInvalidValue;
   if (dtype == VLP_BF16) {
+    if (N % 8 || ldy % 8 || ldr % 8) return (int)hipErrorInvalidValue;
     KMat<bf16> la{(const bf16*)x, ldx, M, K};
     KMat<bf16> lb{(const bf16*)w, K, N, K};
     EpiLinear<bf16> ep{nullptr, nullptr, (bf16*)y, ldy, bias, 2, nullptr, (const bf16*)res, ldr, 0.f, 0, N, rscale, rps};
@@ -854,6 +857,7 @@ VLP_EXPORT int vlp_linear_dgrad(int dtype, int M, int Kin, int Nout, const void*
                                 int ldaux, const void* addend, int ldad, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (dtype == VLP_BF16) {
+    if (Kin % 8 || lddx % 8 || (aux && ldaux % 8) || (addend && ldad % 8)) return (int)hipErrorInvalidValue;
     KMat<bf16> la{(const bf16*)dy, lddy, M, Nout};
     MNMat<bf16> lb{(const bf16*)w, Kin, Kin, Nout};
     EpiLinearBwd<bf16> ep{nullptr, nullptr, (bf16*)dx, lddx, mode, (const bf16*)aux, ldaux, (const bf16*)addend, ldad};

@@ -9,225 +9,338 @@
 // (texts) of the N x N logits matrix (N = B * world, its rows start at
 // `offset`).  Role 0 covers the local image rows against all N texts (row
 // log-sum-exp, image->text CE), role 1 the local text columns against all N
-// images.  The key dimension is split over workgroups so that a global batch
-// of N = 2048 keeps the whole chip busy (2 roles x B/16 query blocks x N/64
-// key chunks), in three launches:
-//   1. clip_lse_part : per (query block, key chunk) the max and sum of exp of
-//                      the 16 x 64 logits tile  -> [2][B][nkc] partials
-//   2. clip_grad_part: the partials merged to each query's log-sum-exp, then
-//                      p = exp(l - lse), dl = (p - [i == j]) / (2N) and
-//                      dq_i = s * sum_j dl_ij k_j  -> slab [2][nkc][B][E]
-//                      dk_j = s * sum_i dl_ij q_i  -> slab [2][nqb][N][E]
-//                      ds   = sum dl_ij cos_ij     -> [2][nqb][nkc]
-//   3. clip_fold     : the slabs summed in a fixed order into the gathered
-//                      gradients g_img_all / g_txt_all (written, not added),
-//                      loss parts and d logit_scale.
+// images.  Every product runs on v_mfma_f32_16x16x4f32 (exact fp32 products,
+// fixed accumulation order), in three launches:
+//   1. clip_scores : per (role, 16-query block, 256-key chunk) the 16 x 256
+//                    dot products (one 16 x 64 tile per wave) -> the cosines
+//                    cos[2][Bp][Np] and the per-64-key partial max / sum of
+//                    exp(s * cos)                      -> pm, pl [2][Bp][Np/64]
+//   2. clip_dq     : the partials merged to each query's log-sum-exp; the
+//                    cosines (read, not recomputed) become
+//                    W = (exp(s cos - lse) - [i == j]) / (2N), written over
+//                    cos; dq_i = sum_j W_ij k_j over the chunk -> slab
+//                    [2][N/256][Bp][E]; sum W * cos -> [2][nqb][N/256]
+//   3. clip_dk     : per (role, 64-key block, column group) dk_j = sum_i W_ij
+//                    q_i over all local queries, plus (own rows) the dq slab
+//                    fold of the other role -> g_img_all / g_txt_all (written,
+//                    not added) = s * (dk + dq); block 0 also reduces the loss
+//                    parts and d logit_scale.
 // No atomics: the result is bitwise reproducible run to run.  The owner's
 // rows of the gathered gradients are then reduce-scattered by the host (RCCL).
+// MFMA operand convention (as in gemm.h): mfma(a, b, acc) with lane l = 16g + x
+// supplying a[x][k(g)] and b[y = x][k(g)] leaves acc[r] = sum_k a[4g + r][k] b[l & 15][k].
 #include "gemm.h"
 
 namespace vlp {
 
-constexpr int kQ = 16;        // queries per workgroup
-constexpr int kKC = 64;       // keys per workgroup
-constexpr int kMaxE = 128;
+constexpr int kQ = 16;        // queries per query block
+constexpr int kKT = 64;       // keys per wave tile (partials granularity)
+constexpr int kKC = 256;      // keys per workgroup in launches 1 and 2
+constexpr int kKB = 64;       // keys per workgroup in launch 3
+constexpr int kETW = 2;       // 16-column tiles per workgroup in launch 3
+constexpr int kMaxE = 256;
 
 struct ClipWs {               // float offsets into the workspace
-  size_t pm, pl, dq, dk, lterm, lse, ds, total;
+  size_t cw, pm, pl, dq, lterm, lse, ds, total;
+  int Bp, Np, nqb, nkt, nkc;
 };
 __host__ __device__ inline ClipWs clip_ws_layout(int B, int N, int E) {
-  const size_t nqb = (B + kQ - 1) / kQ, nkc = (N + kKC - 1) / kKC;
   ClipWs w;
-  w.pm = 0;
-  w.pl = w.pm + 2 * (size_t)B * nkc;
-  w.dq = w.pl + 2 * (size_t)B * nkc;
-  w.dk = w.dq + 2 * nkc * (size_t)B * E;
-  w.lterm = w.dk + 2 * nqb * (size_t)N * E;
-  w.lse = w.lterm + 2 * (size_t)B;
-  w.ds = w.lse + 2 * (size_t)B;
-  w.total = w.ds + 2 * nqb * nkc;
+  w.Bp = (B + kQ - 1) / kQ * kQ;
+  w.Np = (N + kKT - 1) / kKT * kKT;
+  w.nqb = w.Bp / kQ;
+  w.nkt = w.Np / kKT;
+  w.nkc = (N + kKC - 1) / kKC;
+  w.cw = 0;
+  w.pm = w.cw + 2 * (size_t)w.Bp * w.Np;
+  w.pl = w.pm + 2 * (size_t)w.Bp * w.nkt;
+  w.dq = w.pl + 2 * (size_t)w.Bp * w.nkt;
+  w.lterm = w.dq + 2 * (size_t)w.nkc * w.Bp * E;
+  w.lse = w.lterm + 2 * (size_t)w.Bp;
+  w.ds = w.lse + 2 * (size_t)w.Bp;
+  w.total = w.ds + 2 * (size_t)w.nqb * w.nkc;
   return w;
 }
 
-// Q[16][E] (this role's local queries) and K[64][E] (a key chunk) into LDS
-__device__ __forceinline__ void clip_stage(int B, int N, int E, int offset, int q0, int k0, const float* qsrc,
-                                           const float* ksrc, float (*Q)[kMaxE + 1], float (*K)[kMaxE + 1]) {
-  const int t = threadIdx.x;
-  for (int e = t; e < kQ * E; e += 256) {
-    const int i = e / E, d = e - i * E;
-    Q[i][d] = (q0 + i) < B ? qsrc[(size_t)(offset + q0 + i) * E + d] : 0.f;
-  }
-  for (int e = t; e < kKC * E; e += 256) {
-    const int j = e / E, d = e - j * E;
-    K[j][d] = (k0 + j) < N ? ksrc[(size_t)(k0 + j) * E + d] : 0.f;
-  }
+__device__ __forceinline__ v4f mfma4(float a, float b, v4f c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+// float4 of row `row` at column `col` (E % 4 == 0); zeros outside [0, rows) x [0, E)
+__device__ __forceinline__ v4f ld_row4(const float* base, int row, int rows, int col, int E) {
+  if (row < rows && col < E) return *reinterpret_cast<const v4f*>(base + (size_t)row * E + col);
+  return v4f{0.f, 0.f, 0.f, 0.f};
 }
 
-// thread (qi = t >> 4, kj = t & 15) computes the dot products of query qi with keys kj + 16r
-__device__ __forceinline__ void clip_dots(int E, int qi, int kj, const float (*Q)[kMaxE + 1],
-                                          const float (*K)[kMaxE + 1], float (&dot)[4]) {
-#pragma unroll
-  for (int r = 0; r < 4; ++r) dot[r] = 0.f;
-  for (int d = 0; d < E; ++d) {
-    const float qv = Q[qi][d];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) dot[r] = fmaf(qv, K[kj + 16 * r][d], dot[r]);
-  }
-}
-
+// Launch 1.  Wave w: keys k0 = kc * 256 + 64 w, 4 sub-tiles of 16 keys.  Lane
+// l = 16g + i holds the cosines of query i with keys k0 + 16t + 4g + r (t, r in
+// 0..3) -- written as float4 rows of cw.
+template <int NCH>
 __global__ void __launch_bounds__(256)
-clip_lse_part_kernel(int B, int N, int E, int offset, const float* __restrict__ img_all,
-                     const float* __restrict__ txt_all, const float* __restrict__ logit_scale,
-                     float* __restrict__ ws) {
-  __shared__ float Q[kQ][kMaxE + 1];
-  __shared__ float K[kKC][kMaxE + 1];
-  const int nqb = (B + kQ - 1) / kQ, nkc = (N + kKC - 1) / kKC;
-  const int role = blockIdx.x / (nqb * nkc);
-  const int rem = blockIdx.x - role * nqb * nkc;
-  const int qb = rem / nkc, kc = rem - qb * nkc;
-  const int q0 = qb * kQ, k0 = kc * kKC;
-  clip_stage(B, N, E, offset, q0, k0, role == 0 ? img_all : txt_all, role == 0 ? txt_all : img_all, Q, K);
-  __syncthreads();
+clip_scores_kernel(int B, int N, int E, int offset, const float* __restrict__ img_all,
+                   const float* __restrict__ txt_all, const float* __restrict__ logit_scale,
+                   float* __restrict__ ws) {
+  const ClipWs L = clip_ws_layout(B, N, E);
+  const int per_role = L.nqb * L.nkc;
+  const int role = blockIdx.x / per_role;
+  const int rem = blockIdx.x - role * per_role;
+  const int qb = rem / L.nkc, kc = rem - qb * L.nkc;
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int x = l & 15, g = l >> 4;
+  const int q0 = qb * kQ, k0 = kc * kKC + w * kKT;
+  if (k0 >= L.Np) return;
+  const float* qsrc = (role == 0 ? img_all : txt_all) + (size_t)offset * E;
+  const float* ksrc = role == 0 ? txt_all : img_all;
   const float s = fminf(expf(logit_scale[0]), 100.f);
-  const int t = threadIdx.x, qi = t >> 4, kj = t & 15;
-  float dot[4];
-  clip_dots(E, qi, kj, Q, K, dot);
+  v4f qv[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) qv[c] = ld_row4(qsrc, q0 + x, B, 16 * c + 4 * g, E);
+  v4f acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    v4f kv[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) kv[c] = ld_row4(ksrc, k0 + 16 * t + x, N, 16 * c + 4 * g, E);
+    acc[t] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[t] = mfma4(kv[c][r], qv[c][r], acc[t]);
+  }
+  // acc[t][r] = cos(query q0 + x, key k0 + 16t + 4g + r)
+  float* cw = ws + L.cw + ((size_t)role * L.Bp + q0 + x) * L.Np + k0;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) *reinterpret_cast<v4f*>(cw + 16 * t + 4 * g) = acc[t];
   float m = -INFINITY;
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
-    if (k0 + kj + 16 * r < N) m = fmaxf(m, s * dot[r]);
+  for (int t = 0; t < 4; ++t)
 #pragma unroll
-  for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-  float l = 0.f;
+    for (int r = 0; r < 4; ++r)
+      if (k0 + 16 * t + 4 * g + r < N) m = fmaxf(m, s * acc[t][r]);
+  m = fmaxf(m, __shfl_xor(m, 16, 64));
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  float sum = 0.f;
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
-    if (k0 + kj + 16 * r < N) l += expf(s * dot[r] - m);
+  for (int t = 0; t < 4; ++t)
 #pragma unroll
-  for (int o = 1; o < 16; o <<= 1) l += __shfl_xor(l, o, 64);
-  if (kj == 0 && q0 + qi < B) {
-    const ClipWs L = clip_ws_layout(B, N, E);
-    const size_t o = ((size_t)role * B + q0 + qi) * nkc + kc;
+    for (int r = 0; r < 4; ++r)
+      if (k0 + 16 * t + 4 * g + r < N) sum += expf(s * acc[t][r] - m);
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
+  if (g == 0 && q0 + x < B) {
+    const size_t o = ((size_t)role * L.Bp + q0 + x) * L.nkt + k0 / kKT;
     ws[L.pm + o] = m;
-    ws[L.pl + o] = l;
+    ws[L.pl + o] = sum;
   }
 }
 
+// Launch 2.  Same grid as launch 1; wave w owns keys k0 = kc * 256 + 64 w in two
+// halves of 32 staged in LDS ([32][E + 4] per wave).  Lane l = 16g + i: query i.
+template <int NCH>
 __global__ void __launch_bounds__(256)
-clip_grad_part_kernel(int B, int N, int E, int offset, const float* __restrict__ img_all,
-                      const float* __restrict__ txt_all, const float* __restrict__ logit_scale,
-                      float* __restrict__ ws) {
-  __shared__ float Q[kQ][kMaxE + 1];
-  __shared__ float K[kKC][kMaxE + 1];
-  __shared__ float Wt[kQ][kKC + 1];
-  __shared__ float red[4];
-  const int nqb = (B + kQ - 1) / kQ, nkc = (N + kKC - 1) / kKC;
-  const int role = blockIdx.x / (nqb * nkc);
-  const int rem = blockIdx.x - role * nqb * nkc;
-  const int qb = rem / nkc, kc = rem - qb * nkc;
-  const int q0 = qb * kQ, k0 = kc * kKC;
+clip_dq_kernel(int B, int N, int E, int offset, const float* __restrict__ img_all,
+               const float* __restrict__ txt_all, const float* __restrict__ logit_scale,
+               float* __restrict__ ws) {
+  constexpr int EP = NCH * 16 + 4;                       // LDS row stride (floats)
+  __shared__ __attribute__((aligned(16))) float lds[4 * 32 * EP];
+  __shared__ float red_ds[4];
   const ClipWs L = clip_ws_layout(B, N, E);
-  clip_stage(B, N, E, offset, q0, k0, role == 0 ? img_all : txt_all, role == 0 ? txt_all : img_all, Q, K);
+  const int per_role = L.nqb * L.nkc;
+  const int role = blockIdx.x / per_role;
+  const int rem = blockIdx.x - role * per_role;
+  const int qb = rem / L.nkc, kc = rem - qb * L.nkc;
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int x = l & 15, g = l >> 4;
+  const int q0 = qb * kQ, k0 = kc * kKC + w * kKT;
+  const bool active = k0 < L.Np;
+  const bool qvalid = q0 + x < B;
+  const float* ksrc = role == 0 ? txt_all : img_all;
   const float s = fminf(expf(logit_scale[0]), 100.f);
   const float inv2n = 0.5f / (float)N;
-  const int t = threadIdx.x, qi = t >> 4, kj = t & 15;
-  const bool qvalid = q0 + qi < B;
-  // this query's log-sum-exp from the key-chunk partials (16 lanes share the merge)
-  float m = -INFINITY, l = 0.f;
+  // this query's log-sum-exp from the 64-key partials (lane groups g stride them)
+  float m = -INFINITY, sl = 0.f;
   if (qvalid) {
-    const size_t base = ((size_t)role * B + q0 + qi) * nkc;
-    for (int c = kj; c < nkc; c += 16) {
+    const size_t base = ((size_t)role * L.Bp + q0 + x) * L.nkt;
+    for (int c = g; c < L.nkt; c += 4) {
       const float m2 = ws[L.pm + base + c], l2 = ws[L.pl + base + c];
+      if (m2 == -INFINITY) continue;
       const float mn = fmaxf(m, m2);
-      l = (m == -INFINITY ? 0.f : l * expf(m - mn)) + l2 * expf(m2 - mn);
+      sl = (m == -INFINITY ? 0.f : sl * expf(m - mn)) + l2 * expf(m2 - mn);
       m = mn;
     }
   }
 #pragma unroll
-  for (int o = 1; o < 16; o <<= 1) {
-    const float m2 = __shfl_xor(m, o, 64), l2 = __shfl_xor(l, o, 64);
+  for (int o = 16; o < 64; o <<= 1) {
+    const float m2 = __shfl_xor(m, o, 64), l2 = __shfl_xor(sl, o, 64);
     const float mn = fmaxf(m, m2);
-    l = (m == -INFINITY ? 0.f : l * expf(m - mn)) + (m2 == -INFINITY ? 0.f : l2 * expf(m2 - mn));
+    sl = (m == -INFINITY ? 0.f : sl * expf(m - mn)) + (m2 == -INFINITY ? 0.f : l2 * expf(m2 - mn));
     m = mn;
   }
-  const float lse = m + logf(l);
-  if (kc == 0 && kj == 0 && qvalid) ws[L.lse + (size_t)role * B + q0 + qi] = lse;
-  __syncthreads();
-  float dot[4];
-  clip_dots(E, qi, kj, Q, K, dot);
-  const int qglob = offset + q0 + qi;
+  const float lse = qvalid ? m + logf(sl) : 0.f;
+  if (kc == 0 && w == 0 && g == 0 && qvalid) ws[L.lse + (size_t)role * L.Bp + q0 + x] = lse;
+  const int qglob = offset + q0 + x;
+  float* kl = lds + w * 32 * EP;
+  float* cwrow = ws + L.cw + ((size_t)role * L.Bp + q0 + x) * L.Np;
+  v4f acc[NCH];
+#pragma unroll
+  for (int t = 0; t < NCH; ++t) acc[t] = v4f{0.f, 0.f, 0.f, 0.f};
   float ds = 0.f;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int j = kj + 16 * r;
-    float w = 0.f;
-    if (qvalid && k0 + j < N) {
-      const float lg = s * dot[r];
-      const bool diag = k0 + j == qglob;
-      w = (expf(lg - lse) - (diag ? 1.f : 0.f)) * inv2n;
-      ds = fmaf(w, dot[r], ds);
-      if (diag) ws[L.lterm + (size_t)role * B + q0 + qi] = lse - lg;
+#pragma unroll 1
+  for (int h = 0; h < 2; ++h) {
+    const int j0 = k0 + 32 * h;
+    if (active) {
+      // stage keys j0 .. j0 + 31 (zero rows past N): 32 x NCH*16 floats, float4 per lane
+      for (int e = l; e < 32 * NCH * 4; e += 64) {
+        const int row = e / (NCH * 4), c4 = e - row * (NCH * 4);
+        *reinterpret_cast<v4f*>(kl + row * EP + 4 * c4) = ld_row4(ksrc, j0 + row, N, 4 * c4, E);
+      }
     }
-    Wt[qi][j] = w;
-  }
-  ds = warp_sum(ds);
-  if ((t & 63) == 0) red[t >> 6] = ds;
-  __syncthreads();
-  if (t == 0) ws[L.ds + ((size_t)role * nqb + qb) * nkc + kc] = (red[0] + red[1]) + (red[2] + red[3]);
-  // dq[i][d] = s * sum_j W[i][j] K[j][d]  (this chunk's part; 8 outputs per thread for E = 128)
-  for (int o = t; o < kQ * E; o += 256) {
-    const int i = o / E, d = o - i * E;
-    if (q0 + i >= B) continue;
-    float a = 0.f;
-#pragma unroll 8
-    for (int j = 0; j < kKC; ++j) a = fmaf(Wt[i][j], K[j][d], a);
-    ws[L.dq + (((size_t)role * nkc + kc) * B + q0 + i) * E + d] = s * a;
-  }
-  // dk[j][d] = s * sum_i W[i][j] Q[i][d]  (this query block's part)
-  for (int o = t; o < kKC * E; o += 256) {
-    const int j = o / E, d = o - j * E;
-    if (k0 + j >= N) continue;
-    float a = 0.f;
+    __syncthreads();
+    if (active) {
+      v4f wv[2];
 #pragma unroll
-    for (int i = 0; i < kQ; ++i) a = fmaf(Wt[i][j], Q[i][d], a);
-    ws[L.dk + (((size_t)role * nqb + qb) * N + k0 + j) * E + d] = s * a;
+      for (int u = 0; u < 2; ++u) {
+        const int jb = j0 + 16 * u + 4 * g;
+        const v4f cv = *reinterpret_cast<const v4f*>(cwrow + jb);
+        v4f wr;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float wt = 0.f;
+          if (qvalid && jb + r < N) {
+            const float lg = s * cv[r];
+            const bool diag = jb + r == qglob;
+            wt = (expf(lg - lse) - (diag ? 1.f : 0.f)) * inv2n;
+            ds = fmaf(wt, cv[r], ds);
+            if (diag) ws[L.lterm + (size_t)role * L.Bp + q0 + x] = lse - lg;
+          }
+          wr[r] = wt;
+        }
+        wv[u] = wr;
+        *reinterpret_cast<v4f*>(cwrow + jb) = wr;          // W replaces the cosines (launch 3 reads it)
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float* krow = kl + (16 * u + 4 * g + r) * EP + x;
+#pragma unroll
+          for (int t = 0; t < NCH; ++t) acc[t] = mfma4(wv[u][r], krow[16 * t], acc[t]);
+        }
+    }
+    __syncthreads();
   }
+  // acc[t][r] = sum over this wave's keys of W[q0 + 4g + r][j] k_j[16t + x]; fold the 4 waves
+  float* red = lds;                                   // [4][16][NCH*16]
+  constexpr int EW = NCH * 16;
+#pragma unroll
+  for (int t = 0; t < NCH; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[(w * 16 + 4 * g + r) * EW + 16 * t + x] = acc[t][r];
+  ds = warp_sum(ds);
+  if (l == 0) red_ds[w] = ds;
+  __syncthreads();
+  float* dq = ws + L.dq + (((size_t)role * L.nkc + kc) * L.Bp + q0) * E;
+  for (int o = threadIdx.x; o < 16 * E; o += 256) {
+    const int i = o / E, e = o - i * E;
+    dq[(size_t)i * E + e] = (red[i * EW + e] + red[(16 + i) * EW + e]) + (red[(32 + i) * EW + e] + red[(48 + i) * EW + e]);
+  }
+  if (threadIdx.x == 0)
+    ws[L.ds + ((size_t)role * L.nqb + qb) * L.nkc + kc] = (red_ds[0] + red_ds[1]) + (red_ds[2] + red_ds[3]);
 }
 
-// g_img_all[r] = sum_qb dk[role 1][qb][r] + (own row ? sum_kc dq[role 0][kc][r - offset] : 0);
-// g_txt_all likewise with the roles swapped.  Block 0 also writes the loss parts
-// (sum of lse - diag over the local queries), d logit_scale and lse_out.
+// Launch 3.  Workgroup (role, 64-key block kb, column group eg of kETW 16-wide
+// tiles); wave w owns keys kb * 64 + 16 w.  W [64 queries][64 keys] and the
+// queries' columns are staged per 64-query chunk.  Lane l = 16g + x holds
+// dk[key 16w + 4g + r][column 16t + x].
 __global__ void __launch_bounds__(256)
-clip_fold_kernel(int B, int N, int E, int offset, const float* __restrict__ logit_scale,
-                 const float* __restrict__ ws, float* __restrict__ g_img_all, float* __restrict__ g_txt_all,
-                 float* __restrict__ d_logit_scale, float* __restrict__ loss_parts, float* __restrict__ lse_out) {
-  const int nqb = (B + kQ - 1) / kQ, nkc = (N + kKC - 1) / kKC;
+clip_dk_kernel(int B, int N, int E, int offset, const float* __restrict__ img_all,
+               const float* __restrict__ txt_all, const float* __restrict__ logit_scale,
+               const float* __restrict__ ws, float* __restrict__ g_img_all, float* __restrict__ g_txt_all,
+               float* __restrict__ d_logit_scale, float* __restrict__ loss_parts, float* __restrict__ lse_out) {
+  constexpr int WP = kKB + 4, QP = 16 * kETW + 4;
+  __shared__ __attribute__((aligned(16))) float Ws[64 * WP];
+  __shared__ __attribute__((aligned(16))) float Qs[64 * QP];
   const ClipWs L = clip_ws_layout(B, N, E);
-  const size_t per = (size_t)N * E;
-  for (size_t o = blockIdx.x * (size_t)blockDim.x + threadIdx.x; o < 2 * per; o += (size_t)gridDim.x * blockDim.x) {
-    const int tensor = (int)(o / per);        // 0: g_img_all, 1: g_txt_all
-    const size_t e = o - tensor * per;
-    const int r = (int)(e / E), d = (int)(e - (size_t)r * E);
-    const int krole = 1 - tensor, qrole = tensor;
-    float a = 0.f;
-    for (int qb = 0; qb < nqb; ++qb) a += ws[L.dk + (((size_t)krole * nqb + qb) * N + r) * E + d];
-    if (r >= offset && r < offset + B)
-      for (int kc = 0; kc < nkc; ++kc) a += ws[L.dq + (((size_t)qrole * nkc + kc) * B + (r - offset)) * E + d];
-    (tensor == 0 ? g_img_all : g_txt_all)[e] = a;
+  const int ncg = (E + 16 * kETW - 1) / (16 * kETW);
+  const int nkb = L.Np / kKB;
+  const int per_role = nkb * ncg;
+  const int role = blockIdx.x / per_role;
+  const int rem = blockIdx.x - role * per_role;
+  const int kb = rem / ncg, eg = rem - kb * ncg;
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int x = l & 15, g = l >> 4;
+  const int j0 = kb * kKB, c0 = eg * 16 * kETW;
+  const float* qsrc = (role == 0 ? img_all : txt_all) + (size_t)offset * E;
+  const float* cw = ws + L.cw + (size_t)role * L.Bp * L.Np;
+  v4f acc[kETW];
+#pragma unroll
+  for (int t = 0; t < kETW; ++t) acc[t] = v4f{0.f, 0.f, 0.f, 0.f};
+  for (int i0 = 0; i0 < L.Bp; i0 += 64) {
+    for (int e = threadIdx.x; e < 64 * 16; e += 256) {     // W rows i0.., 16 float4 per row
+      const int row = e >> 4, c4 = e & 15;
+      v4f v = v4f{0.f, 0.f, 0.f, 0.f};
+      if (i0 + row < L.Bp) v = *reinterpret_cast<const v4f*>(cw + (size_t)(i0 + row) * L.Np + j0 + 4 * c4);
+      *reinterpret_cast<v4f*>(Ws + row * WP + 4 * c4) = v;
+    }
+    for (int e = threadIdx.x; e < 64 * 4 * kETW; e += 256) {
+      const int row = e / (4 * kETW), c4 = e - row * (4 * kETW);
+      *reinterpret_cast<v4f*>(Qs + row * QP + 4 * c4) = ld_row4(qsrc, i0 + row, B, c0 + 4 * c4, E);
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int kk = 0; kk < 16; ++kk)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * kk + 4 * g + r;
+        const float a = Ws[i * WP + 16 * w + x];
+#pragma unroll
+        for (int t = 0; t < kETW; ++t) acc[t] = mfma4(a, Qs[i * QP + 16 * t + x], acc[t]);
+      }
+    __syncthreads();
   }
-  if (blockIdx.x == 0 && threadIdx.x < 2) {
-    const int role = threadIdx.x;
-    float lt = 0.f;
-    for (int q = 0; q < B; ++q) lt += ws[L.lterm + (size_t)role * B + q];
-    loss_parts[role] = lt;
-    if (role == 0) {
-      float ds = 0.f;
-      for (size_t i = 0; i < 2 * (size_t)nqb * nkc; ++i) ds += ws[L.ds + i];
-      const float ex = expf(logit_scale[0]);
-      d_logit_scale[0] = ex <= 100.f ? ds * fminf(ex, 100.f) : 0.f;
+  const float s = fminf(expf(logit_scale[0]), 100.f);
+  float* gout = role == 0 ? g_txt_all : g_img_all;       // keys of role 0 are texts
+  const int orole = 1 - role;                            // its queries are this tensor's own rows
+  const float* dq = ws + L.dq + (size_t)orole * L.nkc * L.Bp * E;
+#pragma unroll
+  for (int t = 0; t < kETW; ++t) {
+    const int col = c0 + 16 * t + x;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = j0 + 16 * w + 4 * g + r;
+      if (j >= N || col >= E) continue;
+      float a = acc[t][r];
+      if (j >= offset && j < offset + B) {
+        float f = 0.f;
+        for (int c = 0; c < L.nkc; ++c) f += dq[((size_t)c * L.Bp + (j - offset)) * E + col];
+        a += f;
+      }
+      gout[(size_t)j * E + col] = s * a;
     }
   }
-  if (lse_out && blockIdx.x == 0)
-    for (int q = threadIdx.x; q < 2 * B; q += blockDim.x) lse_out[q] = ws[L.lse + q];
+  if (blockIdx.x == 0 && w == 0) {
+    // loss parts, d logit_scale and lse_out: fixed-order lane-strided sums + xor tree
+    float lt0 = 0.f, lt1 = 0.f, dsum = 0.f;
+    for (int q = l; q < B; q += 64) {
+      lt0 += ws[L.lterm + q];
+      lt1 += ws[L.lterm + L.Bp + q];
+    }
+    const int nds = L.nqb * L.nkc;
+    for (int i = l; i < 2 * nds; i += 64) dsum += ws[L.ds + i];
+    lt0 = warp_sum(lt0);
+    lt1 = warp_sum(lt1);
+    dsum = warp_sum(dsum);
+    if (l == 0) {
+      loss_parts[0] = lt0;
+      loss_parts[1] = lt1;
+      const float ex = expf(logit_scale[0]);
+      d_logit_scale[0] = ex <= 100.f ? dsum * fminf(ex, 100.f) : 0.f;
+    }
+    if (lse_out)
+      for (int q = l; q < B; q += 64) {
+        lse_out[q] = ws[L.lse + q];
+        lse_out[B + q] = ws[L.lse + L.Bp + q];
+      }
+  }
 }
 
 // row-wise L2 normalisation (F.normalize, p=2, dim=1, eps=1e-12)
@@ -321,7 +434,7 @@ __global__ void cast_kernel(size_t n, const float* __restrict__ x, T* __restrict
 using namespace vlp;
 
 VLP_EXPORT int vlp_clip_loss_ws_floats(int B, int N, int E, long long* n) {
-  if (B < 1 || N < B || E < 1 || E > kMaxE) return (int)hipErrorInvalidValue;
+  if (B < 1 || N < B || E < 4 || E > kMaxE || E % 4) return (int)hipErrorInvalidValue;
   *n = (long long)clip_ws_layout(B, N, E).total;
   return 0;
 }
@@ -330,19 +443,22 @@ VLP_EXPORT int vlp_clip_loss_fused(int B, int N, int E, int offset, const float*
                                    const float* txt_all, const float* logit_scale, float* g_img_all,
                                    float* g_txt_all, float* d_logit_scale, float* loss_parts,
                                    float* lse_out, float* ws, long long ws_floats, void* stream) {
-  if (B < 1 || N < B || E < 1 || E > kMaxE || offset < 0 || offset + B > N) return (int)hipErrorInvalidValue;
-  if ((long long)clip_ws_layout(B, N, E).total > ws_floats) return (int)hipErrorInvalidValue;
+  if (B < 1 || N < B || E < 4 || E > kMaxE || E % 4 || offset < 0 || offset + B > N)
+    return (int)hipErrorInvalidValue;
+  const ClipWs L = clip_ws_layout(B, N, E);
+  if ((long long)L.total > ws_floats) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
-  const int nqb = (B + kQ - 1) / kQ, nkc = (N + kKC - 1) / kKC;
-  const dim3 grid(2 * nqb * nkc);
-  hipLaunchKernelGGL(clip_lse_part_kernel, grid, dim3(256), 0, st, B, N, E, offset, img_all, txt_all, logit_scale,
-                     ws);
-  hipLaunchKernelGGL(clip_grad_part_kernel, grid, dim3(256), 0, st, B, N, E, offset, img_all, txt_all,
-                     logit_scale, ws);
-  int fb = (int)((2 * (size_t)N * E + 255) / 256);
-  if (fb > 2048) fb = 2048;
-  hipLaunchKernelGGL(clip_fold_kernel, dim3(fb), dim3(256), 0, st, B, N, E, offset, logit_scale, ws, g_img_all,
-                     g_txt_all, d_logit_scale, loss_parts, lse_out);
+  const dim3 g12(2 * L.nqb * L.nkc);
+  if (E <= 128) {
+    hipLaunchKernelGGL(clip_scores_kernel<8>, g12, dim3(256), 0, st, B, N, E, offset, img_all, txt_all, logit_scale, ws);
+    hipLaunchKernelGGL(clip_dq_kernel<8>, g12, dim3(256), 0, st, B, N, E, offset, img_all, txt_all, logit_scale, ws);
+  } else {
+    hipLaunchKernelGGL(clip_scores_kernel<16>, g12, dim3(256), 0, st, B, N, E, offset, img_all, txt_all, logit_scale, ws);
+    hipLaunchKernelGGL(clip_dq_kernel<16>, g12, dim3(256), 0, st, B, N, E, offset, img_all, txt_all, logit_scale, ws);
+  }
+  const int ncg = (E + 16 * kETW - 1) / (16 * kETW);
+  hipLaunchKernelGGL(clip_dk_kernel, dim3(2 * (L.Np / kKB) * ncg), dim3(256), 0, st, B, N, E, offset, img_all,
+                     txt_all, logit_scale, (const float*)ws, g_img_all, g_txt_all, d_logit_scale, loss_parts, lse_out);
   return (int)hipGetLastError();
 }
 

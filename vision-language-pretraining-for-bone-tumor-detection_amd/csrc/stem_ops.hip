@@ -849,12 +849,10 @@ VLP_EXPORT int vlp_stem1_bwd_fused(const void* xs, const void* wp1, const void* 
   const int cw = stem1_gram_cw(g.Wo);
   if (cw == 128) {
     constexpr size_t lds = 4 * 128 * 128;
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)&stem1_bwd_gram_kernel<128>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds);
-      attr = true;
-    }
+    // per device and cheap: set on every call (a process-wide flag missed a second GPU)
+    const hipError_t ae = hipFuncSetAttribute((const void*)&stem1_bwd_gram_kernel<128>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (ae != hipSuccess) return (int)ae;
     hipLaunchKernelGGL(stem1_bwd_gram_kernel<128>, dim3(nwg), dim3(512), lds, st, g, (const bf16*)xs, Hq, Wq,
                        (const bf16*)dp, idx, ws);
   } else {

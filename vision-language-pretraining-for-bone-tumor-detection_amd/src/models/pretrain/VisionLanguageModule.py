@@ -542,16 +542,18 @@ class VisionLanguageModule(_Base):
         return loss
 
     def on_validation_epoch_end(self):
-        if self._val_loss_n:
-            # the reference's MeanMetric syncs across ranks: sum and count over every rank
-            tot = torch.stack([self._val_loss_sum.double().reshape(()),
-                               torch.tensor(float(self._val_loss_n), dtype=torch.float64,
-                                            device=self._val_loss_sum.device)])
-            d = torch.distributed
-            if d.is_available() and d.is_initialized() and d.get_world_size() > 1:
-                dev = self._val_loss_sum.device if d.get_backend() == "nccl" else torch.device("cpu")
-                tot = tot.to(dev)
-                d.all_reduce(tot)
+        # the reference's MeanMetric syncs across ranks: sum and count over every rank.  The
+        # collective runs on every rank, also one that saw no validation batch (zeros)
+        dev = self._val_loss_sum.device if self._val_loss_sum is not None else self.device
+        tot = torch.stack([self._val_loss_sum.double().reshape(()) if self._val_loss_sum is not None
+                           else torch.zeros((), dtype=torch.float64, device=dev),
+                           torch.tensor(float(self._val_loss_n), dtype=torch.float64, device=dev)])
+        d = torch.distributed
+        if d.is_available() and d.is_initialized() and d.get_world_size() > 1:
+            cdev = tot.device if d.get_backend() == "nccl" else torch.device("cpu")
+            tot = tot.to(cdev)
+            d.all_reduce(tot)
+        if tot[1].item() > 0:
             self.log("val/combined/loss", (tot[0] / tot[1]).float(), prog_bar=True)
         ie, te, labels = self._get_cached_embeddings_and_labels(mode="val")
         for k, v in self.precision_at_k_on_image_embeddings(ie, labels, ks=self.k_for_precision_at_k).items():

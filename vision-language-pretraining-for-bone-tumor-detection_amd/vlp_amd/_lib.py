@@ -22,6 +22,7 @@ LIB_PATH = os.environ.get("VLP_HIP_LIB", os.path.join(_HERE, "libvlp_hip.so"))
 HEADER_PATH = os.path.join(_REPO, "include", "vlp_hip.h")
 
 F32, BF16 = 0, 1
+ABI_VERSION = 2     # vlp_abi_version() of the library this binding was written against
 
 _CTYPE = {
     "int": ctypes.c_int,
@@ -89,6 +90,10 @@ class _Lib:
             fn.argtypes = argtypes
             fn.restype = ctypes.c_int if p["ret"] == "int" else None
             self._fns[name] = fn
+        ver = self._fns["vlp_abi_version"]()
+        if ver != ABI_VERSION:
+            raise ImportError(f"{path}: C ABI version {ver}, this binding needs {ABI_VERSION} "
+                              f"(rebuild the library: make -C vision-language-pretraining-for-bone-tumor-detection_amd/csrc)")
 
     def __getattr__(self, name):
         fns = self.__dict__.get("_fns")

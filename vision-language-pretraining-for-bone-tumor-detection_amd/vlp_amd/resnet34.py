@@ -638,7 +638,8 @@ class ImageTowerFn(torch.autograd.Function):
         else:
             feat, saved = tower.run_forward(x, tower.training)
         ctx.tower = tower
-        ctx.saved = saved if torch.is_grad_enabled() or True else None
+        # under no_grad apply() records no node, so ctx (and saved) is dropped with it
+        ctx.saved = saved
         return feat.float()
 
     @staticmethod
