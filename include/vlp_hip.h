@@ -90,6 +90,25 @@ int vlp_conv_dgrad_relu(int dtype, const void* dy, const void* wt, void* g, int 
                         const void* relu_out, const uint8_t* relu_mask, const void* y,
                         const float* mean, const float* invstd, double* stat1, double* stat2,
                         int stat_rep, void* stream);
+/* Layer-1 data gradients with their input's BatchNorm backward folded in (timm
+ * BasicBlock backward, VisionLanguageModule.py:30-32; replaces vlp_bn_bwd_apply +
+ * vlp_conv_dgrad / vlp_conv_dgrad_relu).  The input dy = k*g_in + b*y_in + c (per
+ * channel, in_coef = [k | b | c] from vlp_bn_bwd_coef) is formed once per input row
+ * in the rows kernel's LDS ring and written to dy_out (the weight gradient's
+ * operand); the epilogues are those of vlp_conv_dgrad (y_bn) and vlp_conv_dgrad_relu.
+ * Shapes: vlp_conv_dgrad_act_ok (bf16, C = Co = 64, 3x3 stride 1 pad 1, W = 128),
+ * else hipErrorInvalidValue.  Bit-identical to the separate pass + data gradient. */
+int vlp_conv_dgrad_act_ok(int dtype, int N, int H, int W, int C, int Co, int KH, int KW, int S, int P);
+int vlp_conv_dgrad_bn_act(int dtype, const void* g_in, const void* y_in, const float* in_coef, void* dy_out,
+                          const void* wt, void* dx, int N, int H, int W, int C, int Co, int KH, int KW,
+                          int S, int P, const void* y_bn, const float* bn_scale, const float* bn_shift,
+                          const float* bn_mean, const float* bn_invstd, double* stat1, double* stat2,
+                          int stat_rep, void* stream);
+int vlp_conv_dgrad_relu_act(int dtype, const void* g_in, const void* y_in, const float* in_coef,
+                            void* dy_out, const void* wt, void* gout, int N, int H, int W, int C, int Co,
+                            int KH, int KW, int S, int P, const void* addend, const void* relu_out,
+                            const uint8_t* relu_mask, const void* y, const float* mean,
+                            const float* invstd, double* stat1, double* stat2, int stat_rep, void* stream);
 /* Weight gradient as split-K fp32 slabs: split s of the pixel reduction writes
  * split_ws[s][Co][KH][KW][C] (plain stores, no atomics); *nsplit receives the
  * split count (<= ws_floats / (Co*KH*KW*C)).  vlp_conv_wgrad_fold then sums the
@@ -214,6 +233,10 @@ int vlp_bn_bwd_reduce(int dtype, long long M, int C, const void* dout, const flo
                       const void* mask, const void* ya, const float* mean_a, const float* istd_a,
                       const void* yb, const float* mean_b, const float* istd_b, double* sum_g,
                       double* sum_ga, double* sum_gb, int stat_rep, void* stream);
+/* coef[3][C] = (k, b, c) of dy = k*g + b*y + c over M rows (the folded BN backward;
+ * sums already folded, as vlp_bn_bwd_apply reads them) */
+int vlp_bn_bwd_coef(long long M, int C, const float* gamma, const float* istd, const float* mean,
+                    const double* sum_g, const double* sum_gx, float* coef, void* stream);
 /* dy_s = gamma_s*istd_s*(g - mean(g) - xhat_s*mean(g*xhat_s)) for sides a, b; g_out = g.
  * dyT_a / dyT_b (optional, bf16, C % 64 == 0, M % 8 == 0): also write dy_s
  * transposed to [C][M] (the weight-gradient GEMM's pixel-contiguous operand). */

@@ -102,10 +102,15 @@ def _rel(a, b):
 
 
 @pytest.mark.gpu
-def test_fusion_step_vs_oracle_fp32():
+@pytest.mark.parametrize("B,H", [(6, 64), (8, 256)])
+def test_fusion_step_vs_oracle_fp32(B, H):
+    """fp32 HIP step vs the CPU oracle (FusionModule.py:318-390).  Per tensor
+    rel-L2 <= 1e-3 at 64 px; at 256 px (B = 8, layer 1 at 64 x 64 on the
+    generic tiles) a ReLU whose pre-activation sits within rounding of 0 flips
+    between any two fp32 implementations, so there: <= 2e-2 per
+    tensor and <= 5e-3 for all conv weights of the tower as one vector."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    B, H = 6, 64
     batch = _fusion_batch(B, H)
     o = _oracle()
     m = _hip("fp32", o)
@@ -122,11 +127,24 @@ def test_fusion_step_vs_oracle_fp32():
     assert abs(loss.item() - Lo.item()) < 1e-4, (loss.item(), Lo.item())
     assert float(m.logged["train/coral_loss"].detach()) > 0.0
     og = {k.replace("image_network.trunk.", "image_network."): p.grad for k, p in o.named_parameters()}
+    tol = 1e-3 if H <= 64 else 2e-2
+    errs, convs_h, convs_o = {}, [], []
     for k, p in m.named_parameters():
         if og[k] is None or og[k].norm() < 1e-6:    # biases feeding BatchNorm1d: analytically 0
             continue
         assert p.grad is not None, k
-        assert _rel(p.grad, og[k]) < 1e-3, (k, _rel(p.grad, og[k]))
+        errs[k] = _rel(p.grad, og[k])
+        if k.startswith("image_network.") and p.dim() == 4:
+            convs_h.append(p.grad.double().cpu().flatten())
+            convs_o.append(og[k].double().flatten())
+    worst = max(errs, key=errs.get)
+    tower = _rel(torch.cat(convs_h), torch.cat(convs_o))
+    print(f"fusion fp32 B={B} {H}px: loss {loss.item():.6f} vs {Lo.item():.6f}; worst tensor {worst} "
+          f"{errs[worst]:.2e}; tower conv vector {tower:.2e}")
+    assert len(convs_h) == 36
+    for k, e in errs.items():
+        assert e < tol, (k, e)
+    assert tower < (1e-3 if H <= 64 else 5e-3), tower
 
 
 @pytest.mark.gpu

@@ -139,6 +139,71 @@ def test_conv_fwd_act_matches_pass_then_conv(ops, N, H):
                          t1, t2, stat_rep=4)
 
 
+@pytest.mark.parametrize("N,H", [(3, 5), (2, 128), (300, 4)])
+@pytest.mark.parametrize("epi", ["bn", "relu_bits", "relu_act"])
+def test_conv_dgrad_act_matches_pass_then_dgrad(ops, N, H, epi):
+    """vlp_conv_dgrad_bn_act / vlp_conv_dgrad_relu_act (the BN backward apply of
+    the input formed in the layer-1 rows kernel's ring) against the separate
+    bn_bwd_apply pass + conv_dgrad / conv_dgrad_relu: dy and the output
+    bit-identical, BN sums equal up to fp64 atomic order; N = 300 > CUs puts two
+    images on some workgroups, H = 5 / 4 exercise the first-row and tail paths."""
+    torch.manual_seed(12)
+    C, W = 64, 128
+    dev = torch.device("cuda")
+    M = N * H * W
+    bf = torch.bfloat16
+    g_in = torch.randn(N, H, W, C, device=dev).to(bf)
+    y_in = (torch.randn(N, H, W, C, device=dev) * 2 + 0.3).to(bf)
+    mean = torch.randn(C, device=dev) * 0.2
+    istd = torch.rand(C, device=dev) + 0.5
+    gamma = torch.randn(C, device=dev)
+    sg = (torch.randn(C, device=dev) * M * 0.01).double()
+    sgx = (torch.randn(C, device=dev) * M * 0.01).double()
+    w = (torch.randn(C, C, 3, 3) * (9 * C) ** -0.5).to(bf).float()
+    wt = torch.empty(C, 3, 3, C, dtype=bf, device=dev)
+    ops.pack_conv(w.cuda(), None, wt)
+    assert ops.conv_dgrad_act_ok(g_in, C, 3, 3, 1, 1)
+    dy_ref = torch.empty_like(g_in)
+    ops.bn_bwd_apply(M, C, g_in, None, 1, None, (y_in, mean, istd, gamma, sg, sgx, dy_ref), None, None, g_in)
+    coef = torch.empty(3 * C, device=dev)
+    ops.bn_bwd_coef(M, gamma, istd, mean, sg, sgx, coef)
+    r1, r2, t1, t2 = (torch.zeros(4 * C, dtype=torch.float64, device=dev) for _ in range(4))
+    dy = torch.full_like(g_in, float("nan"))
+    ye = torch.randn(N, H, W, C, device=dev).to(bf)             # epilogue operand (BN input of the output)
+    mu_e, is_e = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5
+    if epi == "bn":
+        sc_e, sh_e = torch.randn(C, device=dev), torch.randn(C, device=dev) * 0.3
+        out_ref = ops.conv_dgrad(dy_ref, wt, H, W, C, 3, 3, 1, 1, y_bn=ye, bn=(sc_e, sh_e, mu_e, is_e),
+                                 stat1=r1, stat2=r2, stat_rep=4)
+        out = ops.conv_dgrad_bn_act(g_in, y_in, coef, dy, wt, H, W, C, 3, 3, 1, 1, ye, (sc_e, sh_e, mu_e, is_e),
+                                    t1, t2, stat_rep=4)
+    else:
+        act = torch.randn(N, H, W, C, device=dev).to(bf)
+        if epi == "relu_bits":
+            rm = torch.empty(M * C // 8, dtype=torch.uint8, device=dev)
+            ops.bn_add_relu(act, torch.ones(C, device=dev), torch.zeros(C, device=dev), None, None, None,
+                            torch.empty_like(act), relu_mask=rm)
+            relu = rm
+        else:
+            relu = act
+        addend = torch.randn(N, H, W, C, device=dev).to(bf)
+        out_ref = ops.conv_dgrad_relu(dy_ref, wt, H, W, C, 3, 3, 1, 1, relu, ye, mu_e, is_e, r1, r2,
+                                      addend=addend, stat_rep=4)
+        out = ops.conv_dgrad_relu_act(g_in, y_in, coef, dy, wt, H, W, C, 3, 3, 1, 1, relu, ye, mu_e, is_e, t1, t2,
+                                      addend=addend, stat_rep=4)
+    torch.cuda.synchronize()
+    assert torch.equal(dy, dy_ref)
+    assert torch.equal(out, out_ref)
+    assert torch.allclose(t1.view(4, C).sum(0), r1.view(4, C).sum(0), rtol=1e-9, atol=1e-9)
+    assert torch.allclose(t2.view(4, C).sum(0), r2.view(4, C).sum(0), rtol=1e-9, atol=1e-9)
+    # dy against the BN backward restated in torch (fp32 on the bf16 operands)
+    k = gamma * istd
+    mg, mgx = (sg / M).float(), (sgx / M).float()
+    ref = k * (g_in.float() - mg - (y_in.float() - mean) * istd * mgx)
+    assert rel(dy.float().cpu(), ref.cpu()) < 1e-2
+    assert not ops.conv_dgrad_act_ok(g_in[:, :, :64].contiguous(), C, 3, 3, 1, 1)
+
+
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_dgrad_wgrad(ops, dt, case):

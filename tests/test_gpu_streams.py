@@ -20,6 +20,10 @@ Test C: bf16 ResNet34 + TinyBERT step at 512^2 (layer-1 width 128), layer-1
 bn1 + ReLU fused into conv2's ring (resnet34._USE_ACT_FUSED) vs the separate
 pass: the activation and conv2 output are bit-identical by construction, so
 every gradient and the loss stay within 4x the run-to-run noise.
+Test D: the same step with the layer-1 BN backward applies formed in the data
+gradients' rows-kernel rings (resnet34._USE_BWD_ACT) vs the separate
+bn_bwd_apply passes: dy1 / dy2 and the data gradients are bit-identical by
+construction (tests/test_gpu_ops.py), so the same 4x-noise gate holds.
 """
 import functools
 
@@ -149,4 +153,41 @@ def test_layer1_act_fused_matches_pass_bf16():
         noise = max((g0[k] - g1[k]).abs().max().item(), (g2[k] - g3[k]).abs().max().item())
         d = (g2[k] - g0[k]).abs().max().item()
         assert d <= 4 * noise + 1e-30, (k, d, noise)
+    assert abs(l2 - l0) <= 4 * max(abs(l1 - l0), abs(l3 - l2)) + 1e-7, (l0, l1, l2, l3)
+
+
+def test_layer1_bwd_act_fused_matches_pass_bf16():
+    from src.models.pretrain.VisionLanguageModule import VisionLanguageModule
+    from vlp_amd import resnet34 as r34
+    torch.manual_seed(3)
+    m = VisionLanguageModule("resnet34", "tinybert", functools.partial(torch.optim.AdamW, lr=5e-5), False, False,
+                             512, 312, 128, compute_dtype="bf16", text_dropout=0.0)
+    m.train()
+    with torch.no_grad():
+        for k, p in m.named_parameters():
+            if k.endswith("bn2.weight"):
+                p.fill_(0.5)
+    b = synth_batch(2, 512, 16, 8, with_u8=True)
+    b = {"x-ray-u8": b["x-ray-u8"].cuda(), "label": b["label"], "caption": b["caption"],
+         "caption_tokenized": {k: v.cuda() for k, v in b["caption_tokenized"].items()}}
+    was = r34._USE_BWD_ACT
+    try:
+        r34._USE_BWD_ACT = False
+        l0, g0 = _grads(m, b)
+        l1, g1 = _grads(m, b)
+        r34._USE_BWD_ACT = True
+        l2, g2 = _grads(m, b)
+        l3, g3 = _grads(m, b)
+    finally:
+        r34._USE_BWD_ACT = was
+    img = [k for k in g0 if k.startswith("image_encoder.")]
+    assert len(img) > 100
+    worst = []
+    for k in img:
+        noise = max((g0[k] - g1[k]).abs().max().item(), (g2[k] - g3[k]).abs().max().item())
+        d = (g2[k] - g0[k]).abs().max().item()
+        worst.append((d - 4 * noise, k, d, noise))
+    worst.sort()
+    print("layer-1 bwd fused vs pass, worst (excess, name, diff, noise):", worst[-3:])
+    assert worst[-1][0] <= 1e-30, worst[-3:]
     assert abs(l2 - l0) <= 4 * max(abs(l1 - l0), abs(l3 - l2)) + 1e-7, (l0, l1, l2, l3)

@@ -333,14 +333,8 @@ bn_bwd_apply_kernel(unsigned nchunks, int cpr, double count, const T* __restrict
 #pragma unroll
   for (int j = 0; j < E; ++j) {
     int c = c0 + j;
-    float k = A.gamma[c] * A.istd[c];
-    float mg = (float)A.sum_g[c] * inv_count, mgx = (float)A.sum_gx[c] * inv_count;
-    ka[j] = k; ba[j] = -k * A.istd[c] * mgx; ca[j] = -k * mg + k * A.istd[c] * mgx * A.mean[c];
-    if (HAS_B) {
-      float k2 = B.gamma[c] * B.istd[c];
-      float mg2 = (float)B.sum_g[c] * inv_count, mgx2 = (float)B.sum_gx[c] * inv_count;
-      kb[j] = k2; bb[j] = -k2 * B.istd[c] * mgx2; cb[j] = -k2 * mg2 + k2 * B.istd[c] * mgx2 * B.mean[c];
-    }
+    bn_bwd_coef(A.gamma[c], A.istd[c], A.mean[c], A.sum_g[c], A.sum_gx[c], inv_count, ka[j], ba[j], ca[j]);
+    if (HAS_B) bn_bwd_coef(B.gamma[c], B.istd[c], B.mean[c], B.sum_g[c], B.sum_gx[c], inv_count, kb[j], bb[j], cb[j]);
   }
   // the plain form (no broadcast gradient, no mask, no g_out, one side) runs
   // U chunks per iteration with both loads of every chunk issued first
@@ -360,7 +354,7 @@ bn_bwd_apply_kernel(unsigned nchunks, int cpr, double count, const T* __restrict
           Chunk<T>::unpack(gv[k], g);
           Chunk<T>::unpack(yv[k], y);
 #pragma unroll
-          for (int j = 0; j < E; ++j) d[j] = fmaf(ka[j], g[j], fmaf(ba[j], y[j], ca[j]));
+          for (int j = 0; j < E; ++j) d[j] = bn_bwd_dy(ka[j], ba[j], ca[j], g[j], y[j]);
           ew_st16<U, NT>((T*)A.dy + (size_t)(i + k * stride) * E, Chunk<T>::pack(d));
         }
       }
@@ -369,7 +363,7 @@ bn_bwd_apply_kernel(unsigned nchunks, int cpr, double count, const T* __restrict
         Chunk<T>::unpack(ldg16(dout + (size_t)i * E), g);
         Chunk<T>::unpack(ldg16((const T*)A.y + (size_t)i * E), y);
 #pragma unroll
-        for (int j = 0; j < E; ++j) d[j] = fmaf(ka[j], g[j], fmaf(ba[j], y[j], ca[j]));
+        for (int j = 0; j < E; ++j) d[j] = bn_bwd_dy(ka[j], ba[j], ca[j], g[j], y[j]);
         ew_st16<U, NT>((T*)A.dy + (size_t)i * E, Chunk<T>::pack(d));
       }
       return;
@@ -392,12 +386,12 @@ bn_bwd_apply_kernel(unsigned nchunks, int cpr, double count, const T* __restrict
     if (g_out) stg16(g_out + (size_t)i * E, Chunk<T>::pack(g));
     Chunk<T>::unpack(ldg16((const T*)A.y + (size_t)i * E), y);
 #pragma unroll
-    for (int j = 0; j < E; ++j) d[j] = fmaf(ka[j], g[j], fmaf(ba[j], y[j], ca[j]));
+    for (int j = 0; j < E; ++j) d[j] = bn_bwd_dy(ka[j], ba[j], ca[j], g[j], y[j]);
     stg16((T*)A.dy + (size_t)i * E, Chunk<T>::pack(d));
     if (HAS_B) {
       Chunk<T>::unpack(ldg16((const T*)B.y + (size_t)i * E), y);
 #pragma unroll
-      for (int j = 0; j < E; ++j) d[j] = fmaf(kb[j], g[j], fmaf(bb[j], y[j], cb[j]));
+      for (int j = 0; j < E; ++j) d[j] = bn_bwd_dy(kb[j], bb[j], cb[j], g[j], y[j]);
       stg16((T*)B.dy + (size_t)i * E, Chunk<T>::pack(d));
     }
   }
@@ -427,14 +421,8 @@ bn_bwd_apply_t_kernel(long long M, int C, double count, const bf16* __restrict__
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int c = c0 + j;
-    const float k = A.gamma[c] * A.istd[c];
-    const float mg = (float)A.sum_g[c] * inv_count, mgx = (float)A.sum_gx[c] * inv_count;
-    ka[j] = k; ba[j] = -k * A.istd[c] * mgx; ca[j] = -k * mg + k * A.istd[c] * mgx * A.mean[c];
-    if (HAS_B) {
-      const float k2 = B.gamma[c] * B.istd[c];
-      const float mg2 = (float)B.sum_g[c] * inv_count, mgx2 = (float)B.sum_gx[c] * inv_count;
-      kb[j] = k2; bb[j] = -k2 * B.istd[c] * mgx2; cbv[j] = -k2 * mg2 + k2 * B.istd[c] * mgx2 * B.mean[c];
-    }
+    bn_bwd_coef(A.gamma[c], A.istd[c], A.mean[c], A.sum_g[c], A.sum_gx[c], inv_count, ka[j], ba[j], ca[j]);
+    if (HAS_B) bn_bwd_coef(B.gamma[c], B.istd[c], B.mean[c], B.sum_g[c], B.sum_gx[c], inv_count, kb[j], bb[j], cbv[j]);
   }
 #pragma unroll
   for (int it = 0; it < 2; ++it) {
@@ -459,14 +447,14 @@ bn_bwd_apply_t_kernel(long long M, int C, double count, const bf16* __restrict__
       if (g_out) stg16(g_out + i, Chunk<bf16>::pack(g));
       Chunk<bf16>::unpack(ldg16((const bf16*)A.y + i), y);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = fmaf(ka[j], g[j], fmaf(ba[j], y[j], ca[j]));
+      for (int j = 0; j < 8; ++j) d[j] = bn_bwd_dy(ka[j], ba[j], ca[j], g[j], y[j]);
       const uint4 pd = Chunk<bf16>::pack(d);
       stg16((bf16*)A.dy + i, pd);
       Chunk<bf16>::unpack(pd, d);   // transposed copy holds the same rounded values
       if (HAS_B) {
         Chunk<bf16>::unpack(ldg16((const bf16*)B.y + i), y);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) e[j] = fmaf(kb[j], g[j], fmaf(bb[j], y[j], cbv[j]));
+        for (int j = 0; j < 8; ++j) e[j] = bn_bwd_dy(kb[j], bb[j], cbv[j], g[j], y[j]);
         const uint4 pe = Chunk<bf16>::pack(e);
         stg16((bf16*)B.dy + i, pe);
         Chunk<bf16>::unpack(pe, e);
@@ -1091,6 +1079,29 @@ VLP_EXPORT int vlp_bn_bwd_apply(int dtype, long long M, int C, const void* dout,
       hipLaunchKernelGGL((bn_bwd_apply_kernel<float, false>), g, dim3(256), 0, st, n, cpr, (double)M,
                          (const float*)dout, dbc, HW, (const float*)mask, A, B, (float*)g_out);
   }
+  return (int)hipGetLastError();
+}
+
+// k, b, c of the folded BN backward (bn_bwd_coef) -> coef[3][C]: the input
+// transform table of the layer-1 rows kernel's data gradient (vlp_conv_dgrad_*_act)
+__global__ void bn_bwd_coef_kernel(int C, float inv_count, const float* __restrict__ gamma,
+                                   const float* __restrict__ istd, const float* __restrict__ mean,
+                                   const double* __restrict__ sum_g, const double* __restrict__ sum_gx,
+                                   float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float k, b, cc;
+  bn_bwd_coef(gamma[c], istd[c], mean[c], sum_g[c], sum_gx[c], inv_count, k, b, cc);
+  coef[c] = k;
+  coef[C + c] = b;
+  coef[2 * C + c] = cc;
+}
+
+VLP_EXPORT int vlp_bn_bwd_coef(long long M, int C, const float* gamma, const float* istd, const float* mean,
+                               const double* sum_g, const double* sum_gx, float* coef, void* stream) {
+  if (M < 1 || C < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, C,
+                     (float)(1.0 / (double)M), gamma, istd, mean, sum_g, sum_gx, coef);
   return (int)hipGetLastError();
 }
 

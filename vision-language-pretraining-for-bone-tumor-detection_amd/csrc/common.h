@@ -112,6 +112,23 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
   return (t + ((n - t) >> f.s1)) >> f.s2;
 }
 
+// Folded BatchNorm backward, dy = k*g + b*y + c with k = gamma*istd,
+// mg = mean(g), mgx = mean(g*xhat): b = -k*istd*mgx, c = -k*mg + k*istd*mgx*mean.
+// Every operation rounded as written (no contraction), so the elementwise pass
+// (bn_ops) and the layer-1 rows kernel's ring transform (conv_ops) produce the
+// same bits.
+__device__ __forceinline__ void bn_bwd_coef(float gamma, float istd, float mean, double sum_g, double sum_gx,
+                                            float inv_count, float& k, float& b, float& c) {
+  k = __fmul_rn(gamma, istd);
+  const float mg = __fmul_rn((float)sum_g, inv_count), mgx = __fmul_rn((float)sum_gx, inv_count);
+  const float t = __fmul_rn(__fmul_rn(k, istd), mgx);
+  b = -t;
+  c = __fadd_rn(-__fmul_rn(k, mg), __fmul_rn(t, mean));
+}
+__device__ __forceinline__ float bn_bwd_dy(float k, float b, float c, float g, float y) {
+  return __fmaf_rn(k, g, __fmaf_rn(b, y, c));
+}
+
 __device__ __forceinline__ float warp_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -1160,27 +1160,37 @@ constexpr int kRcW = 128;                        // image width handled
 constexpr int kRcSlot = (kRcW + 2) * 128;        // one ring row (bytes)
 constexpr int kRcWeights = 9 * 64 * 128;         // 73728
 constexpr int kRcRing = 5;
-constexpr int kRcXtab = kRcWeights + kRcRing * kRcSlot + 2048;   // BN (scale, shift) table, 512 B
-constexpr int kRcLds = kRcXtab + 512;
+constexpr int kRcXtab = kRcWeights + kRcRing * kRcSlot + 2048;   // input-transform table: (scale, shift) or (k, b, c)
+constexpr int kRcLds = kRcXtab + 768;
 
 #ifndef VLP_ACT_NT
 #define VLP_ACT_NT 0   // non-temporal stores of the transformed input rows
 #endif
-// XF: the input is the raw output of the previous conv; every input row is
-// turned into relu(sc[c]*x + sh[c]) once, in place in the ring right after it
-// lands (padding rows stay zero), and written to xout (the activation the
-// weight gradient reads) -- BN-apply + ReLU without a separate pass
-template <class EP, bool XF = false>
+// Input transforms (XF), applied once per input row, in place in the ring right
+// after the row lands (padding rows stay zero), the result also written to
+// xin.out (the operand the weight gradient reads):
+//   XF = 1 (forward): the input is the raw output of the previous conv, turned
+//     into relu(sc[c]*x + sh[c]) -- BN-apply + ReLU without a separate pass;
+//   XF = 2 (data gradient): the ring streams the BN output gradient g and the
+//     transform is that BN's folded backward dy = k[c]*g + b[c]*y + c[c]
+//     (coefficients from vlp_bn_bwd_coef; y = the BN input, LDS-DMA'd one row
+//     ahead) -- the bn_bwd_apply pass without a separate launch.
+struct RowsXIn {
+  const float* t0; const float* t1;   // XF 1: scale, shift; XF 2: t0 = [k | b | c] (3 x 64)
+  const bf16* y;                      // XF 2: the BN input
+  bf16* out;                          // the transformed input rows
+};
+template <class EP, int XF = 0>
 __global__ void __launch_bounds__(512)
 conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __restrict__ w, int flip,
-                        EP ep, int M, const float* __restrict__ xsc = nullptr,
-                        const float* __restrict__ xsh = nullptr, bf16* __restrict__ xout = nullptr) {
+                        EP ep, int M, RowsXIn xin) {
   // 8 waves: wave w computes pixels 32*(w&3) .. +31 and channels 32*(w>>2) .. +31
   // of each output row; its 9 taps x 2 k-substeps x 2 column blocks of filter
   // fragments (144 VGPRs) stay in registers, so the row loop reads only the
   // input ring (4 ds_read_b128 per tap) and two waves share each SIMD.
   constexpr int S = RowTrait<EP>::value ? 2 : 4;  // global stores per lane per output row
-  static_assert(!XF || !RowTrait<EP>::value, "input transform with the direct epilogue only");
+  static_assert(XF != 1 || !RowTrait<EP>::value, "forward input transform with the direct epilogue only");
+  static_assert(XF != 2 || RowTrait<EP>::value, "backward input transform with a row-chunk epilogue only");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* wlds = smem;
   char* ring = smem + kRcWeights;
@@ -1248,37 +1258,74 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
     __syncthreads();
   }
   float* xtab = reinterpret_cast<float*>(smem + kRcXtab);
-  if constexpr (XF) {
-    if (tid < 128) xtab[tid] = tid < 64 ? xsc[tid] : xsh[tid - 64];
+  if constexpr (XF == 1) {
+    if (tid < 128) xtab[tid] = tid < 64 ? xin.t0[tid] : xin.t1[tid - 64];
     __syncthreads();
   }
+  if constexpr (XF == 2) {
+    if (tid < 192) xtab[tid] = xin.t0[tid];
+    __syncthreads();
+  }
+  // XF 2: the BN input y of a row, one row ahead, LDS-DMA'd into a one-row
+  // buffer in the filter area's free part (past the 16 KB epilogue staging tile
+  // and the 32 KB statistics scratch) at the same chunk positions as the ring
+  // row: each thread reads back exactly the chunks its own DMA wrote
+  char* ybuf = smem + 16384 + 32768;
+  static_assert(16384 + 32768 + kRcW * 128 <= kRcWeights, "y row buffer fits the filter area");
+  const rsrc_t ry = XF == 2 ? buf_rsrc(xin.y, (unsigned)((size_t)N * H * kRcW * 64 * 2)) : rz;
+  auto yload = [&](int n, int r) __attribute__((always_inline)) {
+    const bool live = (unsigned)r < (unsigned)H;   // past the last row: a null fetch keeps the vmcnt pattern
+    const rsrc_t rr = live ? ry : rz;
+    const unsigned base = live ? (unsigned)(((size_t)n * H + r) * kRcW * 128) : 0u;
+    // the lane offsets are recomputed per call from an opaque seed (hoisted out of
+    // the row loop they are loop-invariant VGPRs beside the epilogue operands)
+    int sd = lane;
+    asm volatile("" : "+v"(sd));
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = wv * 2 + jj;
+      const int q = j * 64 + sd;
+      const int px = q >> 3, c = (q & 7) ^ (((px + 1) >> 1) & 7);
+      dma16(rr, base + (unsigned)(px * 128 + c * 16), ybuf + j * 1024);
+    }
+  };
   // ring row r (0 <= r < H) of image n -> relu(sc*x + sh), in place and to xout;
   // each thread transforms the two 16-B chunks its own ring fetch wrote, so
   // its vmcnt wait alone makes them readable (no barrier before the transform)
   auto xrow = [&](int n, int r) __attribute__((always_inline)) {
     char* slot = ring + ((r + 1) % kRcRing) * kRcSlot + 128;
+    int sd = lane;
+    if constexpr (XF == 2) asm volatile("" : "+v"(sd));
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
-      const int q = (wv * 2 + jj) * 64 + lane;
+      const int q = (wv * 2 + jj) * 64 + sd;
       const int px = q >> 3, cc = (q & 7) ^ (((px + 1) >> 1) & 7);
-      const v4f s0 = *reinterpret_cast<const v4f*>(xtab + cc * 8), s1 = *reinterpret_cast<const v4f*>(xtab + cc * 8 + 4);
-      const v4f h0 = *reinterpret_cast<const v4f*>(xtab + 64 + cc * 8), h1 = *reinterpret_cast<const v4f*>(xtab + 68 + cc * 8);
       uint4* p = reinterpret_cast<uint4*>(slot + q * 16);
       float f[8];
       Chunk<bf16>::unpack(*p, f);
+      if constexpr (XF == 2) {
+        float yy[8];
+        Chunk<bf16>::unpack(*reinterpret_cast<const uint4*>(ybuf + q * 16), yy);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        f[j] = fmaxf(fmaf(f[j], s0[j], h0[j]), 0.f);
-        f[4 + j] = fmaxf(fmaf(f[4 + j], s1[j], h1[j]), 0.f);
+        for (int j = 0; j < 8; ++j)
+          f[j] = bn_bwd_dy(xtab[cc * 8 + j], xtab[64 + cc * 8 + j], xtab[128 + cc * 8 + j], f[j], yy[j]);
+      } else {
+        const v4f s0 = *reinterpret_cast<const v4f*>(xtab + cc * 8), s1 = *reinterpret_cast<const v4f*>(xtab + cc * 8 + 4);
+        const v4f h0 = *reinterpret_cast<const v4f*>(xtab + 64 + cc * 8), h1 = *reinterpret_cast<const v4f*>(xtab + 68 + cc * 8);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f[j] = fmaxf(fmaf(f[j], s0[j], h0[j]), 0.f);
+          f[4 + j] = fmaxf(fmaf(f[4 + j], s1[j], h1[j]), 0.f);
+        }
       }
       const uint4 v = Chunk<bf16>::pack(f);
       *p = v;
 #if VLP_ACT_NT
       typedef unsigned v4u_nt __attribute__((ext_vector_type(4)));
       __builtin_nontemporal_store(v4u_nt{v.x, v.y, v.z, v.w},
-                                  reinterpret_cast<v4u_nt*>(xout + (((size_t)n * H + r) * kRcW + px) * 64 + cc * 8));
+                                  reinterpret_cast<v4u_nt*>(xin.out + (((size_t)n * H + r) * kRcW + px) * 64 + cc * 8));
 #else
-      stg16(xout + (((size_t)n * H + r) * kRcW + px) * 64 + cc * 8, v);
+      stg16(xin.out + (((size_t)n * H + r) * kRcW + px) * 64 + cc * 8, v);
 #endif
     }
   };
@@ -1286,17 +1333,41 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
   for (int n = blockIdx.x; n < N; n += gridDim.x) {
     wait_vmcnt<0>();
     __syncthreads();
-    fetch(n, -1); fetch(n, 0); fetch(n, 1); fetch(n, 2);
+    if constexpr (XF == 2) {
+      fetch(n, -1); fetch(n, 0); yload(n, 0);
+    } else {
+      fetch(n, -1); fetch(n, 0); fetch(n, 1); fetch(n, 2);
+    }
     for (int i = 0; i < H; ++i) {
-      // XF adds the xout stores (2 per row, rows 0 and 1 both in row 0) before
-      // each row's ring fetch
-      if (i == 0) wait_vmcnt<2>();                           // rows -1..1 landed (row 2 in flight)
-      else if (i == 1) wait_vmcnt<2 + S + (XF ? 4 : 0)>();   // row 2 (row 3, row-0 stores in flight)
-      else wait_vmcnt<2 + 2 * S + (XF ? 2 : 0)>();           // row i+1 (rows i+2, stores of i-2, i-1)
-      if constexpr (XF) {
-        if (i == 0) { xrow(n, 0); xrow(n, 1); }
-        else if (i + 1 < H) xrow(n, i + 1);
+      if constexpr (XF == 2) {
+        // per row i: [dy stores of row i+1] [epilogue operands of row i] [y of row
+        // i+2] [ring fetch of row i+3] MFMAs [epilogue stores of row i]; row i+1's
+        // ring data and y are older than the last fetch and epilogue stores
+        if (i == 0) {
+          // prologue order: fetch -1, fetch 0, y 0, then y 1, fetch 1, fetch 2 here
+          wait_vmcnt<0>();
+          xrow(n, 0);
+          yload(n, 1);
+          fetch(n, 1);
+          fetch(n, 2);
+          wait_vmcnt<2>();                                   // y 1 and ring row 1 landed (row 2 in flight)
+          xrow(n, 1);
+        } else {
+          wait_vmcnt<2 + S>();                               // y / ring row i+1 landed (fetch i+2, row i-1 stores in flight)
+          if (i + 1 < H) xrow(n, i + 1);
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      } else {
+        // XF adds the xout stores (2 per row, rows 0 and 1 both in row 0) before
+        // each row's ring fetch
+        if (i == 0) wait_vmcnt<2>();                           // rows -1..1 landed (row 2 in flight)
+        else if (i == 1) wait_vmcnt<2 + S + (XF ? 4 : 0)>();   // row 2 (row 3, row-0 stores in flight)
+        else wait_vmcnt<2 + 2 * S + (XF ? 2 : 0)>();           // row i+1 (rows i+2, stores of i-2, i-1)
+        if constexpr (XF == 1) {
+          if (i == 0) { xrow(n, 0); xrow(n, 1); }
+          else if (i + 1 < H) xrow(n, i + 1);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
       }
       raw_barrier();                            // all waves: ring rows landed (and transformed), row i-1 done
       // epilogue operands of this row (row-chunk epilogues): issued now, consumed
@@ -1311,6 +1382,10 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
 #pragma unroll
         for (int h2 = 0; h2 < 2; ++h2) ep.pre8((n * H + i) * kRcW + (tid >> 3) + 64 * h2, (tid & 7) * 8, pre[h2]);
         __builtin_amdgcn_sched_barrier(0);      // keep the issue order
+        if constexpr (XF == 2) {
+          yload(n, i + 2);
+          __builtin_amdgcn_sched_barrier(0);
+        }
         fetch(n, i + 3);
       }
       v4f acc[2][2];
@@ -1450,20 +1525,17 @@ static bool rows_c64_ok(const ConvGeom& g) {
   return !off && g.C == 64 && g.Co == 64 && g.KH == 3 && g.KW == 3 && g.S == 1 && g.P == 1 && g.W == kRcW &&
          g.H >= 3 && (size_t)g.N * g.H * kRcW * 128 < (1ull << 31);
 }
-template <class EP, bool XF = false>
+template <class EP, int XF = 0>
 static int launch_rows_c64(const ConvGeom& g, const void* x, const void* w, int flip, const EP& ep,
-                           hipStream_t st, const float* xsc = nullptr, const float* xsh = nullptr,
-                           void* xout = nullptr) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)&conv3x3_c64_rows_kernel<EP, XF>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, kRcLds);
-    attr = true;
-  }
+                           hipStream_t st, const RowsXIn& xin = RowsXIn{}) {
+  // per device and cheap: set on every launch (a process-wide flag would miss a second GPU)
+  const hipError_t ae = hipFuncSetAttribute((const void*)&conv3x3_c64_rows_kernel<EP, XF>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, kRcLds);
+  if (ae != hipSuccess) return (int)ae;
   int grid = device_cus();
   if (grid > g.N) grid = g.N;
   hipLaunchKernelGGL((conv3x3_c64_rows_kernel<EP, XF>), dim3(grid), dim3(512), kRcLds, st, g.N, g.H,
-                     (const bf16*)x, (const bf16*)w, flip, ep, g.N * g.H * g.W, xsc, xsh, (bf16*)xout);
+                     (const bf16*)x, (const bf16*)w, flip, ep, g.N * g.H * g.W, xin);
   return (int)hipGetLastError();
 }
 
@@ -1840,8 +1912,70 @@ VLP_EXPORT int vlp_conv_fwd_act(int dtype, const void* x, const void* wp, void* 
   g.M = g.N * g.Ho * g.Wo;
   g.K = g.KH * g.KW * g.C;
   EpiConvFwd<bf16> ep{stat_sum, stat_sumsq, stat_rep, (bf16*)y, g.Co};
-  return launch_rows_c64<EpiConvFwd<bf16>, true>(g, x, wp, 0, ep, (hipStream_t)stream, in_scale, in_shift,
-                                                 x_act);
+  RowsXIn xin{};
+  xin.t0 = in_scale;
+  xin.t1 = in_shift;
+  xin.out = (bf16*)x_act;
+  return launch_rows_c64<EpiConvFwd<bf16>, 1>(g, x, wp, 0, ep, (hipStream_t)stream, xin);
+}
+
+// Layer-1 data gradients with the BN backward of their input folded into the
+// rows kernel's ring (XF = 2): g_in is the BN output gradient, y_in the BN
+// input; dy_out receives dy = k*g + b*y + c (the weight gradient's operand).
+static RowsXIn rows_bwd_xin(const void* y_in, const float* in_coef, void* dy_out) {
+  RowsXIn xin{};
+  xin.t0 = in_coef;
+  xin.y = (const bf16*)y_in;
+  xin.out = (bf16*)dy_out;
+  return xin;
+}
+
+VLP_EXPORT int vlp_conv_dgrad_act_ok(int dtype, int N, int H, int W, int C, int Co, int KH, int KW, int S,
+                                    int P) {
+  return vlp_conv_fwd_act_ok(dtype, N, H, W, C, Co, KH, KW, S, P);
+}
+
+VLP_EXPORT int vlp_conv_dgrad_bn_act(int dtype, const void* g_in, const void* y_in, const float* in_coef,
+                                     void* dy_out, const void* wt, void* dx, int N, int H,
+                                     int W, int C, int Co, int KH, int KW, int S, int P, const void* y_bn,
+                                     const float* bn_scale, const float* bn_shift, const float* bn_mean,
+                                     const float* bn_invstd, double* stat1, double* stat2, int stat_rep,
+                                     void* stream) {
+  if (!vlp_conv_dgrad_act_ok(dtype, N, H, W, C, Co, KH, KW, S, P) || !g_in || !y_in || !dy_out || !in_coef ||
+      !y_bn || !bn_scale || !bn_shift || !bn_mean || !bn_invstd || !stat1 || !stat2)
+    return (int)hipErrorInvalidValue;
+  ConvGeom g = make_geom(N, H, W, C, Co, KH, KW, S, P);
+  g.M = g.N * g.H * g.W;
+  g.K = g.KH * g.KW * g.Co;
+  EpiDgradBN<bf16> ep{stat1, stat2, stat_rep, (bf16*)dx, g.C, (const bf16*)y_bn, bn_scale, bn_shift, bn_mean,
+                      bn_invstd};
+  return launch_rows_c64<EpiDgradBN<bf16>, 2>(g, g_in, wt, 1, ep, (hipStream_t)stream,
+                                              rows_bwd_xin(y_in, in_coef, dy_out));
+}
+
+VLP_EXPORT int vlp_conv_dgrad_relu_act(int dtype, const void* g_in, const void* y_in, const float* in_coef,
+                                       void* dy_out, const void* wt, void* gout, int N,
+                                       int H, int W, int C, int Co, int KH, int KW, int S, int P,
+                                       const void* addend, const void* relu_out, const uint8_t* relu_mask,
+                                       const void* y, const float* mean, const float* invstd, double* stat1,
+                                       double* stat2, int stat_rep, void* stream) {
+  if (!vlp_conv_dgrad_act_ok(dtype, N, H, W, C, Co, KH, KW, S, P) || !g_in || !y_in || !dy_out || !in_coef ||
+      (relu_out == nullptr) == (relu_mask == nullptr) || !y ||
+      !mean || !invstd || !stat1 || !stat2)
+    return (int)hipErrorInvalidValue;
+  ConvGeom g = make_geom(N, H, W, C, Co, KH, KW, S, P);
+  g.M = g.N * g.H * g.W;
+  g.K = g.KH * g.KW * g.Co;
+  const RowsXIn xin = rows_bwd_xin(y_in, in_coef, dy_out);
+  hipStream_t st = (hipStream_t)stream;
+  if (relu_mask) {
+    EpiDgradRelu<bf16, true> ep{stat1, stat2, stat_rep, (bf16*)gout, (const bf16*)addend, g.C,
+                                (const bf16*)relu_out, (const bf16*)y, mean, invstd, relu_mask};
+    return launch_rows_c64<EpiDgradRelu<bf16, true>, 2>(g, g_in, wt, 1, ep, st, xin);
+  }
+  EpiDgradRelu<bf16, false> ep{stat1, stat2, stat_rep, (bf16*)gout, (const bf16*)addend, g.C,
+                               (const bf16*)relu_out, (const bf16*)y, mean, invstd, relu_mask};
+  return launch_rows_c64<EpiDgradRelu<bf16, false>, 2>(g, g_in, wt, 1, ep, st, xin);
 }
 
 VLP_EXPORT int vlp_conv_dgrad(int dtype, const void* dy, const void* wt, void* dx, int N, int H,

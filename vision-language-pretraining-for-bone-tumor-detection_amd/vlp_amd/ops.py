@@ -109,6 +109,49 @@ def conv_dgrad_relu(dy, wt, H, W, C, KH, KW, S, P, relu_out, y, mean, invstd, st
     return g
 
 
+def conv_dgrad_act_ok(dy, C, KH, KW, S, P):
+    N, H, W, Co = dy.shape
+    return bool(lib()._dll.vlp_conv_dgrad_act_ok(dcode(dy), N, H, W, C, Co, KH, KW, S, P))
+
+
+def bn_bwd_coef(M, gamma, istd, mean, sum_g, sum_gx, coef):
+    """coef[3][C] = (k, b, c) of the folded BN backward dy = k*g + b*y + c."""
+    lib().vlp_bn_bwd_coef(int(M), gamma.numel(), ptr(gamma), ptr(istd), ptr(mean), ptr(sum_g), ptr(sum_gx),
+                          ptr(coef), _s())
+
+
+def conv_dgrad_bn_act(g_in, y_in, in_coef, dy_out, wt, H, W, C, KH, KW, S, P, y_bn, bn, stat1, stat2,
+                      stat_rep=1, out=None):
+    """conv_dgrad(dy, y_bn=..., bn=...) with dy = k*g_in + b*y_in + c formed in the
+    layer-1 rows kernel's ring from in_coef (bn_bwd_coef) and written to dy_out
+    (vlp_conv_dgrad_bn_act: the bn_bwd_apply pass fused)."""
+    N, Ho, Wo, Co = g_in.shape
+    dx = out if out is not None else torch.empty((N, H, W, C), dtype=g_in.dtype, device=g_in.device)
+    sc, sh, mu, ist = bn
+    tk = ktimer.begin("conv_dgrad[bn,act]/narrow", 2.0 * N * Ho * Wo * Co * C * KH * KW)
+    lib().vlp_conv_dgrad_bn_act(dcode(g_in), ptr(g_in), ptr(y_in), ptr(in_coef), ptr(dy_out), ptr(wt), ptr(dx),
+                                N, H, W, C, Co, KH, KW, S, P, ptr(y_bn), ptr(sc), ptr(sh), ptr(mu), ptr(ist),
+                                ptr(stat1), ptr(stat2), int(stat_rep), _s())
+    ktimer.end(tk)
+    return dx
+
+
+def conv_dgrad_relu_act(g_in, y_in, in_coef, dy_out, wt, H, W, C, KH, KW, S, P, relu_out, y, mean, invstd,
+                        stat1, stat2, addend=None, stat_rep=1, out=None):
+    """conv_dgrad_relu with its input dy = k*g_in + b*y_in + c formed in the rows
+    kernel's ring and written to dy_out (vlp_conv_dgrad_relu_act)."""
+    N, Ho, Wo, Co = g_in.shape
+    g = out if out is not None else torch.empty((N, H, W, C), dtype=g_in.dtype, device=g_in.device)
+    bits = relu_out.dtype == torch.uint8
+    tk = ktimer.begin("conv_dgrad[relu,act]/narrow", 2.0 * N * Ho * Wo * Co * C * KH * KW)
+    lib().vlp_conv_dgrad_relu_act(dcode(g_in), ptr(g_in), ptr(y_in), ptr(in_coef), ptr(dy_out), ptr(wt), ptr(g),
+                                  N, H, W, C, Co, KH, KW, S, P, ptr(addend), None if bits else ptr(relu_out),
+                                  ptr(relu_out) if bits else None, ptr(y), ptr(mean), ptr(invstd), ptr(stat1),
+                                  ptr(stat2), int(stat_rep), _s())
+    ktimer.end(tk)
+    return g
+
+
 def conv_wgrad(dy, x, KH, KW, S, P, dw_ws, in_scale=None, in_shift=None, dyT=None):
     N, H, W, C = x.shape
     Co = dy.shape[-1]

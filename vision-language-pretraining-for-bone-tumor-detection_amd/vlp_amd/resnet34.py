@@ -54,6 +54,10 @@ _USE_STEM1 = os.environ.get("VLP_STEM1", "1") != "0"
 # bf16: stem conv + BN sums + max-pool fused (stem_ops.hip); False keeps the
 # conv -> y0 -> max-pool kernels (tests compare the two)
 _USE_STEM_FUSED = True
+# layer-1 data gradients form their input dy = k*g + b*y + c in the rows kernel's
+# ring (vlp_conv_dgrad_bn_act / vlp_conv_dgrad_relu_act) instead of a separate
+# bn_bwd_apply pass (tests/test_gpu_streams.py holds on vs off)
+_USE_BWD_ACT = True
 # bf16 layer 1: bn1 + ReLU applied in conv2's input ring (vlp_conv_fwd_act), a1
 # written by that kernel; False keeps the separate bn_add_relu pass
 _USE_ACT_FUSED = True
@@ -498,21 +502,36 @@ class ResNet34Tower(ArenaModule):
                 g_id = torch.empty_like(out)
             tA = self._tbuf(ws, "tA", C, M)
             tB = self._tbuf(ws, "tB", C, M) if (has_ds and tA is not None) else None
-            ops.bn_bwd_apply(M, C, dout, dbc, HW, None if dout_masked else out, A, Bside,
-                             None if dout_masked else g_id, out, dyT_a=tA, dyT_b=tB)
-            # conv2: dgrad through relu(bn1(y1)) with BN1 backward sums; wgrad on relu(bn1(y1))
+            # layer 1: both BN backward applies move into the rows kernels' rings
+            fuse_in = (_USE_BWD_ACT and T == torch.bfloat16 and dout_masked and not has_ds and tA is None
+                       and c1.S == 1 and ops.conv_dgrad_act_ok(dout, C, 3, 3, 1, 1))
             sc1, sh1, mu1, is1 = self._coef(ws, k1)
             sg1f, sgx1f = self._bstat(ws, k1, full=True)
-            g1 = ops.conv_dgrad(dy2, ws[c2.key + ".wt"], Hh, Ww, C, 3, 3, 1, 1, y_bn=y1,
-                                bn=(sc1, sh1, mu1, is1), stat1=sg1f, stat2=sgx1f, stat_rep=STAT_REP)
+            if fuse_in:
+                coef = ws.get("bwd_coef")
+                if coef is None:
+                    coef = ws["bwd_coef"] = torch.empty(2, 3 * 64, dtype=torch.float32, device=dev)
+                ops.bn_bwd_coef(M, self.arena.view(k2 + ".weight"), is2, mu2, sg2, sgx2, coef[0])
+                # conv2: dgrad of dy2 = BN2'(dout) through relu(bn1(y1)) with BN1 backward sums
+                g1 = ops.conv_dgrad_bn_act(dout, y2, coef[0], dy2, ws[c2.key + ".wt"], Hh, Ww, C, 3, 3, 1, 1,
+                                           y1, (sc1, sh1, mu1, is1), sg1f, sgx1f, stat_rep=STAT_REP)
+            else:
+                ops.bn_bwd_apply(M, C, dout, dbc, HW, None if dout_masked else out, A, Bside,
+                                 None if dout_masked else g_id, out, dyT_a=tA, dyT_b=tB)
+                # conv2: dgrad through relu(bn1(y1)) with BN1 backward sums; wgrad on relu(bn1(y1))
+                g1 = ops.conv_dgrad(dy2, ws[c2.key + ".wt"], Hh, Ww, C, 3, 3, 1, 1, y_bn=y1,
+                                    bn=(sc1, sh1, mu1, is1), stat1=sg1f, stat2=sgx1f, stat_rep=STAT_REP)
             ops.bn_grad_rep(STAT_REP, C, sg1f, sgx1f, self.arena.gview(k1 + ".weight"),
                             self.arena.gview(k1 + ".bias"))
             sg1, sgx1 = sg1f[:C], sgx1f[:C]
             self._wgrad(ws, c2, dy2, B["a1"], dyT=tA)
             dy1 = torch.empty_like(y1)
-            ops.bn_bwd_apply(M, C, g1, None, 1, None,
-                             (y1, mu1, is1, self.arena.view(k1 + ".weight"), sg1, sgx1, dy1), None, None, y1,
-                             dyT_a=tA)
+            if fuse_in:
+                ops.bn_bwd_coef(M, self.arena.view(k1 + ".weight"), is1, mu1, sg1, sgx1, coef[1])
+            else:
+                ops.bn_bwd_apply(M, C, g1, None, 1, None,
+                                 (y1, mu1, is1, self.arena.view(k1 + ".weight"), sg1, sgx1, dy1), None, None, y1,
+                                 dyT_a=tA)
             Hi, Wi = x.shape[1], x.shape[2]
             addend = g_id
             if has_ds:
@@ -530,8 +549,13 @@ class ResNet34Tower(ArenaModule):
                 _, _, mu0, is0 = self._coef(ws, "bn1")
                 sg0f, sgx0f = self._bstat(ws, "bn1", full=True)
                 rmask = B["xmask"] if B.get("xmask") is not None else x
-                dx = ops.conv_dgrad_relu(dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, rmask, saved["yarg"],
-                                         mu0, is0, sg0f, sgx0f, addend=addend, stat_rep=STAT_REP)
+                if fuse_in:
+                    dx = ops.conv_dgrad_relu_act(g1, y1, coef[1], dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, 1, 1,
+                                                 rmask, saved["yarg"], mu0, is0, sg0f, sgx0f, addend=addend,
+                                                 stat_rep=STAT_REP)
+                else:
+                    dx = ops.conv_dgrad_relu(dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, rmask,
+                                             saved["yarg"], mu0, is0, sg0f, sgx0f, addend=addend, stat_rep=STAT_REP)
                 dout_masked = True
             elif prev is not None and not prev[1]:
                 kp = prev[0] + ".bn2"
@@ -540,11 +564,17 @@ class ResNet34Tower(ArenaModule):
                 # sign bits for stride 1; the stride-2 parity-class epilogue reads the
                 # activation faster than single mask bytes (measured 840 vs 884 us)
                 rmask = B["xmask"] if (B.get("xmask") is not None and c1.S == 1) else x
-                dx = ops.conv_dgrad_relu(dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, rmask,
-                                         blocks[bi - 1]["y2"], mup, isp, sgpf, sgxpf, addend=addend,
-                                         stat_rep=STAT_REP)
+                if fuse_in:
+                    dx = ops.conv_dgrad_relu_act(g1, y1, coef[1], dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, 1, 1,
+                                                 rmask, blocks[bi - 1]["y2"], mup, isp, sgpf, sgxpf,
+                                                 addend=addend, stat_rep=STAT_REP)
+                else:
+                    dx = ops.conv_dgrad_relu(dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, rmask,
+                                             blocks[bi - 1]["y2"], mup, isp, sgpf, sgxpf, addend=addend,
+                                             stat_rep=STAT_REP)
                 dout_masked = True
             else:
+                assert not fuse_in
                 dx = ops.conv_dgrad(dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, addend=addend)
                 dout_masked = False
             self._wgrad(ws, c1, dy1, x, dyT=tA)
