@@ -286,8 +286,9 @@ clip_dk_kernel(int B, int N, int E, int offset, const float* __restrict__ img_al
       *reinterpret_cast<v4f*>(Qs + row * QP + 4 * c4) = ld_row4(qsrc, i0 + row, B, c0 + 4 * c4, E);
     }
     __syncthreads();
-#pragma unroll 4
-    for (int kk = 0; kk < 16; ++kk)
+    // 64 queries = 4 blocks of 16; MFMA (kk, r) takes queries 16kk + 4g + r of lane group g
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = 16 * kk + 4 * g + r;

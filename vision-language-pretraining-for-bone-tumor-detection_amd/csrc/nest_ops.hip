@@ -194,6 +194,31 @@ struct TileStage {
   }
 };
 
+// ---------------- grid ----------------
+// The attention kernels run a 1-D grid of nx tiles x H heads x BT blocks.
+// VLP_ATTN_XCD = 1: the block id is remapped so that each XCD owns a contiguous
+// run of (tile, head, block) ids -- the nx tiles of one (block, head), which all
+// re-read that pair's 64 KB K/V (Q/dO) slices, then sit on one XCD together and
+// hit its L2 (with the plain round-robin dispatch they spread over all 8 XCDs).
+// 0: the id is used as is (neighbouring tiles on different XCDs).
+#ifndef VLP_ATTN_XCD
+#define VLP_ATTN_XCD 1
+#endif
+__device__ __forceinline__ void attn_tile(int nx, int H, int& x, int& h, int& bt) {
+  const int total = (int)gridDim.x;
+  int id = (int)blockIdx.x;
+#if VLP_ATTN_XCD
+  if (total >= 16) {
+    const int xcd = id & 7, idx = id >> 3, q = total >> 3, rr = total & 7;
+    id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
+  }
+#endif
+  x = id % nx;
+  const int r = id / nx;
+  h = r % H;
+  bt = r / H;
+}
+
 // ---------------- forward ----------------
 // grid (ceil(N/128), H, BT); 4 waves, wave w owns queries qt*128 + 32w .. +31
 // as two 16-query subtiles that share every K / V fragment read.
@@ -210,7 +235,8 @@ nest_attn_fwd_kernel(int BT, int H, int N, const T* __restrict__ qkv, T* __restr
   constexpr int QW = 2, KSN = kDh / M::KS;
   __shared__ __attribute__((aligned(16))) T sK[M::IMG];
   __shared__ __attribute__((aligned(16))) T sV[M::IMG];
-  const int qt = blockIdx.x, h = blockIdx.y, bt = blockIdx.z;
+  int qt, h, bt;
+  attn_tile((N + kQBlock - 1) / kQBlock, H, qt, h, bt);
   const int C = H * kDh;
   const size_t ld3 = 3 * (size_t)C;
   const T* base = qkv + (size_t)bt * N * ld3;
@@ -346,7 +372,8 @@ nest_attn_bwd_dq_kernel(int BT, int H, int N, const T* __restrict__ qkv, const T
   constexpr int QW = 2, KSN = kDh / M::KS;
   __shared__ __attribute__((aligned(16))) T sK[M::IMG];
   __shared__ __attribute__((aligned(16))) T sV[M::IMG];
-  const int qt = blockIdx.x, h = blockIdx.y, bt = blockIdx.z;
+  int qt, h, bt;
+  attn_tile((N + kQBlock - 1) / kQBlock, H, qt, h, bt);
   const int C = H * kDh;
   const size_t ld3 = 3 * (size_t)C;
   const T* base = qkv + (size_t)bt * N * ld3;
@@ -455,7 +482,8 @@ nest_attn_bwd_dkdv_kernel(int BT, int H, int N, const T* __restrict__ qkv, const
   __shared__ __attribute__((aligned(16))) T sQ[M::IMG];
   __shared__ __attribute__((aligned(16))) T sD[M::IMG];
   __shared__ __attribute__((aligned(16))) float sL[kTileRows], sDl[kTileRows];
-  const int kt = blockIdx.x, h = blockIdx.y, bt = blockIdx.z;
+  int kt, h, bt;
+  attn_tile((N + 63) / 64, H, kt, h, bt);
   const int C = H * kDh;
   const size_t ld3 = 3 * (size_t)C;
   const T* base = qkv + (size_t)bt * N * ld3;
@@ -761,12 +789,13 @@ using namespace vlp;
 
 template <typename T>
 static void attn_fwd_t(int BT, int H, int N, const void* qkv, void* out, float* lse, float scale, hipStream_t st) {
-  hipLaunchKernelGGL(nest_attn_fwd_kernel<T>, dim3((N + kQBlock - 1) / kQBlock, H, BT), dim3(256), 0, st, BT, H, N,
+  hipLaunchKernelGGL(nest_attn_fwd_kernel<T>, dim3(((N + kQBlock - 1) / kQBlock) * H * BT), dim3(256), 0, st, BT, H, N,
                      (const T*)qkv, (T*)out, lse, scale * 1.4426950408889634f);
 }
 VLP_EXPORT int vlp_nest_attn_fwd(int dtype, int BT, int H, int N, int dh, const void* qkv, void* out, float* lse,
                                  float scale, void* stream) {
-  if (dh != kDh || BT < 1 || H < 1 || N < 1 || BT > 65535 || H > 65535) return (int)hipErrorInvalidValue;
+  if (dh != kDh || BT < 1 || H < 1 || N < 1 || (long long)((N + 63) / 64) * H * BT >= (1ll << 31))
+    return (int)hipErrorInvalidValue;
   NEST_DT(dtype, attn_fwd_t, BT, H, N, qkv, out, lse, scale, (hipStream_t)stream);
   return (int)hipGetLastError();
 }
@@ -777,7 +806,7 @@ static void attn_bwd_t(int BT, int H, int N, const void* qkv, const void* out, c
   const size_t rows = (size_t)BT * N * H;
   hipLaunchKernelGGL(nest_attn_delta_kernel<T>, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, BT, H, N,
                      (const T*)out, (const T*)dout, delta);
-  const dim3 gq((N + kQBlock - 1) / kQBlock, H, BT), gk((N + 63) / 64, H, BT);
+  const dim3 gq(((N + kQBlock - 1) / kQBlock) * H * BT), gk(((N + 63) / 64) * H * BT);
   const float sl2 = scale * 1.4426950408889634f;
   hipLaunchKernelGGL(nest_attn_bwd_dq_kernel<T>, gq, dim3(256), 0, st, BT, H, N, (const T*)qkv, (const T*)dout, lse,
                      (const float*)delta, (T*)dqkv, sl2, scale);
@@ -787,7 +816,8 @@ static void attn_bwd_t(int BT, int H, int N, const void* qkv, const void* out, c
 VLP_EXPORT int vlp_nest_attn_bwd(int dtype, int BT, int H, int N, int dh, const void* qkv, const void* out,
                                  const void* dout, const float* lse, float* delta, void* dqkv, float scale,
                                  void* stream) {
-  if (dh != kDh || BT < 1 || H < 1 || N < 1 || BT > 65535 || H > 65535) return (int)hipErrorInvalidValue;
+  if (dh != kDh || BT < 1 || H < 1 || N < 1 || (long long)((N + 63) / 64) * H * BT >= (1ll << 31))
+    return (int)hipErrorInvalidValue;
   NEST_DT(dtype, attn_bwd_t, BT, H, N, qkv, out, dout, lse, delta, dqkv, scale, (hipStream_t)stream);
   return (int)hipGetLastError();
 }
