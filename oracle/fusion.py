@@ -68,8 +68,9 @@ class OracleFusion(nn.Module):
         return self.combination_network(torch.cat((img_logits, clin), dim=1)).flatten(), f
 
     def compute_loss(self, f, logits, labels, dataset):
-        w = torch.where(labels == 0, self.label_weights[0], self.label_weights[1])
-        cls = F.binary_cross_entropy_with_logits(logits, labels.float(), weight=w)
+        w = torch.where(labels == 0, self.label_weights[0], self.label_weights[1]).to(logits.dtype)
+        # labels in the logits' dtype (float() in the reference; the fp64 envelope runs this in double)
+        cls = F.binary_cross_entropy_with_logits(logits, labels.to(logits.dtype), weight=w)
         if self.coral_lambda == 0.0:
             return cls, cls, torch.tensor(0.0)
         pooled = f.mean((2, 3)) if f.dim() == 4 else f

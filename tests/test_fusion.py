@@ -105,10 +105,12 @@ def _rel(a, b):
 @pytest.mark.parametrize("B,H", [(6, 64), (8, 256)])
 def test_fusion_step_vs_oracle_fp32(B, H):
     """fp32 HIP step vs the CPU oracle (FusionModule.py:318-390).  Per tensor
-    rel-L2 <= 1e-3 at 64 px; at 256 px (B = 8, layer 1 at 64 x 64 on the
+    rel-L2 <= 1e-3 at 64 px.  At 256 px (B = 8, layer 1 at 64 x 64 on the
     generic tiles) a ReLU whose pre-activation sits within rounding of 0 flips
-    between any two fp32 implementations, so there: <= 2e-2 per
-    tensor and <= 5e-3 for all conv weights of the tower as one vector."""
+    between any two fp32 implementations, so there the gate is the
+    fp64 envelope of the VLP parity tests: with e(.) the rel-L2 against the
+    oracle run in fp64, every tensor e(HIP) <= max(4 e(oracle fp32), 2e-2) and
+    the tower's 36 conv weights as one vector e(HIP) <= max(2 e(oracle fp32), 5e-3)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     batch = _fusion_batch(B, H)
@@ -127,24 +129,33 @@ def test_fusion_step_vs_oracle_fp32(B, H):
     assert abs(loss.item() - Lo.item()) < 1e-4, (loss.item(), Lo.item())
     assert float(m.logged["train/coral_loss"].detach()) > 0.0
     og = {k.replace("image_network.trunk.", "image_network."): p.grad for k, p in o.named_parameters()}
-    tol = 1e-3 if H <= 64 else 2e-2
-    errs, convs_h, convs_o = {}, [], []
+    ref = og
+    if H > 64:   # fp64 envelope
+        o64 = _oracle().double()
+        o64.train()
+        l64, f64 = o64(*(batch[k].double() for k in ("x-ray", "age_encoded", "sex_encoded", "anatomy_site_encoded")))
+        o64.compute_loss(f64, l64, batch["tumor"], batch["dataset"])[0].backward()
+        ref = {k.replace("image_network.trunk.", "image_network."): p.grad for k, p in o64.named_parameters()}
+    errs, envs, convs = {}, {}, ([], [], [])
     for k, p in m.named_parameters():
         if og[k] is None or og[k].norm() < 1e-6:    # biases feeding BatchNorm1d: analytically 0
             continue
         assert p.grad is not None, k
-        errs[k] = _rel(p.grad, og[k])
+        errs[k] = _rel(p.grad, ref[k])
+        envs[k] = 1e-3 if H <= 64 else max(4 * _rel(og[k], ref[k]), 2e-2)
         if k.startswith("image_network.") and p.dim() == 4:
-            convs_h.append(p.grad.double().cpu().flatten())
-            convs_o.append(og[k].double().flatten())
-    worst = max(errs, key=errs.get)
-    tower = _rel(torch.cat(convs_h), torch.cat(convs_o))
+            convs[0].append(p.grad.double().cpu().flatten())
+            convs[1].append(og[k].double().flatten())
+            convs[2].append(ref[k].double().flatten())
+    worst = max(errs, key=lambda k: errs[k] / envs[k])
+    tower = _rel(torch.cat(convs[0]), torch.cat(convs[2]))
+    tower_env = 1e-3 if H <= 64 else max(2 * _rel(torch.cat(convs[1]), torch.cat(convs[2])), 5e-3)
     print(f"fusion fp32 B={B} {H}px: loss {loss.item():.6f} vs {Lo.item():.6f}; worst tensor {worst} "
-          f"{errs[worst]:.2e}; tower conv vector {tower:.2e}")
-    assert len(convs_h) == 36
+          f"{errs[worst]:.2e} (envelope {envs[worst]:.2e}); tower conv vector {tower:.2e} (envelope {tower_env:.2e})")
+    assert len(convs[0]) == 36
     for k, e in errs.items():
-        assert e < tol, (k, e)
-    assert tower < (1e-3 if H <= 64 else 5e-3), tower
+        assert e <= envs[k], (k, e, envs[k])
+    assert tower <= tower_env, (tower, tower_env)
 
 
 @pytest.mark.gpu
