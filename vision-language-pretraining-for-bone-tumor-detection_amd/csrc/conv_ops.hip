@@ -63,11 +63,30 @@ __device__ __forceinline__ uint4 xform_chunk(uint4 v, const float* sc, const flo
 // are wave-uniform scalars; every ResNet34 conv except the stem satisfies it
 // (the stem has its own loaders).
 
+// K-step order of the bf16 buffer-protocol convolutions (VLP_KPERM = 1):
+// channel chunk major, filter tap minor -- the 9 taps of one 64-channel chunk
+// are consecutive K-steps, so a tile's shifted re-reads of the same input rows
+// follow each other and hit L2 (tap-major order re-read them every C/64 steps,
+// and 32 tiles x C/64 steps x 32 KB per XCD overflowed its 4 MB L2)
+#ifndef VLP_KPERM
+#define VLP_KPERM 1
+#endif
+__device__ __forceinline__ int conv_kperm(int k, int K, int taps, int nch) {
+  if (k >= K) return k;
+  const int s = k >> 6;
+  const int chunk = s / taps, tap = s - chunk * taps;
+  return (tap * nch + chunk) << 6;
+}
+
 // ---- forward A operand: input patches, K-contiguous ----
 template <typename T, bool XF>
 struct ConvFwdA {
   static constexpr bool kKContig = true;
   static constexpr bool kDirect = !XF;
+  static constexpr bool kKPerm = VLP_KPERM && std::is_same<T, bf16>::value && !XF;
+  __device__ int kperm(int k) const {
+    return g.C % 64 ? k : conv_kperm(k, g.K, g.KH * g.KW, g.C >> 6);
+  }
   struct State { const T* base; int hi0, wi0; bool ok; };
   ConvGeom g; const T* x; const float* sc; const float* sh;
   __device__ State fixed(int m) const {
@@ -167,6 +186,10 @@ template <typename T>
 struct ConvDgradA {
   static constexpr bool kKContig = true;
   static constexpr bool kDirect = true;
+  static constexpr bool kKPerm = VLP_KPERM && std::is_same<T, bf16>::value;
+  __device__ int kperm(int k) const {
+    return g.Co % 64 ? k : conv_kperm(k, g.K, g.KH * g.KW, g.Co >> 6);
+  }
   struct State { const T* base; int hp, wp; bool ok; };
   ConvGeom g; const T* dy;
   __device__ State fixed(int m) const {
@@ -879,7 +902,7 @@ struct EpiConvFwd {
 // that BN's backward statistics: sum(g), sum(g * xhat).
 // 16-B store of a row-chunk epilogue (VLP_ROW_NT: non-temporal, streaming past the caches)
 #ifndef VLP_ROW_NT
-#define VLP_ROW_NT 0
+#define VLP_ROW_NT 1   // r4: measured +0.35 % per step (2 interleaved pairs), dgrad epilogues -1..-7 %
 #endif
 __device__ __forceinline__ void stg16_row(void* p, const uint4& v) {
 #if VLP_ROW_NT

@@ -179,6 +179,16 @@ template <class E, class = void> struct SplitTrait { static constexpr bool value
 template <class E> struct SplitTrait<E, std::void_t<decltype(E::kSplitOut)>> {
   static constexpr bool value = E::kSplitOut;
 };
+// K-step order: a loader with kKPerm maps the logical K offset of a 64-deep
+// step to the physical one (kperm); the buffer-protocol kernels apply the SAME
+// map to both operands, so the product is unchanged up to fp32 summation order
+template <class L, class = void> struct KPermTrait { static constexpr bool value = false; };
+template <class L> struct KPermTrait<L, std::void_t<decltype(L::kKPerm)>> { static constexpr bool value = L::kKPerm; };
+template <class L>
+__device__ __forceinline__ int kperm_of(const L& l, int k) {
+  if constexpr (KPermTrait<L>::value) return l.kperm(k);
+  else return k;
+}
 template <class E, class = void> struct RowTrait { static constexpr bool value = false; };
 template <class E> struct RowTrait<E, std::void_t<decltype(E::kRow)>> {
   static constexpr bool value = E::kRow;
@@ -1063,8 +1073,8 @@ gemm_bk_kernel(GemmShape sh, LA la, LB lb, EP ep) {
 
   // odd nk: tile 0 goes to slot 1 so the main loop always runs slot pairs
   const int s0 = (nk & 1) * STAGE;
-  sa.issue(la, nk > 0 ? ra : rz, kb, smem + s0, wv);
-  sb.issue(lb, nk > 0 ? rb : rz, kb, smem + s0 + ABYTES, wv);
+  sa.issue(la, nk > 0 ? ra : rz, kperm_of(la, kb), smem + s0, wv);
+  sb.issue(lb, nk > 0 ? rb : rz, kperm_of(la, kb), smem + s0 + ABYTES, wv);
 
   // one K-step: tile t sits in ring slot SL; tile t+1 is fetched into 1-SL
   auto body = [&](auto slc, int t) __attribute__((always_inline)) {
@@ -1083,8 +1093,9 @@ gemm_bk_kernel(GemmShape sh, LA la, LB lb, EP ep) {
     }
     const bool live = t + 1 < nk;
     char* f = smem + (1 - SL) * STAGE;
-    sa.issue(la, live ? ra : rz, kb + (t + 1) * BK, f, wv);
-    sb.issue(lb, live ? rb : rz, kb + (t + 1) * BK, f + ABYTES, wv);
+    const int kn = kperm_of(la, kb + (t + 1) * BK);
+    sa.issue(la, live ? ra : rz, kn, f, wv);
+    sb.issue(lb, live ? rb : rz, kn, f + ABYTES, wv);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -1175,10 +1186,10 @@ gemm_big_kernel(GemmShape sh, LA la, LB lb, EP ep) {
 
   // odd nk: tile 0 goes to slot 1 so the main loop always runs slot pairs
   const int s0 = (nk & 1) * STAGE;
-  sa.issue(la, nk > 0 ? ra : rz, kb, smem + s0, wv);
-  sb.issue(lb, nk > 0 ? rb : rz, kb, smem + s0 + ABYTES, wv);
-  sa.issue(la, nk > 1 ? ra : rz, kb + BK, smem + (STAGE - s0), wv);
-  sb.issue(lb, nk > 1 ? rb : rz, kb + BK, smem + (STAGE - s0) + ABYTES, wv);
+  sa.issue(la, nk > 0 ? ra : rz, kperm_of(la, kb), smem + s0, wv);
+  sb.issue(lb, nk > 0 ? rb : rz, kperm_of(la, kb), smem + s0 + ABYTES, wv);
+  sa.issue(la, nk > 1 ? ra : rz, kperm_of(la, kb + BK), smem + (STAGE - s0), wv);
+  sb.issue(lb, nk > 1 ? rb : rz, kperm_of(la, kb + BK), smem + (STAGE - s0) + ABYTES, wv);
   // MN-contig operands: one LDS address per (ring slot, fragment)
   constexpr int QA = MB < 4 ? MB : 4, QB = NB < 4 ? NB : 4;
   unsigned abase[2][LA::kKContig ? 1 : QA], bbase[2][LB::kKContig ? 1 : QB];
@@ -1244,8 +1255,9 @@ gemm_big_kernel(GemmShape sh, LA la, LB lb, EP ep) {
     raw_barrier();
     const bool live = t + 2 < nk;
     char* f = smem + SL * STAGE;
-    sa.issue(la, live ? ra : rz, kb + (t + 2) * BK, f, wv);
-    sb.issue(lb, live ? rb : rz, kb + (t + 2) * BK, f + ABYTES, wv);
+    const int kn = kperm_of(la, kb + (t + 2) * BK);
+    sa.issue(la, live ? ra : rz, kn, f, wv);
+    sb.issue(lb, live ? rb : rz, kn, f + ABYTES, wv);
 #pragma unroll
     for (int a = 0; a < MB; ++a)
 #pragma unroll
@@ -1454,8 +1466,9 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
     if constexpr (G == 0) ss.init(la, row0, kb, wg);
     else ss.init(lb, col0, kb, wg);
     auto fetch = [&](auto hc, int u, char* slot) __attribute__((always_inline)) {
-      if constexpr (G == 0) ss.template issue<decltype(hc)::value>(la, u < nh ? ra : rz, kb + (u >> 1) * BK, slot, wg);
-      else ss.template issue<decltype(hc)::value>(lb, u < nh ? rb : rz, kb + (u >> 1) * BK, slot + HA, wg);
+      const int k0 = kperm_of(la, kb + (u >> 1) * BK);
+      if constexpr (G == 0) ss.template issue<decltype(hc)::value>(la, u < nh ? ra : rz, k0, slot, wg);
+      else ss.template issue<decltype(hc)::value>(lb, u < nh ? rb : rz, k0, slot + HA, wg);
     };
     using H0 = std::integral_constant<int, 0>;
     using H1 = std::integral_constant<int, 1>;
@@ -1495,7 +1508,7 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
       unsigned xtap = 0;
       if constexpr (XA) {
         int ci0;
-        xtap = la.xtap(kb + (q >> 1) * BK, ci0);
+        xtap = la.xtap(kperm_of(la, kb + (q >> 1) * BK), ci0);
         const float* t = xtab + ci0 + (SL & 1) * 32 + fg * 8;
         xs0 = *reinterpret_cast<const v4f*>(t);
         xs1 = *reinterpret_cast<const v4f*>(t + 4);
