@@ -186,10 +186,9 @@ template <typename T>
 struct ConvDgradA {
   static constexpr bool kKContig = true;
   static constexpr bool kDirect = true;
-  static constexpr bool kKPerm = VLP_KPERM && std::is_same<T, bf16>::value;
-  __device__ int kperm(int k) const {
-    return g.Co % 64 ? k : conv_kperm(k, g.K, g.KH * g.KW, g.Co >> 6);
-  }
+  // the chunk-major order measured slower here (layer 3/4 +7-8 % per launch, r4d): tap-major kept
+  static constexpr bool kKPerm = false;
+  __device__ int kperm(int k) const { return k; }
   struct State { const T* base; int hp, wp; bool ok; };
   ConvGeom g; const T* dy;
   __device__ State fixed(int m) const {
