@@ -109,6 +109,15 @@ int vlp_conv_dgrad_relu_act(int dtype, const void* g_in, const void* y_in, const
                             int KH, int KW, int S, int P, const void* addend, const void* relu_out,
                             const uint8_t* relu_mask, const void* y, const float* mean,
                             const float* invstd, double* stat1, double* stat2, int stat_rep, void* stream);
+/* First block of layers 2-4 (timm BasicBlock with downsample, VisionLanguageModule.py:30-32):
+ * conv1's 3x3/2 data gradient with the 1x1/2 downsample's data gradient folded into
+ * pixel-parity class (0, 0) as extra K-steps -- replaces vlp_conv_dgrad of the
+ * downsample and the addend of vlp_conv_dgrad_relu.  dyd = dy + N*Ho*Wo*Co and
+ * wtd = wt + C*KH*KW*Co (one allocation each), bf16, KH = KW = 3, S = 2, P = 1. */
+int vlp_conv_dgrad_relu_ds(int dtype, const void* dy, const void* dyd, const void* wt, const void* wtd, void* g,
+                           int N, int H, int W, int C, int Co, int KH, int KW, int S, int P,
+                           const void* relu_out, const uint8_t* relu_mask, const void* y, const float* mean,
+                           const float* invstd, double* stat1, double* stat2, int stat_rep, void* stream);
 /* Weight gradient as split-K fp32 slabs: split s of the pixel reduction writes
  * split_ws[s][Co][KH][KW][C] (plain stores, no atomics); *nsplit receives the
  * split count (<= ws_floats / (Co*KH*KW*C)).  vlp_conv_wgrad_fold then sums the

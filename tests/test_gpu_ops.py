@@ -204,6 +204,56 @@ def test_conv_dgrad_act_matches_pass_then_dgrad(ops, N, H, epi):
     assert not ops.conv_dgrad_act_ok(g_in[:, :, :64].contiguous(), C, 3, 3, 1, 1)
 
 
+@pytest.mark.parametrize("N,Hi,C,Co", [(2, 64, 64, 128), (4, 32, 128, 256), (8, 16, 256, 512), (3, 14, 64, 128)])
+def test_conv_dgrad_relu_ds_fold(ops, N, Hi, C, Co):
+    """vlp_conv_dgrad_relu_ds: conv1 (3x3/2) data gradient with the downsample's
+    1x1/2 data gradient folded into parity class (0, 0), against torch autograd of
+    conv1(x) + downsample(x) in fp32 on the same bf16 operands, and against the
+    unfused HIP path (downsample dgrad as the addend): the fold sums the two in
+    fp32 inside one GEMM where the unfused path rounds the addend to bf16 first.
+    Shapes: the 256x64 (C = 64), 128x128 (C = 128) and ping-pong 256x256
+    (C = 256) class GEMMs, and an odd spatial size (14 -> 7)."""
+    torch.manual_seed(21)
+    bf = torch.bfloat16
+    dev = torch.device("cuda")
+    Ho = (Hi + 1) // 2
+    x = torch.randn(N, C, Hi, Hi).to(bf).float().requires_grad_()
+    w1 = (torch.randn(Co, C, 3, 3) * (9 * C) ** -0.5).to(bf).float()
+    wd = (torch.randn(Co, C, 1, 1) * C ** -0.5).to(bf).float()
+    y1 = F.conv2d(x, w1, stride=2, padding=1)
+    yd = F.conv2d(x, wd, stride=2)
+    dy = torch.randn_like(y1).to(bf).float()
+    dyd = torch.randn_like(yd).to(bf).float()
+    (y1 * dy + yd * dyd).sum().backward()
+    buf = torch.empty(C * 9 * Co + C * Co, dtype=bf, device=dev)
+    wt, wtd = buf[:C * 9 * Co].view(C, 3, 3, Co), buf[C * 9 * Co:].view(C, 1, 1, Co)
+    ops.pack_conv(w1.cuda(), None, wt)
+    ops.pack_conv(wd.cuda(), None, wtd)
+    pair = torch.empty(2, N, Ho, Ho, Co, dtype=bf, device=dev)
+    pair[0].copy_(nhwc(dy).to(bf))
+    pair[1].copy_(nhwc(dyd).to(bf))
+    act = torch.randn(N, Hi, Hi, C, device=dev).to(bf)            # block input (ReLU output stand-in)
+    ye = torch.randn(N, Hi, Hi, C, device=dev).to(bf)
+    mu, ist = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5
+    s1, s2, r1, r2 = (torch.zeros(4 * C, dtype=torch.float64, device=dev) for _ in range(4))
+    g = ops.conv_dgrad_relu_ds(pair[0], pair[1], wt, wtd, Hi, Hi, C, 3, 3, 2, 1, act, ye, mu, ist, s1, s2, stat_rep=4)
+    add = ops.conv_dgrad(pair[1], wtd, Hi, Hi, C, 1, 1, 2, 0)
+    g_ref = ops.conv_dgrad_relu(pair[0], wt, Hi, Hi, C, 3, 3, 2, 1, act, ye, mu, ist, r1, r2, addend=add, stat_rep=4)
+    torch.cuda.synchronize()
+    mask = (nchw(act.float().cpu()) > 0).float()
+    ref = x.grad * mask
+    got = nchw(g.float().cpu())
+    assert rel(got, ref) < tol(bf), rel(got, ref)
+    assert rel(got, nchw(g_ref.float().cpu())) < tol(bf)
+    # BN backward sums of g against ye: both paths, and torch on the HIP output
+    xh = (nchw(ye.float().cpu()) - mu.cpu()[None, :, None, None]) * ist.cpu()[None, :, None, None]
+    assert rel(s1.view(4, C).sum(0).cpu(), got.sum((0, 2, 3)).double()) < 1e-4
+    assert rel(s2.view(4, C).sum(0).cpu(), (got * xh).sum((0, 2, 3)).double()) < 1e-4
+    # non-adjacent operands are refused
+    with pytest.raises(RuntimeError):
+        ops.conv_dgrad_relu_ds(pair[0], pair[0], wt, wtd, Hi, Hi, C, 3, 3, 2, 1, act, ye, mu, ist, s1, s2)
+
+
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_dgrad_wgrad(ops, dt, case):

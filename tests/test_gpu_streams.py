@@ -191,3 +191,36 @@ def test_layer1_bwd_act_fused_matches_pass_bf16():
     print("layer-1 bwd fused vs pass, worst (excess, name, diff, noise):", worst[-3:])
     assert worst[-1][0] <= 1e-30, worst[-3:]
     assert abs(l2 - l0) <= 4 * max(abs(l1 - l0), abs(l3 - l2)) + 1e-7, (l0, l1, l2, l3)
+
+
+def test_ds_fold_matches_separate_downsample_bf16():
+    """Test E: the downsample's data gradient folded into conv1's stride-2 class (0, 0)
+    GEMM (resnet34._USE_DS_FOLD) vs its own launch + addend.  Not bit-identical (the
+    fold sums the two branches in fp32 before one bf16 rounding), so every image-tower
+    gradient must stay within 1e-2 rel-L2 of the unfused step and the loss equal."""
+    from src.models.pretrain.VisionLanguageModule import VisionLanguageModule
+    from vlp_amd import resnet34 as r34
+    torch.manual_seed(4)
+    m = VisionLanguageModule("resnet34", "tinybert", functools.partial(torch.optim.AdamW, lr=5e-5), False, False,
+                             512, 312, 128, compute_dtype="bf16", text_dropout=0.0)
+    m.train()
+    with torch.no_grad():
+        for k, p in m.named_parameters():
+            if k.endswith("bn2.weight"):
+                p.fill_(0.5)
+    b = synth_batch(4, 256, 16, 9, with_u8=True)
+    b = {"x-ray-u8": b["x-ray-u8"].cuda(), "label": b["label"], "caption": b["caption"],
+         "caption_tokenized": {k: v.cuda() for k, v in b["caption_tokenized"].items()}}
+    was = r34._USE_DS_FOLD
+    try:
+        r34._USE_DS_FOLD = False
+        l0, g0 = _grads(m, b)
+        r34._USE_DS_FOLD = True
+        l1, g1 = _grads(m, b)
+    finally:
+        r34._USE_DS_FOLD = was
+    assert abs(l1 - l0) <= 1e-6, (l0, l1)
+    img = [k for k in g0 if k.startswith("image_encoder.") and g0[k].norm() > 0]
+    worst = sorted(((_rel(g1[k], g0[k]), k) for k in img), reverse=True)[:3]
+    print("ds fold vs separate, worst rel-L2:", worst)
+    assert worst[0][0] <= 1e-2, worst

@@ -287,12 +287,18 @@ static S2Class make_s2class(const ConvGeom& g, int ph, int pw) {
   c.fd_ntw = make_fastdiv(c.ntw > 0 ? c.ntw : 1);
   return c;
 }
+// Downsample fold (class (0, 0) of a 3x3/2 conv beside its 1x1/2 downsample):
+// the K-steps past Kc1 read the downsample's output gradient dyd (same pixel
+// grid, placed dd_off elements after dy in one allocation) against the
+// downsample's packed weights (wd_off elements after wt) -- the two data
+// gradients sum in one GEMM, no separate launch and no addend pass.
 template <typename T>
 struct ConvDgradS2A {
   static constexpr bool kKContig = true;
   static constexpr bool kDirect = true;
   struct State { const T* base; int hb, wb; bool ok; };   // hb = (h + P - kh0) / 2
   ConvGeom g; S2Class c; const T* dy; int Mc, Kc;
+  int Kc1 = 1 << 30; long long dd_off = 0;                // downsample segment (buffer protocol only)
   __device__ State fixed(int m) const {
     State s;
     s.ok = m < Mc;
@@ -339,7 +345,9 @@ struct ConvDgradS2A {
   static constexpr bool kBuf = true;
   struct BState { unsigned base; unsigned mask; };
   struct BStep { unsigned delta; unsigned tap; };
-  __device__ rsrc_t rsrc() const { return buf_rsrc(dy, (unsigned)((size_t)g.N * g.Ho * g.Wo * g.Co * sizeof(T))); }
+  __device__ rsrc_t rsrc() const {
+    return buf_rsrc(dy, (unsigned)(((size_t)dd_off + (size_t)g.N * g.Ho * g.Wo * g.Co) * sizeof(T)));
+  }
   __device__ BState bstart(int m, int koff, int) const {
     const State f = fixed(m);
     unsigned mask = 0;
@@ -353,6 +361,8 @@ struct ConvDgradS2A {
     return BState{(unsigned)(e * (long long)sizeof(T)), f.ok ? mask : 0u};
   }
   __device__ BStep bstep(int k0) const {
+    if (k0 >= Kc1)   // downsample segment: dyd at the class pixel itself (tap 0 of class (0, 0))
+      return BStep{(unsigned)((dd_off + (k0 - Kc1)) * (long long)sizeof(T)), 0u};
     const int tap = fdiv(k0, g.fd_co), co0 = k0 - tap * g.Co;
     const int a = fdiv(tap, c.fd_ntw), b = tap - a * c.ntw;
     return BStep{(unsigned)((co0 - ((long long)a * g.Wo + b) * g.Co) * (long long)sizeof(T)), (unsigned)tap};
@@ -404,6 +414,7 @@ struct WtS2B {
   static constexpr bool kDirect = true;
   struct State { const T* p; bool ok; };
   const T* wt; ConvGeom g; S2Class c; int Kc;
+  int Kc1 = 1 << 30; long long wd_off = 0;                // downsample segment (buffer protocol only)
   __device__ State fixed(int ci) const {
     return State{wt + (size_t)(ci < g.C ? ci : 0) * g.KH * g.KW * g.Co, ci < g.C};
   }
@@ -431,18 +442,28 @@ struct WtS2B {
   }
   // buffer protocol (Kc is a multiple of the K-step: no per-chunk k check)
   static constexpr bool kBuf = true;
-  struct BState { unsigned o; };
-  struct BStep { unsigned delta; };
-  __device__ rsrc_t rsrc() const { return buf_rsrc(wt, (unsigned)((size_t)g.C * g.KH * g.KW * g.Co * sizeof(T))); }
+  struct BState { unsigned o, od; };
+  struct BStep { unsigned delta; unsigned ds; };
+  __device__ rsrc_t rsrc() const {
+    const size_t n = wd_off ? (size_t)wd_off + (size_t)g.C * g.Co : (size_t)g.C * g.KH * g.KW * g.Co;
+    return buf_rsrc(wt, (unsigned)(n * sizeof(T)));
+  }
   __device__ BState bstart(int ci, int koff, int) const {
-    return BState{ci < g.C ? (unsigned)(((size_t)ci * g.KH * g.KW * g.Co + koff) * sizeof(T)) : kOOB};
+    if (ci >= g.C) return BState{kOOB, kOOB};
+    return BState{(unsigned)(((size_t)ci * g.KH * g.KW * g.Co + koff) * sizeof(T)),
+                  (unsigned)(((size_t)wd_off + (size_t)ci * g.Co) * sizeof(T))};
   }
   __device__ BStep bstep(int k0) const {
+    if (k0 >= Kc1) return BStep{(unsigned)((k0 - Kc1) * (long long)sizeof(T)), 1u};
     const int tap = fdiv(k0, g.fd_co), co0 = k0 - tap * g.Co;
     const int a = fdiv(tap, c.fd_ntw), b = tap - a * c.ntw;
-    return BStep{(unsigned)((((long long)(c.kh0 + 2 * a) * g.KW + c.kw0 + 2 * b) * g.Co + co0) * (long long)sizeof(T))};
+    return BStep{(unsigned)((((long long)(c.kh0 + 2 * a) * g.KW + c.kw0 + 2 * b) * g.Co + co0) * (long long)sizeof(T)),
+                 0u};
   }
-  __device__ unsigned boff(BState& s, const BStep& st) const { return s.o + st.delta; }
+  __device__ unsigned boff(BState& s, const BStep& st) const {
+    const unsigned b = st.ds ? s.od : s.o;
+    return b == kOOB ? kOOB : b + st.delta;
+  }
 };
 
 // ---- weight-gradient B operand: input patches, MN-contiguous over (kh,kw,ci) ----
@@ -1649,7 +1670,8 @@ static int conv_dgrad_t(const void* dy, const void* wt, void* dx, ConvGeom g, co
 template <typename T, bool BITS>
 static int conv_dgrad_relu_impl(const void* dy, const void* wt, void* gout, ConvGeom g0, const void* addend,
                                 const void* relu_out, const uint8_t* relu_mask, const void* y, const float* mean,
-                                const float* invstd, double* s1, double* s2, int rep, hipStream_t st) {
+                                const float* invstd, double* s1, double* s2, int rep, hipStream_t st,
+                                long long dd_off = 0, long long wd_off = 0) {
   ConvGeom g = g0;
   g.M = g.N * g.H * g.W;
   g.K = g.KH * g.KW * g.Co;
@@ -1659,10 +1681,17 @@ static int conv_dgrad_relu_impl(const void* dy, const void* wt, void* gout, Conv
     for (int ph = 0; ph < 2; ++ph)
       for (int pw = 0; pw < 2; ++pw) {
         S2Class c = make_s2class(g, ph, pw);
-        const int Mc = g.N * c.Hc * c.Wc, Kc = c.nth * c.ntw * g.Co;
+        const int Mc = g.N * c.Hc * c.Wc, Kc1 = c.nth * c.ntw * g.Co;
         if (Mc <= 0) continue;
+        // the downsample's 1x1/2 data gradient lands on the (0, 0) pixels only
+        const bool fold = dd_off && ph == 0 && pw == 0;
+        const int Kc = Kc1 + (fold ? g.Co : 0);
         ConvDgradS2A<T> la{g, c, (const T*)dy, Mc, Kc};
         WtS2B<T> lb{(const T*)wt, g, c, Kc};
+        if (fold) {
+          la.Kc1 = Kc1; la.dd_off = dd_off;
+          lb.Kc1 = Kc1; lb.wd_off = wd_off;
+        }
         EpiS2Remap<EpiDgradRelu<T, BITS>> ep{s1, s2, rep, in, c, g.H, g.W};
         const int r = gemm_s2<T>(Mc, g.C, Kc, la, lb, ep, st);
         if (r) return r;
@@ -2028,6 +2057,30 @@ VLP_EXPORT int vlp_conv_dgrad_relu(int dtype, const void* dy, const void* wt, vo
                                    stat_rep, st);
   return conv_dgrad_relu_t<float>(dy, wt, g, geo, addend, relu_out, relu_mask, y, mean, invstd, stat1, stat2,
                                   stat_rep, st);
+}
+
+// Stride-2 block entry (layers 2-4, block 0): conv1's 3x3/2 data gradient with the
+// 1x1/2 downsample's data gradient folded into parity class (0, 0) as extra K-steps
+// (replaces vlp_conv_dgrad of the downsample + the addend of vlp_conv_dgrad_relu).
+// dyd must follow dy in one allocation (dyd = dy + N*Ho*Wo*Co) and wtd must follow
+// wt (wtd = wt + C*KH*KW*Co); bf16 only.
+VLP_EXPORT int vlp_conv_dgrad_relu_ds(int dtype, const void* dy, const void* dyd, const void* wt, const void* wtd,
+                                      void* g, int N, int H, int W, int C, int Co, int KH, int KW, int S, int P,
+                                      const void* relu_out, const uint8_t* relu_mask, const void* y,
+                                      const float* mean, const float* invstd, double* stat1, double* stat2,
+                                      int stat_rep, void* stream) {
+  ConvGeom geo = make_geom(N, H, W, C, Co, KH, KW, S, P);
+  const long long dd = (long long)geo.N * geo.Ho * geo.Wo * geo.Co, wd = (long long)C * KH * KW * Co;
+  if (dtype != VLP_BF16 || S != 2 || KH != 3 || KW != 3 || P != 1 || C % 8 || Co % 64 ||
+      (relu_out == nullptr) == (relu_mask == nullptr) || (const bf16*)dyd != (const bf16*)dy + dd ||
+      (const bf16*)wtd != (const bf16*)wt + wd || (size_t)2 * dd * 2 >= (1ull << 32))
+    return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  if (relu_mask)
+    return conv_dgrad_relu_impl<bf16, true>(dy, wt, g, geo, nullptr, relu_out, relu_mask, y, mean, invstd, stat1,
+                                            stat2, stat_rep, st, dd, wd);
+  return conv_dgrad_relu_impl<bf16, false>(dy, wt, g, geo, nullptr, relu_out, relu_mask, y, mean, invstd, stat1,
+                                           stat2, stat_rep, st, dd, wd);
 }
 
 VLP_EXPORT int vlp_conv_wgrad(int dtype, const void* dy, const void* x, float* dw_ws, int N, int H,

@@ -152,6 +152,23 @@ def conv_dgrad_relu_act(g_in, y_in, in_coef, dy_out, wt, H, W, C, KH, KW, S, P, 
     return g
 
 
+def conv_dgrad_relu_ds(dy, dyd, wt, wtd, H, W, C, KH, KW, S, P, relu_out, y, mean, invstd, stat1, stat2,
+                       stat_rep=1, out=None):
+    """conv_dgrad_relu of a stride-2 conv with the 1x1/2 downsample's data gradient
+    (dyd against wtd) folded into parity class (0, 0) in the same GEMMs
+    (vlp_conv_dgrad_relu_ds).  dyd must follow dy and wtd follow wt in memory."""
+    N, Ho, Wo, Co = dy.shape
+    g = out if out is not None else torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
+    bits = relu_out.dtype == torch.uint8
+    flops = 2.0 * N * Ho * Wo * Co * C * (KH * KW + 1)
+    tk = ktimer.begin(f"conv_dgrad[relu,ds]{_tile_auto(C)}", flops)
+    lib().vlp_conv_dgrad_relu_ds(dcode(dy), ptr(dy), ptr(dyd), ptr(wt), ptr(wtd), ptr(g), N, H, W, C, Co, KH, KW, S,
+                                 P, None if bits else ptr(relu_out), ptr(relu_out) if bits else None, ptr(y),
+                                 ptr(mean), ptr(invstd), ptr(stat1), ptr(stat2), int(stat_rep), _s())
+    ktimer.end(tk)
+    return g
+
+
 def conv_wgrad(dy, x, KH, KW, S, P, dw_ws, in_scale=None, in_shift=None, dyT=None):
     N, H, W, C = x.shape
     Co = dy.shape[-1]

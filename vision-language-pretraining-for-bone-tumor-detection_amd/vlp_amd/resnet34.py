@@ -58,6 +58,9 @@ _USE_STEM_FUSED = True
 # ring (vlp_conv_dgrad_bn_act / vlp_conv_dgrad_relu_act) instead of a separate
 # bn_bwd_apply pass (tests/test_gpu_streams.py holds on vs off)
 _USE_BWD_ACT = True
+# bf16 stride-2 block entries: the downsample's data gradient folded into conv1's
+# parity class (0, 0) (vlp_conv_dgrad_relu_ds) instead of its own launch + an addend
+_USE_DS_FOLD = True
 # bf16 layer 1: bn1 + ReLU applied in conv2's input ring (vlp_conv_fwd_act), a1
 # written by that kernel; False keeps the separate bn_add_relu pass
 _USE_ACT_FUSED = True
@@ -223,7 +226,18 @@ class ResNet34Tower(ArenaModule):
                 ws["conv1.wp"] = torch.empty(64, 256, dtype=T, device=dev)
             else:
                 ws[c.key + ".wp"] = torch.empty(c.Co, c.KH, c.KW, c.C, dtype=T, device=dev)
-                ws[c.key + ".wt"] = torch.empty(c.C, c.KH, c.KW, c.Co, dtype=T, device=dev)
+                if c.key.endswith(".downsample.0"):
+                    continue
+                cd = self._convs.get(c.key[:-len("conv1")] + "downsample.0") if c.key.endswith(".conv1") else None
+                if cd is not None:
+                    # a stage's first conv1 and its downsample: transposed weights in one
+                    # allocation, downsample second (vlp_conv_dgrad_relu_ds reads both)
+                    n1 = c.C * c.KH * c.KW * c.Co
+                    buf = torch.empty(n1 + cd.C * cd.Co, dtype=T, device=dev)
+                    ws[c.key + ".wt"] = buf[:n1].view(c.C, c.KH, c.KW, c.Co)
+                    ws[cd.key + ".wt"] = buf[n1:].view(cd.C, 1, 1, cd.Co)
+                else:
+                    ws[c.key + ".wt"] = torch.empty(c.C, c.KH, c.KW, c.Co, dtype=T, device=dev)
         # wgrad workspaces (fp32, GEMM layout), one flat buffer zeroed per backward
         off = 0
         self._wg_off = {}
@@ -493,8 +507,16 @@ class ResNet34Tower(ArenaModule):
             dy2 = torch.empty_like(y2)
             A = (y2, mu2, is2, self.arena.view(k2 + ".weight"), sg2, sgx2, dy2)
             Bside, g_id = None, None
+            prev = self._blocks[bi - 1] if bi > 0 else None
+            ds_fold = (_USE_DS_FOLD and has_ds and T == torch.bfloat16 and c1.S == 2 and prev is not None
+                       and not prev[1] and tuple(y1.shape) == tuple(yd.shape))
+            dy_pair = None
             if has_ds:
-                dyd = torch.empty_like(yd)
+                if ds_fold:   # dy1 and dyd in one allocation (dyd second): one GEMM reads both
+                    dy_pair = torch.empty((2,) + tuple(y1.shape), dtype=y1.dtype, device=dev)
+                    dyd = dy_pair[1]
+                else:
+                    dyd = torch.empty_like(yd)
                 Bside = (yd, mud, isd, self.arena.view(kd + ".weight"), sg2, sgxd, dyd)
             elif dout_masked:
                 g_id = dout          # the identity branch's gradient is g itself
@@ -525,7 +547,7 @@ class ResNet34Tower(ArenaModule):
                             self.arena.gview(k1 + ".bias"))
             sg1, sgx1 = sg1f[:C], sgx1f[:C]
             self._wgrad(ws, c2, dy2, B["a1"], dyT=tA)
-            dy1 = torch.empty_like(y1)
+            dy1 = dy_pair[0] if dy_pair is not None else torch.empty_like(y1)
             if fuse_in:
                 ops.bn_bwd_coef(M, self.arena.view(k1 + ".weight"), is1, mu1, sg1, sgx1, coef[1])
             else:
@@ -536,11 +558,11 @@ class ResNet34Tower(ArenaModule):
             addend = g_id
             if has_ds:
                 cd = self._convs[pre + ".downsample.0"]
-                addend = ops.conv_dgrad(dyd, ws[cd.key + ".wt"], Hi, Wi, Cin, 1, 1, cd.S, 0)
+                if not ds_fold:
+                    addend = ops.conv_dgrad(dyd, ws[cd.key + ".wt"], Hi, Wi, Cin, 1, 1, cd.S, 0)
                 self._wgrad(ws, cd, dyd, x, dyT=tB)
             # the gradient reaching block bi-1 passes its output ReLU and feeds its bn2:
             # when that block has no downsample branch, mask + reduce in this epilogue
-            prev = self._blocks[bi - 1] if bi > 0 else None
             stem_sums = bi == 0 and saved.get("yarg") is not None
             if stem_sums:
                 # block 0's input is the maxpool output p = relu(bn1(y0)) at each window's
@@ -568,6 +590,10 @@ class ResNet34Tower(ArenaModule):
                     dx = ops.conv_dgrad_relu_act(g1, y1, coef[1], dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, 1, 1,
                                                  rmask, blocks[bi - 1]["y2"], mup, isp, sgpf, sgxpf,
                                                  addend=addend, stat_rep=STAT_REP)
+                elif ds_fold:
+                    dx = ops.conv_dgrad_relu_ds(dy1, dyd, ws[c1.key + ".wt"], ws[cd.key + ".wt"], Hi, Wi, Cin, 3, 3,
+                                                c1.S, 1, rmask, blocks[bi - 1]["y2"], mup, isp, sgpf, sgxpf,
+                                                stat_rep=STAT_REP)
                 else:
                     dx = ops.conv_dgrad_relu(dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, rmask,
                                              blocks[bi - 1]["y2"], mup, isp, sgpf, sgxpf, addend=addend,
