@@ -451,7 +451,7 @@ struct WtS2B {
   __device__ BState bstart(int ci, int koff, int) const {
     if (ci >= g.C) return BState{kOOB, kOOB};
     return BState{(unsigned)(((size_t)ci * g.KH * g.KW * g.Co + koff) * sizeof(T)),
-                  (unsigned)(((size_t)wd_off + (size_t)ci * g.Co) * sizeof(T))};
+                  (unsigned)(((size_t)wd_off + (size_t)ci * g.Co + koff) * sizeof(T))};
   }
   __device__ BStep bstep(int k0) const {
     if (k0 >= Kc1) return BStep{(unsigned)((k0 - Kc1) * (long long)sizeof(T)), 1u};
