@@ -109,6 +109,16 @@ int vlp_conv_dgrad_relu_act(int dtype, const void* g_in, const void* y_in, const
                             int KH, int KW, int S, int P, const void* addend, const void* relu_out,
                             const uint8_t* relu_mask, const void* y, const float* mean,
                             const float* invstd, double* stat1, double* stat2, int stat_rep, void* stream);
+/* Second block of layers 2-4 (timm BasicBlock backward, VisionLanguageModule.py:30-32): conv1's
+ * data gradient (+ addend) through the previous block's output ReLU (relu_mask sign bits),
+ * with that block's bn2 (y, mean, invstd) and downsample-BN (yd, meand, invstdd) backward
+ * sums stat1 = sum g, stat2 = sum g*xhat, stat3 = sum g*xhatd in the epilogue (replaces
+ * vlp_bn_bwd_reduce over dout, out, y2, yd).  bf16, stride 1, C >= 128, C % 64 == 0. */
+int vlp_conv_dgrad_relu2(int dtype, const void* dy, const void* wt, void* g, int N, int H, int W, int C, int Co,
+                         int KH, int KW, int S, int P, const void* addend, const uint8_t* relu_mask, const void* y,
+                         const float* mean, const float* invstd, const void* yd, const float* meand,
+                         const float* invstdd, double* stat1, double* stat2, double* stat3, int stat_rep,
+                         void* stream);
 /* First block of layers 2-4 (timm BasicBlock with downsample, VisionLanguageModule.py:30-32):
  * conv1's 3x3/2 data gradient with the 1x1/2 downsample's data gradient folded into
  * pixel-parity class (0, 0) as extra K-steps -- replaces vlp_conv_dgrad of the

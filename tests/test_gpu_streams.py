@@ -195,8 +195,10 @@ def test_layer1_bwd_act_fused_matches_pass_bf16():
 
 def test_ds_fold_matches_separate_downsample_bf16():
     """Test E: the downsample's data gradient folded into conv1's stride-2 class (0, 0)
-    GEMM (resnet34._USE_DS_FOLD) vs its own launch + addend.  Not bit-identical (the
-    fold sums the two branches in fp32 before one bf16 rounding), so every image-tower
+    GEMM (resnet34._USE_DS_FOLD) and the next block's three-sum ReLU epilogue
+    (resnet34._USE_RELU2) vs the separate downsample launch + addend and the
+    bn_bwd_reduce pass.  Not bit-identical (the fold sums the two branches in fp32
+    before one bf16 rounding; the sums run in another order), so every image-tower
     gradient must stay within 1e-2 rel-L2 of the unfused step and the loss equal."""
     from src.models.pretrain.VisionLanguageModule import VisionLanguageModule
     from vlp_amd import resnet34 as r34
@@ -211,14 +213,14 @@ def test_ds_fold_matches_separate_downsample_bf16():
     b = synth_batch(4, 256, 16, 9, with_u8=True)
     b = {"x-ray-u8": b["x-ray-u8"].cuda(), "label": b["label"], "caption": b["caption"],
          "caption_tokenized": {k: v.cuda() for k, v in b["caption_tokenized"].items()}}
-    was = r34._USE_DS_FOLD
+    was = (r34._USE_DS_FOLD, r34._USE_RELU2)
     try:
-        r34._USE_DS_FOLD = False
+        r34._USE_DS_FOLD = r34._USE_RELU2 = False
         l0, g0 = _grads(m, b)
-        r34._USE_DS_FOLD = True
+        r34._USE_DS_FOLD = r34._USE_RELU2 = True
         l1, g1 = _grads(m, b)
     finally:
-        r34._USE_DS_FOLD = was
+        r34._USE_DS_FOLD, r34._USE_RELU2 = was
     assert abs(l1 - l0) <= 1e-6, (l0, l1)
     img = [k for k in g0 if k.startswith("image_encoder.") and g0[k].norm() > 0]
     worst = sorted(((_rel(g1[k], g0[k]), k) for k in img), reverse=True)[:3]

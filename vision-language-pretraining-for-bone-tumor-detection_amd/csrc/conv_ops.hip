@@ -1145,6 +1145,56 @@ struct EpiDgradRelu {
   __device__ void store8(int row, int col, const uint4& u) const { stg16(g_out + (size_t)row * C + col, u); }
 };
 
+// data gradient (+ residual-branch addend) through the output ReLU of a block
+// whose output feeds BOTH its bn2 and its downsample BN (the first block of
+// layers 2-4): g = (dgrad + addend) * (out > 0) (sign bits), plus that block's
+// three backward sums sum(g), sum(g * xhat2), sum(g * xhatd) -- replaces the
+// separate bn_bwd_reduce pass over (dout, out, y2, yd) and the masked copy of g.
+// Row-chunk epilogue only (the host routes it to the LDS-DMA kernels).
+template <typename T>
+struct EpiDgradRelu2 {
+  static constexpr bool kStats = true;
+  static constexpr bool kStats3 = true;
+  double* stat1; double* stat2; int stat_rep; double* stat3;
+  T* g_out; const T* addend; int C;
+  const uint8_t* rmask; const T* y; const T* yd;
+  const float* mean; const float* invstd; const float* meand; const float* invstdd;
+  struct Pre { uint4 u[4]; };
+  static constexpr bool kRow = true;
+  static constexpr int kCoefs = 4;
+  static constexpr int kPreDepth = 6;
+  __device__ const float* coef(int k) const { return k == 0 ? mean : k == 1 ? invstd : k == 2 ? meand : invstdd; }
+  __device__ void pre8(int row, int col, Pre& p) const {
+    const size_t o = (size_t)row * C + col;
+    p.u[0] = addend ? ldg16(addend + o) : zero4();
+    p.u[1].x = rmask[o >> 3];
+    p.u[2] = ldg16(y + o);
+    p.u[3] = ldg16(yd + o);
+  }
+  __device__ void row8r3(int row, int col, const float (&v)[8], const Pre& p, float (&s1)[8], float (&s2)[8],
+                         float (&s3)[8], const float (&cf)[4][8]) const {
+    const size_t o = (size_t)row * C + col;
+    float a[8], y2[8], y3[8], g[8];
+    Chunk<bf16>::unpack(p.u[0], a);
+    Chunk<bf16>::unpack(p.u[2], y2);
+    Chunk<bf16>::unpack(p.u[3], y3);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      g[j] = ((p.u[1].x >> j) & 1u) ? v[j] + a[j] : 0.f;
+      s1[j] += g[j];
+      s2[j] += g[j] * ((y2[j] - cf[0][j]) * cf[1][j]);
+      s3[j] += g[j] * ((y3[j] - cf[2][j]) * cf[3][j]);
+    }
+    stg16_row(g_out + o, Chunk<bf16>::pack(g));
+  }
+  // non-row epilogue forms (instantiated by the dispatch, never launched: the
+  // host entry point refuses shapes that would not take a row-chunk kernel)
+  static constexpr bool kStage = false;
+  __device__ v4f value(int, int, v4f v, v4f& s1, v4f& s2) const { s1 = s2 = v4f{0.f, 0.f, 0.f, 0.f}; return v; }
+  __device__ void operator()(int, int, v4f, v4f& s1, v4f& s2) const { s1 = s2 = v4f{0.f, 0.f, 0.f, 0.f}; }
+  __device__ void store8(int row, int col, const uint4& u) const { stg16(g_out + (size_t)row * C + col, u); }
+};
+
 // ---------------- tile-config dispatch ----------------
 template <typename T, class LA, class LB, class EP>
 static int gemm_auto(int M, int N, int K, int ksplit, const LA& la, const LB& lb, const EP& ep,
@@ -2057,6 +2107,29 @@ VLP_EXPORT int vlp_conv_dgrad_relu(int dtype, const void* dy, const void* wt, vo
                                    stat_rep, st);
   return conv_dgrad_relu_t<float>(dy, wt, g, geo, addend, relu_out, relu_mask, y, mean, invstd, stat1, stat2,
                                   stat_rep, st);
+}
+
+// The second block of layers 2-4: conv1's data gradient (+ the identity
+// gradient) through the previous block's output ReLU (sign bits) with that
+// block's bn2 AND downsample-BN backward sums in the epilogue (EpiDgradRelu2).
+VLP_EXPORT int vlp_conv_dgrad_relu2(int dtype, const void* dy, const void* wt, void* g, int N, int H, int W, int C,
+                                    int Co, int KH, int KW, int S, int P, const void* addend,
+                                    const uint8_t* relu_mask, const void* y, const float* mean, const float* invstd,
+                                    const void* yd, const float* meand, const float* invstdd, double* stat1,
+                                    double* stat2, double* stat3, int stat_rep, void* stream) {
+  ConvGeom g0 = make_geom(N, H, W, C, Co, KH, KW, S, P);
+  // row-chunk epilogue kernels only: bf16 LDS-DMA engine, stride 1, N = C >= 128, K a multiple of 64
+  if (dtype != VLP_BF16 || gemm_variant() < 5 || S != 1 || C < 128 || C % 64 || Co % 64 || !relu_mask || !y ||
+      !yd || !mean || !invstd || !meand || !invstdd || !stat1 || !stat2 || !stat3)
+    return (int)hipErrorInvalidValue;
+  ConvGeom g1 = g0;
+  g1.M = g1.N * g1.H * g1.W;
+  g1.K = g1.KH * g1.KW * g1.Co;
+  EpiDgradRelu2<bf16> ep{stat1, stat2, stat_rep, stat3, (bf16*)g, (const bf16*)addend, g1.C, relu_mask,
+                         (const bf16*)y, (const bf16*)yd, mean, invstd, meand, invstdd};
+  ConvDgradA<bf16> la{g1, (const bf16*)dy};
+  KMat<bf16> lb{(const bf16*)wt, g1.K, g1.C, g1.K};
+  return gemm_auto<bf16>(g1.M, g1.C, g1.K, 1, la, lb, ep, (hipStream_t)stream);
 }
 
 // Stride-2 block entry (layers 2-4, block 0): conv1's 3x3/2 data gradient with the

@@ -173,6 +173,12 @@ template <class E> struct StageTrait<E, std::void_t<decltype(E::kStage)>> {
 };
 // operands a row-chunk epilogue fetches ahead of its row8() call (16-B chunks)
 struct RowPre { uint4 u[3]; };
+// row-chunk epilogues may declare their own prefetch record (E::Pre) and a third
+// per-column statistic (E::kStats3, E::stat3, row8r3 instead of row8r)
+template <class E, class = void> struct PreTypeTrait { using type = RowPre; };
+template <class E> struct PreTypeTrait<E, std::void_t<typename E::Pre>> { using type = typename E::Pre; };
+template <class E, class = void> struct Stat3Trait { static constexpr bool value = false; };
+template <class E> struct Stat3Trait<E, std::void_t<decltype(E::kStats3)>> { static constexpr bool value = E::kStats3; };
 // split-K epilogues that write their own partial slab (no atomics): the kernel
 // hands the epilogue its split index via at_split(split)
 template <class E, class = void> struct SplitTrait { static constexpr bool value = false; };
@@ -620,6 +626,12 @@ __device__ __forceinline__ void wait_vmcnt() {
 }
 __device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
+template <class EP>
+__device__ __forceinline__ double* stat3_of(const EP& ep) {
+  if constexpr (Stat3Trait<EP>::value) return ep.stat3;
+  else return nullptr;
+}
+
 // Epilogue shared by the multi-stage kernels: lane l = 16g + i owns
 // C[row = rbase + i][col = cbase + 4g .. 4g+3] of each 16x16 block.
 template <int BM, int BN, int WGM, int WGN, class EP, int MB, int NB>
@@ -670,7 +682,10 @@ __device__ __forceinline__ void ms_epilogue(const GemmShape& sh, const EP& ep, v
     const int col = col0 + c * 8;
     const int r0 = threadIdx.x / CPR;
     const bool cok = col < sh.N;
-    RowPre pre[D];
+    using PreT = typename PreTypeTrait<EP>::type;
+    constexpr bool S3 = Stat3Trait<EP>::value;
+    constexpr int NS = S3 ? 3 : 2;
+    PreT pre[D];
 #pragma unroll
     for (int i = 0; i < D; ++i) {
       const int r = r0 + i * RS;
@@ -689,14 +704,16 @@ __device__ __forceinline__ void ms_epilogue(const GemmShape& sh, const EP& ep, v
       }
     }
     __syncthreads();
-    float s1[8], s2[8];
+    float s1[8], s2[8], s3[S3 ? 8 : 1];
 #pragma unroll
     for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+#pragma unroll
+    for (int j = 0; j < (S3 ? 8 : 1); ++j) s3[j] = 0.f;
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
       const int r = r0 + i * RS;
       const int row = row0 + r;
-      const RowPre cur = pre[i % D];
+      const PreT cur = pre[i % D];
       if (i + D < NIT) {
         const int rn = r + D * RS;
         if (cok && rn < BM && row0 + rn < sh.M) ep.pre8(row0 + rn, col, pre[i % D]);
@@ -704,26 +721,29 @@ __device__ __forceinline__ void ms_epilogue(const GemmShape& sh, const EP& ep, v
       if (cok && r < BM && row < sh.M) {
         float v[8];
         Chunk<bf16>::unpack(*reinterpret_cast<const uint4*>(stg + r * BN + ((c ^ (r & (CPR - 1))) << 3)), v);
-        if constexpr (NCF > 0) ep.row8r(row, col, v, cur, s1, s2, cf);
+        if constexpr (S3) ep.row8r3(row, col, v, cur, s1, s2, s3, cf);
+        else if constexpr (NCF > 0) ep.row8r(row, col, v, cur, s1, s2, cf);
         else ep.row8(row, col, v, cur, s1, s2);
       }
     }
     if constexpr (EP::kStats) {
       __syncthreads();
-      float* red = reinterpret_cast<float*>(smem);   // [NT][16]
+      float* red = reinterpret_cast<float*>(smem);   // [NT][8 * NS]
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        red[threadIdx.x * 16 + j] = s1[j];
-        red[threadIdx.x * 16 + 8 + j] = s2[j];
+        red[threadIdx.x * 8 * NS + j] = s1[j];
+        red[threadIdx.x * 8 * NS + 8 + j] = s2[j];
+        if constexpr (S3) red[threadIdx.x * 8 * NS + 16 + j] = s3[j];
       }
       __syncthreads();
       const int rep = ep.stat_rep > 1 ? (wid % ep.stat_rep) : 0;
-      for (int q = threadIdx.x; q < 2 * BN; q += NT) {
-        const int cl = q >> 1, stt = q & 1;
+      for (int q = threadIdx.x; q < NS * BN; q += NT) {
+        const int cl = q / NS, stt = q - cl * NS;
         const int cc = cl >> 3, j = cl & 7;
         float x = 0.f;
-        for (int k = cc; k < NT; k += CPR) x += red[k * 16 + stt * 8 + j];
-        if (col0 + cl < sh.N) atomicAdd((stt ? ep.stat2 : ep.stat1) + (size_t)rep * sh.N + col0 + cl, (double)x);
+        for (int k = cc; k < NT; k += CPR) x += red[k * 8 * NS + stt * 8 + j];
+        double* dst = stt == 0 ? ep.stat1 : stt == 1 ? ep.stat2 : stat3_of(ep);
+        if (col0 + cl < sh.N) atomicAdd(dst + (size_t)rep * sh.N + col0 + cl, (double)x);
       }
     }
     return;

@@ -59,7 +59,7 @@ def parse_header(path: str = HEADER_PATH) -> Dict[str, dict]:
 
 # entry points timed by ops.py under a kernel-family key (with algorithmic FLOPs)
 _FAMILY_TIMED = {"vlp_conv_fwd", "vlp_conv_fwd_act", "vlp_conv_dgrad", "vlp_conv_dgrad_relu",
-                 "vlp_conv_dgrad_bn_act", "vlp_conv_dgrad_relu_act", "vlp_conv_dgrad_relu_ds", "vlp_conv_wgrad", "vlp_conv_wgrad_ws", "vlp_stem_fwd", "vlp_stem_wgrad", "vlp_stem_wgrad_ws",
+                 "vlp_conv_dgrad_bn_act", "vlp_conv_dgrad_relu_act", "vlp_conv_dgrad_relu_ds", "vlp_conv_dgrad_relu2", "vlp_conv_wgrad", "vlp_conv_wgrad_ws", "vlp_stem_fwd", "vlp_stem_wgrad", "vlp_stem_wgrad_ws",
                  "vlp_stem1_fwd", "vlp_stem1_wgrad_ws", "vlp_stem1_pool_fwd", "vlp_stem1_bwd_fused",
                  "vlp_linear_fwd", "vlp_linear_fwd_rs", "vlp_linear_dgrad", "vlp_linear_wgrad", "vlp_linear_wgrad_ws",
                  "vlp_nest_attn_fwd", "vlp_nest_attn_bwd"}

@@ -169,6 +169,21 @@ def conv_dgrad_relu_ds(dy, dyd, wt, wtd, H, W, C, KH, KW, S, P, relu_out, y, mea
     return g
 
 
+def conv_dgrad_relu2(dy, wt, H, W, C, KH, KW, S, P, relu_mask, y, mean, invstd, yd, meand, invstdd,
+                     stat1, stat2, stat3, addend=None, stat_rep=1, out=None):
+    """g = (dgrad(dy) + addend) * relu bits, with the three BN backward sums of a
+    block whose output feeds its bn2 (y, mean, invstd) and its downsample BN (yd,
+    meand, invstdd): sum g, sum g*xhat, sum g*xhatd (vlp_conv_dgrad_relu2)."""
+    N, Ho, Wo, Co = dy.shape
+    g = out if out is not None else torch.empty((N, H, W, C), dtype=dy.dtype, device=dy.device)
+    tk = ktimer.begin(f"conv_dgrad[relu2]{_tile_auto(C)}", 2.0 * N * Ho * Wo * Co * C * KH * KW)
+    lib().vlp_conv_dgrad_relu2(dcode(dy), ptr(dy), ptr(wt), ptr(g), N, H, W, C, Co, KH, KW, S, P, ptr(addend),
+                               ptr(relu_mask), ptr(y), ptr(mean), ptr(invstd), ptr(yd), ptr(meand), ptr(invstdd),
+                               ptr(stat1), ptr(stat2), ptr(stat3), int(stat_rep), _s())
+    ktimer.end(tk)
+    return g
+
+
 def conv_wgrad(dy, x, KH, KW, S, P, dw_ws, in_scale=None, in_shift=None, dyT=None):
     N, H, W, C = x.shape
     Co = dy.shape[-1]

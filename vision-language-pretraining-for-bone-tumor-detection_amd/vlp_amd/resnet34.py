@@ -61,6 +61,9 @@ _USE_BWD_ACT = True
 # bf16 stride-2 block entries: the downsample's data gradient folded into conv1's
 # parity class (0, 0) (vlp_conv_dgrad_relu_ds) instead of its own launch + an addend
 _USE_DS_FOLD = True
+# bf16: the second block of layers 2-4 takes its predecessor's bn2 + downsample-BN
+# backward sums in its conv1 data-gradient epilogue (vlp_conv_dgrad_relu2)
+_USE_RELU2 = True
 # bf16 layer 1: bn1 + ReLU applied in conv2's input ring (vlp_conv_fwd_act), a1
 # written by that kernel; False keeps the separate bn_add_relu pass
 _USE_ACT_FUSED = True
@@ -598,6 +601,19 @@ class ResNet34Tower(ArenaModule):
                     dx = ops.conv_dgrad_relu(dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, rmask,
                                              blocks[bi - 1]["y2"], mup, isp, sgpf, sgxpf, addend=addend,
                                              stat_rep=STAT_REP)
+                dout_masked = True
+            elif (_USE_RELU2 and prev is not None and prev[1] and T == torch.bfloat16 and c1.S == 1
+                  and B.get("xmask") is not None and Cin >= 128 and Cin % 64 == 0):
+                # the previous block (a stage's first) has a downsample: its bn2 and downsample-BN
+                # sums come out of this epilogue too, so its backward needs no reduce pass
+                kp, kdp = prev[0] + ".bn2", prev[0] + ".downsample.1"
+                _, _, mup, isp = self._coef(ws, kp)
+                _, _, mudp, isdp = self._coef(ws, kdp)
+                sgpf, sgxpf = self._bstat(ws, kp, full=True)
+                sgxdpf = self._bstat_ds(ws, kp, full=True)
+                dx = ops.conv_dgrad_relu2(dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, 1, 1, B["xmask"],
+                                          blocks[bi - 1]["y2"], mup, isp, blocks[bi - 1]["yd"], mudp, isdp,
+                                          sgpf, sgxpf, sgxdpf, addend=addend, stat_rep=STAT_REP)
                 dout_masked = True
             else:
                 assert not fuse_in
