@@ -204,6 +204,47 @@ def test_conv_dgrad_act_matches_pass_then_dgrad(ops, N, H, epi):
     assert not ops.conv_dgrad_act_ok(g_in[:, :, :64].contiguous(), C, 3, 3, 1, 1)
 
 
+@pytest.mark.parametrize("N,H,C", [(2, 64, 128), (4, 32, 256), (8, 16, 512), (3, 13, 128)])
+def test_conv_dgrad_relu2_three_sums(ops, N, H, C):
+    """vlp_conv_dgrad_relu2 (the block after a downsample): g = (dgrad + addend)
+    masked by the previous block's output-ReLU bits, with three BN backward sums
+    (against y2 and yd) in the epilogue, against conv_dgrad(addend) + the separate
+    mask / bn_bwd_reduce pass: g bit-identical, sums equal up to summation order.
+    The 128x128 (C = 128) and 256x256 ping-pong (C >= 256) tiles, an odd size."""
+    torch.manual_seed(23)
+    bf = torch.bfloat16
+    dev = torch.device("cuda")
+    M = N * H * H
+    dy = torch.randn(N, H, H, C, device=dev).to(bf)
+    w = (torch.randn(C, C, 3, 3) * (9 * C) ** -0.5).to(bf).float()
+    wt = torch.empty(C, 3, 3, C, dtype=bf, device=dev)
+    ops.pack_conv(w.cuda(), None, wt)
+    addend = torch.randn(N, H, H, C, device=dev).to(bf)
+    act = torch.randn(N, H, H, C, device=dev).to(bf)
+    out_act = torch.empty_like(act)
+    bits = torch.empty(M * C // 8, dtype=torch.uint8, device=dev)
+    ops.bn_add_relu(act, torch.ones(C, device=dev), torch.zeros(C, device=dev), None, None, None, out_act,
+                    relu_mask=bits)
+    y2, yd = (torch.randn(N, H, H, C, device=dev) * 1.5 + 0.2).to(bf), torch.randn(N, H, H, C, device=dev).to(bf)
+    mu2, is2 = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5
+    mud, isd = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5
+    t1, t2, t3 = (torch.zeros(4 * C, dtype=torch.float64, device=dev) for _ in range(3))
+    g = ops.conv_dgrad_relu2(dy, wt, H, H, C, 3, 3, 1, 1, bits, y2, mu2, is2, yd, mud, isd, t1, t2, t3,
+                             addend=addend, stat_rep=4)
+    dx = ops.conv_dgrad(dy, wt, H, H, C, 3, 3, 1, 1, addend=addend)
+    r1, r2, r3 = (torch.zeros(4 * C, dtype=torch.float64, device=dev) for _ in range(3))
+    ops.bn_bwd_reduce(M, C, dx, None, 1, out_act, y2, mu2, is2, yd, mud, isd, r1, r2, r3, dx, stat_rep=4)
+    torch.cuda.synchronize()
+    g_ref = torch.where(out_act > 0, dx, torch.zeros_like(dx))
+    assert torch.equal(g, g_ref)
+    for t, r in ((t1, r1), (t2, r2), (t3, r3)):
+        a, b = t.view(4, C).sum(0), r.view(4, C).sum(0)
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6 * b.abs().max().item()), (a - b).abs().max()
+    with pytest.raises(RuntimeError):   # C = 64 takes no row-chunk kernel: refused
+        ops.conv_dgrad_relu2(dy[..., :64].contiguous(), wt, H, H, 64, 3, 3, 1, 1, bits, y2, mu2, is2, yd, mud, isd,
+                             t1, t2, t3)
+
+
 @pytest.mark.parametrize("N,Hi,C,Co", [(2, 64, 64, 128), (4, 32, 128, 256), (8, 16, 256, 512), (3, 14, 64, 128)])
 def test_conv_dgrad_relu_ds_fold(ops, N, Hi, C, Co):
     """vlp_conv_dgrad_relu_ds: conv1 (3x3/2) data gradient with the downsample's
