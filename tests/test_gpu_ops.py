@@ -237,9 +237,11 @@ def test_conv_dgrad_relu2_three_sums(ops, N, H, C):
     torch.cuda.synchronize()
     g_ref = torch.where(out_act > 0, dx, torch.zeros_like(dx))
     assert torch.equal(g, g_ref)
+    # the epilogue sums g in fp32 before its bf16 rounding, the pass sums the rounded
+    # bf16 g: per channel a random walk of M rounding errors (~2^-9 |g| each)
     for t, r in ((t1, r1), (t2, r2), (t3, r3)):
         a, b = t.view(4, C).sum(0), r.view(4, C).sum(0)
-        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6 * b.abs().max().item()), (a - b).abs().max()
+        assert torch.allclose(a, b, rtol=0, atol=4e-3 * b.abs().max().item()), (a - b).abs().max()
     with pytest.raises(RuntimeError):   # C = 64 takes no row-chunk kernel: refused
         ops.conv_dgrad_relu2(dy[..., :64].contiguous(), wt, H, H, 64, 3, 3, 1, 1, bits, y2, mu2, is2, yd, mud, isd,
                              t1, t2, t3)
