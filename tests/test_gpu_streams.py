@@ -197,11 +197,17 @@ def test_ds_fold_matches_separate_downsample_bf16():
     """Test E: the downsample's data gradient folded into conv1's stride-2 class (0, 0)
     GEMM (resnet34._USE_DS_FOLD) and the next block's three-sum ReLU epilogue
     (resnet34._USE_RELU2) vs the separate downsample launch + addend and the
-    bn_bwd_reduce pass.  Not bit-identical (the fold sums the two branches in fp32
-    before one bf16 rounding; the sums run in another order), so every image-tower
-    image-tower gradient stays close to the unfused step (gates below) and the loss equal."""
+    bn_bwd_reduce pass.  Not bit-identical: the fold sums the two branches in fp32
+    before one bf16 rounding and the epilogue sums g before its bf16 rounding (the
+    pass sums the rounded g), and BN backward amplifies such differences down the
+    tower.  Gate: against the fp32 CPU oracle, every image-tower tensor of the fused
+    step within 1.25x the unfused step's own error + 0.02, and the median no worse
+    than 1.1x + 0.005; fused vs unfused directly <= 0.1 rel-L2 (a missing or doubled
+    downsample term moves gradients by O(1)).  The op tests pin the kernels exactly."""
+    from oracle.clip import OracleVLP, compute_loss
     from src.models.pretrain.VisionLanguageModule import VisionLanguageModule
     from vlp_amd import resnet34 as r34
+    import statistics
     torch.manual_seed(4)
     m = VisionLanguageModule("resnet34", "tinybert", functools.partial(torch.optim.AdamW, lr=5e-5), False, False,
                              512, 312, 128, compute_dtype="bf16", text_dropout=0.0)
@@ -210,9 +216,9 @@ def test_ds_fold_matches_separate_downsample_bf16():
         for k, p in m.named_parameters():
             if k.endswith("bn2.weight"):
                 p.fill_(0.5)
-    b = synth_batch(4, 256, 16, 9, with_u8=True)
-    b = {"x-ray-u8": b["x-ray-u8"].cuda(), "label": b["label"], "caption": b["caption"],
-         "caption_tokenized": {k: v.cuda() for k, v in b["caption_tokenized"].items()}}
+    full = synth_batch(4, 256, 16, 9, with_u8=True)
+    b = {"x-ray-u8": full["x-ray-u8"].cuda(), "label": full["label"], "caption": full["caption"],
+         "caption_tokenized": {k: v.cuda() for k, v in full["caption_tokenized"].items()}}
     was = (r34._USE_DS_FOLD, r34._USE_RELU2)
     try:
         r34._USE_DS_FOLD = r34._USE_RELU2 = False
@@ -222,16 +228,20 @@ def test_ds_fold_matches_separate_downsample_bf16():
     finally:
         r34._USE_DS_FOLD, r34._USE_RELU2 = was
     assert abs(l1 - l0) <= 1e-6, (l0, l1)
-    img = [k for k in g0 if k.startswith("image_encoder.") and g0[k].norm() > 0]
-    errs = {k: _rel(g1[k], g0[k]) for k in img}
-    conv = sorted(((e, k) for k, e in errs.items() if g0[k].dim() == 4), reverse=True)
-    bn = sorted(((e, k) for k, e in errs.items() if g0[k].dim() == 1), reverse=True)
-    print("ds fold vs separate, worst rel-L2: conv", conv[:3], "BN", bn[:3])
-    # the rounding difference enters at the stride-2 blocks and is carried down the
-    # backward through every BN backward below (measured: layer-1 conv weights 1.3e-2,
-    # BN biases 2.4e-2, against 10-70 % bf16-vs-fp32 deviations of either path; a
-    # missing or doubled downsample term moves them by O(1)); the op tests pin the
-    # kernels exactly.  conv weights <= 3e-2, BN parameters <= 1e-1, median <= 5e-3
-    assert conv[0][0] <= 3e-2, conv[:3]
-    assert bn[0][0] <= 1e-1, bn[:3]
-    assert sorted(errs.values())[len(errs) // 2] <= 5e-3
+    o = OracleVLP(128, text_dropout=0.0)
+    o.load_state_dict({k: v.detach().float().cpu() for k, v in m.state_dict().items()})
+    o.train()
+    lg, _, _ = o({"x-ray": full["x-ray"], "caption_tokenized": full["caption_tokenized"]})
+    compute_loss(lg)[0].backward()
+    ref = {k: p.grad for k, p in o.named_parameters() if p.grad is not None}
+    img = [k for k in g0 if k.startswith("image_encoder.") and ref[k].norm() > 0]
+    e0 = {k: _rel(g0[k].cpu(), ref[k]) for k in img}
+    e1 = {k: _rel(g1[k].cpu(), ref[k]) for k in img}
+    d = {k: _rel(g1[k], g0[k]) for k in img}
+    worst = sorted(((e1[k] - (1.25 * e0[k] + 0.02), k, e1[k], e0[k]) for k in img), reverse=True)[:3]
+    print("ds fold vs fp32 oracle, worst (excess, name, fused, unfused):", worst,
+          "| median fused %.4f unfused %.4f | max fused-vs-unfused %.4f"
+          % (statistics.median(e1.values()), statistics.median(e0.values()), max(d.values())))
+    assert worst[0][0] <= 0, worst
+    assert statistics.median(e1.values()) <= 1.1 * statistics.median(e0.values()) + 0.005
+    assert max(d.values()) <= 0.1
