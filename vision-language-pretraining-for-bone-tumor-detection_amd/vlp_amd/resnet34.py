@@ -57,13 +57,13 @@ _USE_STEM_FUSED = True
 # layer-1 data gradients form their input dy = k*g + b*y + c in the rows kernel's
 # ring (vlp_conv_dgrad_bn_act / vlp_conv_dgrad_relu_act) instead of a separate
 # bn_bwd_apply pass (tests/test_gpu_streams.py holds on vs off)
-_USE_BWD_ACT = True
+_USE_BWD_ACT = os.environ.get("VLP_BWD_ACT", "1") != "0"
 # bf16 stride-2 block entries: the downsample's data gradient folded into conv1's
 # parity class (0, 0) (vlp_conv_dgrad_relu_ds) instead of its own launch + an addend
-_USE_DS_FOLD = True
+_USE_DS_FOLD = os.environ.get("VLP_DS_FOLD", "1") != "0"
 # bf16: the second block of layers 2-4 takes its predecessor's bn2 + downsample-BN
 # backward sums in its conv1 data-gradient epilogue (vlp_conv_dgrad_relu2)
-_USE_RELU2 = True
+_USE_RELU2 = os.environ.get("VLP_RELU2", "1") != "0"
 # bf16 layer 1: bn1 + ReLU applied in conv2's input ring (vlp_conv_fwd_act), a1
 # written by that kernel; False keeps the separate bn_add_relu pass
 _USE_ACT_FUSED = True
