@@ -297,6 +297,56 @@ def test_conv_dgrad_relu_ds_fold(ops, N, Hi, C, Co):
         ops.conv_dgrad_relu_ds(pair[0], pair[0], wt, wtd, Hi, Hi, C, 3, 3, 2, 1, act, ye, mu, ist, s1, s2)
 
 
+@pytest.mark.parametrize("N,H,C,epi", [(128, 32, 256, "bn"), (139, 31, 256, "relu"), (256, 16, 512, "bn"),
+                                        (256, 16, 512, "relu")])
+def test_conv_dgrad_staggered_rounds(ops, N, H, C, epi):
+    """Data gradients with a BN / ReLU epilogue that span >= 2 rounds of the chip run
+    staggered rounds (csrc/gemm.h, pp_desync): the first tiles of each XCD's run are
+    split into two K-halves that meet in an fp32 workspace, the second to arrive
+    adding the other's accumulators and running the epilogue. Bench-sized layer-3/4
+    shapes (the model tests' batches stay below 2 rounds), one with a partial last
+    tile and XCD runs of unequal length (139 x 31 x 31). Against torch fp32 on the
+    same bf16 operands; three launches bit-identical (the half sum is order-free and
+    the arrival counters return to zero)."""
+    torch.manual_seed(31)
+    bf = torch.bfloat16
+    dev = torch.device("cuda")
+    dy = torch.randn(N, H, H, C, device=dev).to(bf)
+    w = (torch.randn(C, C, 3, 3, device=dev) * (9 * C) ** -0.5).to(bf).float()
+    wt = torch.empty(C, 3, 3, C, dtype=bf, device=dev)
+    ops.pack_conv(w, None, wt)
+    y = torch.randn(N, H, H, C, device=dev).to(bf)
+    mu, ist = torch.randn(C, device=dev) * 0.1, torch.rand(C, device=dev) + 0.5
+    sc, sh = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.2
+    act = torch.relu(torch.randn(N, H, H, C, device=dev)).to(bf)
+    add = torch.randn(N, H, H, C, device=dev).to(bf)
+    ref = torch.nn.grad.conv2d_input((N, C, H, H), w, dy.permute(0, 3, 1, 2).float(), padding=1)
+    ref = ref.permute(0, 2, 3, 1)
+    if epi == "bn":
+        mask = (y.float() * sc + sh) > 0
+    else:
+        ref = ref + add.float()
+        mask = act > 0
+    gref = torch.where(mask, ref.to(bf).float(), torch.zeros_like(ref))
+    outs = []
+    for _ in range(3):
+        s1 = torch.zeros(C, dtype=torch.float64, device=dev)
+        s2 = torch.zeros_like(s1)
+        if epi == "bn":
+            g = ops.conv_dgrad(dy, wt, H, H, C, 3, 3, 1, 1, y_bn=y, bn=(sc, sh, mu, ist), stat1=s1, stat2=s2)
+        else:
+            g = ops.conv_dgrad_relu(dy, wt, H, H, C, 3, 3, 1, 1, act, y, mu, ist, s1, s2, addend=add)
+        outs.append((g.clone(), s1, s2))
+    torch.cuda.synchronize()
+    g0 = outs[0][0]
+    assert rel(g0.float(), gref) < tol(bf), rel(g0.float(), gref)
+    for o in outs[1:]:
+        assert torch.equal(o[0], g0)
+    xh = (y.float() - mu) * ist
+    assert rel(outs[0][1], gref.sum((0, 1, 2))) < tol(bf)
+    assert rel(outs[0][2], (gref * xh).sum((0, 1, 2))) < tol(bf)
+
+
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_dgrad_wgrad(ops, dt, case):

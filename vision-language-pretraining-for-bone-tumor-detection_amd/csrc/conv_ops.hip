@@ -901,6 +901,7 @@ __device__ __forceinline__ void ld8f(const float* p, float (&o)[8]) {
 // raw conv output + BN batch statistics (sum, sum of squares)
 template <typename T>
 struct EpiConvFwd {
+  static constexpr int kDesync = 2;   // pp_desync kind (gemm.h)
   static constexpr bool kStats = true;
   double* stat1; double* stat2; int stat_rep;
   T* y; int Co;
@@ -934,6 +935,7 @@ __device__ __forceinline__ void stg16_row(void* p, const uint4& v) {
 }
 template <typename T>
 struct EpiDgradBN {
+  static constexpr int kDesync = 1;   // pp_desync kind (gemm.h)
   static constexpr bool kStats = true;
   double* stat1; double* stat2; int stat_rep;
   T* g_out; int C;
@@ -1013,6 +1015,7 @@ struct EpiDgradBN {
 // data gradient plus a residual-branch gradient
 template <typename T>
 struct EpiDgradAdd {
+  static constexpr int kDesync = 1;   // pp_desync kind (gemm.h)
   static constexpr bool kStats = false;
   double* stat1 = nullptr; double* stat2 = nullptr;
   T* dx; const T* addend; int C;
@@ -1056,6 +1059,7 @@ struct EpiDgradAdd {
 // a separate instantiation, so the activation path's registers are not shared
 template <typename T, bool BITS = false>
 struct EpiDgradRelu {
+  static constexpr int kDesync = 1;   // pp_desync kind (gemm.h)
   static constexpr bool kStats = true;
   double* stat1; double* stat2; int stat_rep;
   T* g_out; const T* addend; int C;
@@ -1153,6 +1157,7 @@ struct EpiDgradRelu {
 // Row-chunk epilogue only (the host routes it to the LDS-DMA kernels).
 template <typename T>
 struct EpiDgradRelu2 {
+  static constexpr int kDesync = 1;   // pp_desync kind (gemm.h)
   static constexpr bool kStats = true;
   static constexpr bool kStats3 = true;
   double* stat1; double* stat2; int stat_rep; double* stat3;

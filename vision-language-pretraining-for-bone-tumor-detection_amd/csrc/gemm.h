@@ -26,7 +26,10 @@
 // remapped so that consecutive tile ids share an XCD (L2 reuse of the A panel).
 // Split-K over grid.y for reductions over pixels (weight gradients).
 #pragma once
+#include <mutex>
 #include <type_traits>
+#include <utility>
+#include <vector>
 #include "common.h"
 
 #ifndef VLP_BIG_SCHED   // gemm_big_kernel instruction interleaving (0: compiler order)
@@ -47,6 +50,11 @@ struct GemmShape {
   int xsplit;   // 1: split-K grid is 1-D and every split's tiles share one XCD
   int dbg;      // reserved (0)
   int nsplit;   // K-splits (bk / big kernels: 1-D grid of nsplit * tiles)
+  // gemm_pp_kernel staggered rounds (pp_desync): split tiles per XCD run (0: off),
+  // the per-part fp32 accumulator images and one arrival counter per split tile
+  int sk = 0;
+  float* skp = nullptr;
+  unsigned* skc = nullptr;
 };
 
 // ---------------- LDS image addressing (bytes) ----------------
@@ -185,6 +193,15 @@ template <class E, class = void> struct SplitTrait { static constexpr bool value
 template <class E> struct SplitTrait<E, std::void_t<decltype(E::kSplitOut)>> {
   static constexpr bool value = E::kSplitOut;
 };
+// VLP_PP_DESYNC: bit mask of the epilogue kinds (DesyncTrait) whose launches
+// run staggered rounds when they span >= 2 rounds of the chip
+#ifndef VLP_PP_DESYNC
+#define VLP_PP_DESYNC 1
+#endif
+// epilogues whose launches may run staggered rounds in gemm_pp_kernel
+// (E::kDesync: 1 data-gradient epilogues, 2 forward; enabled by VLP_PP_DESYNC)
+template <class E, class = void> struct DesyncTrait { static constexpr int value = 0; };
+template <class E> struct DesyncTrait<E, std::void_t<decltype(E::kDesync)>> { static constexpr int value = E::kDesync; };
 // K-step order: a loader with kKPerm maps the logical K offset of a 64-deep
 // step to the physical one (kperm); the buffer-protocol kernels apply the SAME
 // map to both operands, so the product is unchanged up to fp32 summation order
@@ -1409,19 +1426,53 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int nwg = sh.tiles_m * sh.tiles_n;
-  const int ntot = nwg * sh.nsplit;
+  const int ntot = sh.sk > 0 ? nwg + 8 * sh.sk : nwg * sh.nsplit;
   const int bid = blockIdx.x;
   int g = bid;
   if (ntot >= 16) {
     const int xcd = bid & 7, idx = bid >> 3, q = ntot >> 3, rr = ntot & 7;
     g = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
   }
-  const int split = g / nwg;
-  const int wid = g - split * nwg;
+  int split = g / nwg;
+  int wid = g - split * nwg;
+  int kb = split * sh.kchunk;
+  int ke = kb + sh.kchunk;
+  // staggered rounds (pp_desync): in each XCD's run of jobs the first 2s
+  // alternate "first K-half of split tile i" / "whole tile s+i", the middle is
+  // whole tiles and the last s are the second K-halves; the workgroups that
+  // started on a half stay half a tile out of phase with the others, so the
+  // memory-bound epilogues of the two cohorts alternate instead of every CU
+  // reaching its epilogue in the same round
+  int part = -1, sidx = 0;
+  if (sh.sk > 0) {
+    const int xcd = bid & 7, idx = bid >> 3, q = ntot >> 3, rr = ntot & 7;
+    const int L = q + (xcd < rr ? 1 : 0);
+    const int start = xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q;
+    const int s = sh.sk, base = start - xcd * s;
+    const int hk = ((sh.K / BK) >> 1) * BK;
+    kb = 0;
+    ke = sh.K;
+    if (idx < 2 * s) {
+      if (idx & 1) {
+        wid = base + s + (idx >> 1);
+      } else {
+        wid = base + (idx >> 1);
+        part = 0;
+        sidx = xcd * s + (idx >> 1);
+        ke = hk;
+      }
+    } else if (idx < L - s) {
+      wid = base + idx;
+    } else {
+      wid = base + (idx - (L - s));
+      part = 1;
+      sidx = xcd * s + (idx - (L - s));
+      kb = hk;
+    }
+    split = 0;
+  }
   const int tm = wid / sh.tiles_n, tn = wid - tm * sh.tiles_n;
   const int row0 = tm * BM, col0 = tn * BN;
-  const int kb = split * sh.kchunk;
-  int ke = kb + sh.kchunk;
   if (ke > sh.K) ke = sh.K;
   const int nk = (ke - kb + BK - 1) / BK;
   const int nh = 2 * (nk > 0 ? nk : 0);
@@ -1582,11 +1633,73 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   if (grp == 0) run(std::integral_constant<int, 0>{});
   else run(std::integral_constant<int, 1>{});
   __syncthreads();   // ring drained (incl. the null-resource tail fetches) before LDS is reused
+  if constexpr ((DesyncTrait<EP>::value & VLP_PP_DESYNC) != 0) {
+    if (part >= 0) {
+      // each K-half stores its accumulators (thread-linear, 16 B per lane), then
+      // counts its arrival; the second to arrive adds the other half and runs the
+      // epilogue (a + b == b + a in fp32: the result does not depend on which)
+      constexpr int NR = MB * NB;
+      v4f* mine = reinterpret_cast<v4f*>(sh.skp) + (size_t)(sidx * 2 + part) * NR * NT + threadIdx.x;
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) mine[(a * NB + b) * NT] = acc[a][b];
+      __threadfence();
+      __syncthreads();
+      unsigned* flag = reinterpret_cast<unsigned*>(smem);
+      if (threadIdx.x == 0) flag[0] = atomicAdd(sh.skc + sidx, 1u);
+      __syncthreads();
+      const unsigned prev = flag[0];
+      __syncthreads();
+      if (prev == 0) return;
+      __threadfence();
+      const v4f* other = reinterpret_cast<const v4f*>(sh.skp) + (size_t)(sidx * 2 + (1 - part)) * NR * NT + threadIdx.x;
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[a][b] += other[(a * NB + b) * NT];
+      if (threadIdx.x == 0) atomicExch(sh.skc + sidx, 0u);
+    }
+  }
   if constexpr (SplitTrait<EP>::value) {
     ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep.at_split(split), acc, row0, col0, wid, wm, wn, smem);
   } else {
     ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep, acc, row0, col0, wid, wm, wn, smem);
   }
+}
+
+// ---------------- staggered rounds for gemm_pp_kernel ----------------
+// per (device, stream) workspace: 2 fp32 accumulator images per split tile and
+// one arrival counter each (counters return to 0 at the end of every launch)
+struct PpDesyncWs { float* part; unsigned* cnt; size_t part_bytes; int nslot; };
+inline PpDesyncWs pp_desync_ws(hipStream_t st, size_t part_bytes, int nslot) {
+  static std::mutex mu;
+  static std::vector<std::pair<std::pair<int, hipStream_t>, PpDesyncWs>> tab;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(mu);
+  for (auto& e : tab)
+    if (e.first.first == dev && e.first.second == st) {
+      if (e.second.part_bytes >= part_bytes && e.second.nslot >= nslot) return e.second;
+      (void)hipStreamSynchronize(st);
+      (void)hipFree(e.second.part);
+      (void)hipFree(e.second.cnt);
+      e.second = PpDesyncWs{nullptr, nullptr, 0, 0};
+      if (hipMalloc(&e.second.part, part_bytes * 2 * nslot) != hipSuccess ||
+          hipMalloc(&e.second.cnt, sizeof(unsigned) * nslot) != hipSuccess ||
+          hipMemset(e.second.cnt, 0, sizeof(unsigned) * nslot) != hipSuccess)
+        return PpDesyncWs{nullptr, nullptr, 0, 0};
+      e.second.part_bytes = part_bytes;
+      e.second.nslot = nslot;
+      return e.second;
+    }
+  PpDesyncWs w{nullptr, nullptr, part_bytes, nslot};
+  if (hipMalloc(&w.part, part_bytes * 2 * nslot) != hipSuccess ||
+      hipMalloc(&w.cnt, sizeof(unsigned) * nslot) != hipSuccess ||
+      hipMemset(w.cnt, 0, sizeof(unsigned) * nslot) != hipSuccess)
+    return PpDesyncWs{nullptr, nullptr, 0, 0};
+  tab.push_back({{dev, st}, w});
+  return w;
 }
 
 
@@ -1832,6 +1945,21 @@ inline int launch_gemm_pp(int M, int N, int K, int ksplit, const LA& la, const L
   sh.nsplit = ksplit;
   last_ksplit() = ksplit;
   dim3 grid(sh.tiles_m * sh.tiles_n * ksplit, 1, 1);
+  if constexpr ((DesyncTrait<EP>::value & VLP_PP_DESYNC) != 0 && !SplitTrait<EP>::value) {
+    // >= 2 rounds of one workgroup per CU and >= 2 K-steps per half: half of
+    // each XCD's CUs start on a K-half (pp_desync above)
+    const int cus = device_cus();
+    const int s = cus / 16;
+    if (ksplit == 1 && s > 0 && cus % 8 == 0 && sh.tiles_m * sh.tiles_n >= 2 * cus && K >= 4 * BK) {
+          const PpDesyncWs w = pp_desync_ws(stream, (size_t)BM * BN * 4, 8 * s);
+      if (w.part) {
+        sh.sk = s;
+        sh.skp = w.part;
+        sh.skc = w.cnt;
+        grid = dim3(sh.tiles_m * sh.tiles_n + 8 * s, 1, 1);
+      }
+    }
+  }
   if constexpr (lds > 65536) {
     static bool attr_set = false;
     if (!attr_set) {
