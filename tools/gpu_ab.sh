@@ -2,7 +2,8 @@
 # Every step runs under its own time limit; the first failure ends the script.
 #
 #   TAG=r4a                        prefix of every log under gpurun_out/
-#   TESTS="tests/test_gpu_ops.py -k dgrad"   optional pytest selection (run once, default library)
+#   TESTS="tests/test_gpu_ops.py"  optional pytest selection (run once, default library)
+#   TESTK="dgrad or stem"          optional -k expression for TESTS
 #   VARIANTS="default row_nt"      libraries: default = the in-tree libvlp_hip.so,
 #                                  NAME = build_exp/NAME/libvlp_hip.so (tools/build_variant.sh NAME "-D...")
 #   CB_ARGS="--ops dgrad_bn,dgrad_relu"      optional tools/conv_bench.py run per variant
@@ -18,7 +19,7 @@ VARIANTS=${VARIANTS:-default}
 lib_of() { if [ "$1" = default ]; then echo $PKG/vlp_amd/libvlp_hip.so; else echo $PWD/build_exp/$1/libvlp_hip.so; fi; }
 
 if [ -n "$TESTS" ]; then
-  timeout -k 10 ${TEST_TIMEOUT:-600} python -u -m pytest $TESTS -m gpu -x -v -s --timeout 300 --timeout-method thread \
+  timeout -k 10 ${TEST_TIMEOUT:-600} python -u -m pytest $TESTS ${TESTK:+-k "$TESTK"} -m gpu -x -v -s --timeout 300 --timeout-method thread \
     -p no:cacheprovider > gpurun_out/${TAG}_tests.log 2>&1 || { echo TESTS FAILED; tail -40 gpurun_out/${TAG}_tests.log; exit 1; }
   tail -1 gpurun_out/${TAG}_tests.log
 fi

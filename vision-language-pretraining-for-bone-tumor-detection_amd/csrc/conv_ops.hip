@@ -461,7 +461,11 @@ struct WtS2B {
                  0u};
   }
   __device__ unsigned boff(BState& s, const BStep& st) const {
-    const unsigned b = st.ds ? s.od : s.o;
+    // bitwise select on the uniform flag: a ?: over the two members was lowered
+    // to a dynamically indexed scratch copy of the state (4 scratch loads per
+    // K-step in the main loop, each one counted in the LDS-DMA vmcnt waits)
+    const unsigned m = 0u - st.ds;
+    const unsigned b = (s.o & ~m) | (s.od & m);
     return b == kOOB ? kOOB : b + st.delta;
   }
 };

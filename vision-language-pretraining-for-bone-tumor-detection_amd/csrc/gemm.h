@@ -195,9 +195,27 @@ template <class E> struct SplitTrait<E, std::void_t<decltype(E::kSplitOut)>> {
 };
 // VLP_PP_DESYNC: bit mask of the epilogue kinds (DesyncTrait) whose launches
 // run staggered rounds when they span >= 2 rounds of the chip
+// Measured off (r4, conv_bench bs = 256, us per launch, d0 = off): layer 3
+// BN / ReLU epilogue 350 / 366 -> 402 / 425, layer 4 261 / 262 -> 315 / 327;
+// the schedule alone (hand-over skipped, wrong sums) already 363 / 383 and
+// 301 / 303, and a blockIdx -> XCD job order instead of the ticket was no
+// better (gpurun_out r4h-r4k).
 #ifndef VLP_PP_DESYNC
-#define VLP_PP_DESYNC 1
+#define VLP_PP_DESYNC 0
 #endif
+#ifndef VLP_PP_DESYNC_DIV   // split tiles per XCD run = CUs / VLP_PP_DESYNC_DIV
+#define VLP_PP_DESYNC_DIV 16
+#endif
+// 16-B global store / load with the sc1 bit: performed at the agent's coherence
+// point (visible to another XCD's L2 without a fence); the caller waits vmcnt
+__device__ __forceinline__ void st_sc1_x4(void* p, v4f v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ v4f ld_sc1_x4(const void* p) {
+  v4f r;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
 // epilogues whose launches may run staggered rounds in gemm_pp_kernel
 // (E::kDesync: 1 data-gradient epilogues, 2 forward; enabled by VLP_PP_DESYNC)
 template <class E, class = void> struct DesyncTrait { static constexpr int value = 0; };
@@ -1426,7 +1444,7 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int nwg = sh.tiles_m * sh.tiles_n;
-  const int ntot = sh.sk > 0 ? nwg + 8 * sh.sk : nwg * sh.nsplit;
+  const int ntot = sh.sk > 0 ? nwg + sh.sk : nwg * sh.nsplit;
   const int bid = blockIdx.x;
   int g = bid;
   if (ntot >= 16) {
@@ -1437,36 +1455,45 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   int wid = g - split * nwg;
   int kb = split * sh.kchunk;
   int ke = kb + sh.kchunk;
-  // staggered rounds (pp_desync): in each XCD's run of jobs the first 2s
-  // alternate "first K-half of split tile i" / "whole tile s+i", the middle is
-  // whole tiles and the last s are the second K-halves; the workgroups that
-  // started on a half stay half a tile out of phase with the others, so the
-  // memory-bound epilogues of the two cohorts alternate instead of every CU
-  // reaching its epilogue in the same round
+  // staggered rounds (pp_desync): the first 2S jobs alternate "first K-half of
+  // split tile i" / "whole tile S+i", the middle is whole tiles and the last S
+  // are the second K-halves; the workgroups that started on a half stay half a
+  // tile out of phase with the others, so the memory-bound epilogues of the two
+  // cohorts alternate instead of every CU reaching its epilogue in one round
   int part = -1, sidx = 0;
   if (sh.sk > 0) {
-    const int xcd = bid & 7, idx = bid >> 3, q = ntot >> 3, rr = ntot & 7;
-    const int L = q + (xcd < rr ? 1 : 0);
-    const int start = xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q;
-    const int s = sh.sk, base = start - xcd * s;
+    // jobs are handed out by an arrival ticket, so the order above is the order
+    // in which workgroups actually start (a fixed blockIdx -> XCD placement
+    // assumption measured 13-16 % slower even without the hand-over); the
+    // workgroup drawing the last ticket resets the counter for the next launch
+    unsigned* tk = reinterpret_cast<unsigned*>(smem);
+    if (threadIdx.x == 0) {
+      const unsigned t = __hip_atomic_fetch_add(sh.skc + sh.sk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == (unsigned)ntot - 1u) __hip_atomic_store(sh.skc + sh.sk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      tk[0] = t;
+    }
+    __syncthreads();
+    const int t = __builtin_amdgcn_readfirstlane((int)tk[0]);
+    __syncthreads();
+    const int S = sh.sk;
     const int hk = ((sh.K / BK) >> 1) * BK;
     kb = 0;
     ke = sh.K;
-    if (idx < 2 * s) {
-      if (idx & 1) {
-        wid = base + s + (idx >> 1);
+    if (t < 2 * S) {
+      if (t & 1) {
+        wid = S + (t >> 1);
       } else {
-        wid = base + (idx >> 1);
+        wid = t >> 1;
         part = 0;
-        sidx = xcd * s + (idx >> 1);
+        sidx = t >> 1;
         ke = hk;
       }
-    } else if (idx < L - s) {
-      wid = base + idx;
+    } else if (t < ntot - S) {
+      wid = t;
     } else {
-      wid = base + (idx - (L - s));
+      wid = t - (ntot - S);
       part = 1;
-      sidx = xcd * s + (idx - (L - s));
+      sidx = wid;
       kb = hk;
     }
     split = 0;
@@ -1635,30 +1662,41 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   __syncthreads();   // ring drained (incl. the null-resource tail fetches) before LDS is reused
   if constexpr ((DesyncTrait<EP>::value & VLP_PP_DESYNC) != 0) {
     if (part >= 0) {
-      // each K-half stores its accumulators (thread-linear, 16 B per lane), then
-      // counts its arrival; the second to arrive adds the other half and runs the
-      // epilogue (a + b == b + a in fp32: the result does not depend on which)
+      // each K-half stores its accumulators, then counts its arrival; the second
+      // to arrive adds the other half and runs the epilogue (a + b == b + a in
+      // fp32: the result does not depend on which). The halves may sit on
+      // different XCDs (separate L2s): the accumulators move by 16-B stores and
+      // loads with the sc1 (agent-coherent) bit and the counter as a relaxed
+      // agent-scope atomic -- no L2 write-back or invalidate, which a fence
+      // would issue (that version ran the launch 25-40 % slower) -- the stores
+      // retired (vmcnt 0) before the count
       constexpr int NR = MB * NB;
       v4f* mine = reinterpret_cast<v4f*>(sh.skp) + (size_t)(sidx * 2 + part) * NR * NT + threadIdx.x;
 #pragma unroll
       for (int a = 0; a < MB; ++a)
 #pragma unroll
-        for (int b = 0; b < NB; ++b) mine[(a * NB + b) * NT] = acc[a][b];
-      __threadfence();
+        for (int b = 0; b < NB; ++b) st_sc1_x4(mine + (a * NB + b) * NT, acc[a][b]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       unsigned* flag = reinterpret_cast<unsigned*>(smem);
-      if (threadIdx.x == 0) flag[0] = atomicAdd(sh.skc + sidx, 1u);
+      if (threadIdx.x == 0)
+        flag[0] = __hip_atomic_fetch_add(sh.skc + sidx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
       const unsigned prev = flag[0];
       __syncthreads();
       if (prev == 0) return;
-      __threadfence();
       const v4f* other = reinterpret_cast<const v4f*>(sh.skp) + (size_t)(sidx * 2 + (1 - part)) * NR * NT + threadIdx.x;
+      v4f o[MB][NB];
 #pragma unroll
       for (int a = 0; a < MB; ++a)
 #pragma unroll
-        for (int b = 0; b < NB; ++b) acc[a][b] += other[(a * NB + b) * NT];
-      if (threadIdx.x == 0) atomicExch(sh.skc + sidx, 0u);
+        for (int b = 0; b < NB; ++b) o[a][b] = ld_sc1_x4(other + (a * NB + b) * NT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[a][b] += o[a][b];
+      if (threadIdx.x == 0) __hip_atomic_store(sh.skc + sidx, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   if constexpr (SplitTrait<EP>::value) {
@@ -1669,8 +1707,8 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
 }
 
 // ---------------- staggered rounds for gemm_pp_kernel ----------------
-// per (device, stream) workspace: 2 fp32 accumulator images per split tile and
-// one arrival counter each (counters return to 0 at the end of every launch)
+// per (device, stream) workspace: 2 fp32 accumulator images per split tile, one
+// arrival counter each and the job ticket (all return to 0 by the end of a launch)
 struct PpDesyncWs { float* part; unsigned* cnt; size_t part_bytes; int nslot; };
 inline PpDesyncWs pp_desync_ws(hipStream_t st, size_t part_bytes, int nslot) {
   static std::mutex mu;
@@ -1949,11 +1987,11 @@ inline int launch_gemm_pp(int M, int N, int K, int ksplit, const LA& la, const L
     // >= 2 rounds of one workgroup per CU and >= 2 K-steps per half: half of
     // each XCD's CUs start on a K-half (pp_desync above)
     const int cus = device_cus();
-    const int s = cus / 16;
+    const int s = cus / VLP_PP_DESYNC_DIV;
     if (ksplit == 1 && s > 0 && cus % 8 == 0 && sh.tiles_m * sh.tiles_n >= 2 * cus && K >= 4 * BK) {
-          const PpDesyncWs w = pp_desync_ws(stream, (size_t)BM * BN * 4, 8 * s);
+          const PpDesyncWs w = pp_desync_ws(stream, (size_t)BM * BN * 4, 8 * s + 1);   // + the ticket
       if (w.part) {
-        sh.sk = s;
+        sh.sk = 8 * s;
         sh.skp = w.part;
         sh.skc = w.cnt;
         grid = dim3(sh.tiles_m * sh.tiles_n + 8 * s, 1, 1);
