@@ -300,14 +300,13 @@ def test_conv_dgrad_relu_ds_fold(ops, N, Hi, C, Co):
 @pytest.mark.parametrize("N,H,C,epi", [(128, 32, 256, "bn"), (139, 31, 256, "relu"), (256, 16, 512, "bn"),
                                         (256, 16, 512, "relu")])
 def test_conv_dgrad_staggered_rounds(ops, N, H, C, epi):
-    """Data gradients with a BN / ReLU epilogue that span >= 2 rounds of the chip run
-    staggered rounds (csrc/gemm.h, pp_desync): the first tiles of each XCD's run are
-    split into two K-halves that meet in an fp32 workspace, the second to arrive
-    adding the other's accumulators and running the epilogue. Bench-sized layer-3/4
-    shapes (the model tests' batches stay below 2 rounds), one with a partial last
-    tile and XCD runs of unequal length (139 x 31 x 31). Against torch fp32 on the
-    same bf16 operands; three launches bit-identical (the half sum is order-free and
-    the arrival counters return to zero)."""
+    """Data gradients with a BN / ReLU epilogue at bench-sized layer-3/4 shapes
+    (>= 2 rounds of the chip; the model tests' batches stay below that), one with a
+    partial last tile (139 x 31 x 31). With VLP_PP_DESYNC (csrc/gemm.h, off by
+    default) these launches run staggered rounds: K-halves of split tiles meet in an
+    fp32 workspace, the second to arrive adding the other's accumulators. Against
+    torch fp32 on the same bf16 operands; three launches bit-identical (the half sum
+    is order-free and the arrival counters and job ticket return to zero)."""
     torch.manual_seed(31)
     bf = torch.bfloat16
     dev = torch.device("cuda")
