@@ -199,7 +199,7 @@ template <class E> struct SplitTrait<E, std::void_t<decltype(E::kSplitOut)>> {
 // BN / ReLU epilogue 350 / 366 -> 402 / 425, layer 4 261 / 262 -> 315 / 327;
 // the schedule alone (hand-over skipped, wrong sums) already 363 / 383 and
 // 301 / 303, and a blockIdx -> XCD job order instead of the ticket was no
-// better (gpurun_out r4h-r4k).
+// better (profiles/r4h..r4k_staggered_rounds_ab.json).
 #ifndef VLP_PP_DESYNC
 #define VLP_PP_DESYNC 0
 #endif
