@@ -150,7 +150,7 @@ struct ConvFwdA {
         if (kh < g.KH && kw < g.KW && (unsigned)(f.hi0 + kh) < (unsigned)g.H && (unsigned)(f.wi0 + kw) < (unsigned)g.W)
           mask |= 1u << (kh * g.KW + kw);
     const long long e = (long long)(f.base - x) + ((long long)f.hi0 * g.W + f.wi0) * g.C + koff;
-    return BState{(unsigned)(e * (long long)sizeof(T)), f.ok ? mask : 0u};
+    return BState{opaque_base((unsigned)(e * (long long)sizeof(T))), f.ok ? mask : 0u};
   }
   __device__ BStep bstep(int k0) const {
     const int tap = fdiv(k0, g.fd_c), ci0 = k0 - tap * g.C;
@@ -254,7 +254,7 @@ struct ConvDgradA {
         if (kh < g.KH && kw < g.KW && (unsigned)(f.hp - kh) < (unsigned)g.Ho && (unsigned)(f.wp - kw) < (unsigned)g.Wo)
           mask |= 1u << (kh * g.KW + kw);
     const long long e = (long long)(f.base - dy) + ((long long)f.hp * g.Wo + f.wp) * g.Co + koff;
-    return BState{(unsigned)(e * (long long)sizeof(T)), f.ok ? mask : 0u};
+    return BState{opaque_base((unsigned)(e * (long long)sizeof(T))), f.ok ? mask : 0u};
   }
   __device__ BStep bstep(int k0) const {
     const int tap = fdiv(k0, g.fd_co), co0 = k0 - tap * g.Co;
@@ -358,7 +358,7 @@ struct ConvDgradS2A {
         if (a < c.nth && b < c.ntw && (unsigned)(f.hb - a) < (unsigned)g.Ho && (unsigned)(f.wb - b) < (unsigned)g.Wo)
           mask |= 1u << (a * c.ntw + b);
     const long long e = (long long)(f.base - dy) + ((long long)f.hb * g.Wo + f.wb) * g.Co + koff;
-    return BState{(unsigned)(e * (long long)sizeof(T)), f.ok ? mask : 0u};
+    return BState{opaque_base((unsigned)(e * (long long)sizeof(T))), f.ok ? mask : 0u};
   }
   __device__ BStep bstep(int k0) const {
     if (k0 >= Kc1)   // downsample segment: dyd at the class pixel itself (tap 0 of class (0, 0))

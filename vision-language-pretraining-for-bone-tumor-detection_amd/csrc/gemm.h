@@ -216,6 +216,19 @@ __device__ __forceinline__ v4f ld_sc1_x4(const void* p) {
   asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(r) : "v"(p) : "memory");
   return r;
 }
+// A loader's per-chunk byte offset, computed once per tile, made opaque to the
+// compiler: otherwise it re-associates offset + per-K-step delta back into the
+// pixel coordinates and recomputes (v_mul_lo_u32 + v_mad_u64_u32 per chunk and
+// K-step) instead of keeping one VGPR per chunk (VLP_OPAQUE_BASE = 0: as before)
+#ifndef VLP_OPAQUE_BASE
+#define VLP_OPAQUE_BASE 1
+#endif
+__device__ __forceinline__ unsigned opaque_base(unsigned v) {
+#if VLP_OPAQUE_BASE
+  asm volatile("" : "+v"(v));
+#endif
+  return v;
+}
 // epilogues whose launches may run staggered rounds in gemm_pp_kernel
 // (E::kDesync: 1 data-gradient epilogues, 2 forward; enabled by VLP_PP_DESYNC)
 template <class E, class = void> struct DesyncTrait { static constexpr int value = 0; };
