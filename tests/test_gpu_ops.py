@@ -844,3 +844,47 @@ def test_stem1_single_channel_fwd_wgrad(ops, dt, N, H, W):
 def test_stem1_geom_rejects_unaligned(ops):
     assert ops.stem1_geom(100, 100) is None        # Wo = 50: the 3-channel path takes it
     assert ops.stem1_geom(512, 512) == (256, 256, 518, 520)
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("N,H,C", [(256, 16, 512), (3, 7, 512), (2, 5, 64), (2, 4, 100)])
+def test_avgpool_fwd_vs_torch(ops, dt, N, H, C):
+    """vlp_avgpool_fwd (timm's global average pool before the head): the 16-B-row
+    kernel (C % 8 == 0, one image per block, fixed-order partial sums) and the
+    scalar fallback (C = 100), against torch fp32 on the same operands."""
+    torch.manual_seed(41)
+    x = torch.randn(N, H, H, C, device="cuda").to(dt)
+    feat = torch.empty(N, C, dtype=dt, device="cuda")
+    ops.avgpool_fwd(x, feat)
+    torch.cuda.synchronize()
+    ref = x.float().mean((1, 2))
+    assert rel(feat.float(), ref.to(dt).float()) < (1e-6 if dt == torch.float32 else 8e-3)
+    feat2 = torch.empty_like(feat)
+    ops.avgpool_fwd(x, feat2)
+    torch.cuda.synchronize()
+    assert torch.equal(feat, feat2)
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("N,H,W", [(2, 32, 32), (3, 48, 64), (2, 224, 224), (1, 512, 512)])
+def test_stem1_prep_u8_exact(ops, dt, N, H, W):
+    """vlp_stem1_prep_u8 element by element: Xs[s][n][hp][j] = (x[n][hp-3][j+2s-3] - mean)
+    * (1/std) rounded to the dtype, zero outside the image, for all four shifted copies
+    (interior chunks take two aligned 8-byte loads and a funnel shift, edge chunks the
+    per-byte path)."""
+    g = torch.Generator().manual_seed(7 * H + N)
+    mean, std = 127.5, 73.9
+    x8 = torch.randint(0, 256, (N, 1, H, W), generator=g, dtype=torch.uint8)
+    Ho, Wo, Hp, Wp1 = ops.stem1_geom(H, W)
+    xs = torch.full((4, N, Hp, Wp1), float("nan"), device="cuda").to(dt)
+    ops.stem1_prep_u8(x8.cuda(), xs, mean, std)
+    torch.cuda.synchronize()
+    inv = torch.tensor(1.0, dtype=torch.float32) / torch.tensor(std, dtype=torch.float32)   # the host's 1.f / std
+    xn = (x8[:, 0].float() - mean) * inv
+    ref = torch.zeros(4, N, Hp, Wp1)
+    for s in range(4):
+        j0 = 3 - 2 * s                                  # column j reads image column j + 2s - 3
+        lo, hi = max(0, j0), min(Wp1, W + j0)
+        hr = min(Hp - 3, H)
+        ref[s, :, 3:3 + hr, lo:hi] = xn[:, :hr, lo - j0:hi - j0]
+    assert torch.equal(xs.cpu(), ref.to(dt))
