@@ -870,8 +870,7 @@ def test_avgpool_fwd_vs_torch(ops, dt, N, H, C):
 def test_stem1_prep_u8_exact(ops, dt, N, H, W):
     """vlp_stem1_prep_u8 element by element: Xs[s][n][hp][j] = (x[n][hp-3][j+2s-3] - mean)
     * (1/std) rounded to the dtype, zero outside the image, for all four shifted copies
-    (interior chunks take two aligned 8-byte loads and a funnel shift, edge chunks the
-    per-byte path)."""
+    (including the 512 x 512 bench image)."""
     g = torch.Generator().manual_seed(7 * H + N)
     mean, std = 127.5, 73.9
     x8 = torch.randint(0, 256, (N, 1, H, W), generator=g, dtype=torch.uint8)

@@ -1942,23 +1942,10 @@ __global__ void stem1_prep_u8_kernel(const uint8_t* __restrict__ x, T* __restric
     const bool hin = h >= 0 && h < H;
     const uint8_t* xr = x + ((size_t)n * H + (hin ? h : 0)) * W;
     float v[8];
-    const int w0 = c * 8 + 2 * (int)sh - 3;
-    const int a = w0 & ~7;
-    if (hin && w0 >= 0 && a + 16 <= W && (W & 7) == 0) {
-      // interior: two aligned 8-byte loads cover the 8 bytes at w0 (one funnel
-      // shift) instead of eight byte loads with a bounds check each
-      const uint64_t lo = *reinterpret_cast<const uint64_t*>(xr + a);
-      const uint64_t hi = *reinterpret_cast<const uint64_t*>(xr + a + 8);
-      const int k = 8 * (w0 - a);
-      const uint64_t b = k ? (lo >> k) | (hi << (64 - k)) : lo;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = ((float)(unsigned)((b >> (8 * j)) & 0xffu) - mean) * inv_std;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int w = w0 + j;
-        v[j] = (hin && w >= 0 && w < W) ? ((float)xr[w] - mean) * inv_std : 0.f;
-      }
+    for (int j = 0; j < 8; ++j) {
+      const int w = c * 8 + j + 2 * (int)sh - 3;
+      v[j] = (hin && w >= 0 && w < W) ? ((float)xr[w] - mean) * inv_std : 0.f;
     }
     T* dst = xs + (size_t)row * g.Wp1 + c * 8;
     if constexpr (sizeof(T) == 2) {
