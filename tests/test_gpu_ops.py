@@ -638,7 +638,9 @@ def test_colsum(ops, M, N, ld, off):
 
 @pytest.mark.parametrize("dt", DT)
 def test_pack_conv_batch(ops, dt):
-    """One-launch packing of many convs == per-conv vlp_pack_conv (bit-exact)."""
+    """One-launch packing of many convs == per-conv vlp_pack_conv (bit-exact): the
+    64 x 64 LDS-tile path (bf16, aligned, Co and C multiples of 64) and the
+    element-per-thread path (fp32, an unaligned view, C = 96) in one call."""
     torch.manual_seed(10)
     shapes = [(64, 64, 3, 3), (128, 64, 1, 1), (256, 128, 3, 3), (512, 512, 3, 3), (128, 64, 3, 3)]
     entries, refs = [], []
@@ -651,6 +653,19 @@ def test_pack_conv_batch(ops, dt):
         entries.append((w, wp, wt))
         refs.append((rp, rt))
     entries[1] = (entries[1][0], entries[1][1], None)   # wt optional
+    # not 16-B aligned (a view at an odd float offset) and C % 64 != 0: the
+    # element-per-thread path beside the 64 x 64 LDS-tile path in the same launch
+    flat = torch.randn(1 + 128 * 64 * 9, device="cuda")
+    wu = flat[1:].view(128, 64, 3, 3)
+    w96 = torch.randn(64, 96, 3, 3, device="cuda")
+    for w in (wu, w96):
+        Co, C, KH, KW = w.shape
+        wp = torch.empty(Co, KH, KW, C, dtype=dt, device="cuda")
+        wt = torch.empty(C, KH, KW, Co, dtype=dt, device="cuda")
+        rp, rt = torch.empty_like(wp), torch.empty_like(wt)
+        ops.pack_conv(w, rp, rt)
+        entries.append((w, wp, wt))
+        refs.append((rp, rt))
     ops.pack_conv_batch_run(ops.pack_conv_batch(entries[0][1], entries))
     torch.cuda.synchronize()
     for i, ((w, wp, wt), (rp, rt)) in enumerate(zip(entries, refs)):

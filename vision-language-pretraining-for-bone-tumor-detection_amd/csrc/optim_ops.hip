@@ -54,6 +54,7 @@ struct PackDesc {
   void* wp;
   void* wt;
   int Co, C, T;
+  int tiled;   // bf16, Co % 64 == C % 64 == 0, T <= 9, w 16-B aligned: 64 x 64 LDS tiles
 };
 struct PackBatch {
   PackDesc d[kPackMax];
@@ -75,6 +76,62 @@ __global__ void __launch_bounds__(256) pack_conv_batch_kernel(PackBatch b) {
       const int j = i - n, c = j / d.Co, co = j - c * d.Co;
       const float* src = d.w + ((size_t)co * d.C + c) * d.T;
       for (int t = 0; t < d.T; ++t) wt[((size_t)c * d.T + t) * d.Co + co] = from_f<T>(src[t]);
+    }
+  }
+}
+
+// The same packing by 64 (co) x 64 (c) tiles through LDS (bf16 only): each of
+// the tile's 64 weight rows w[co][c0 .. c0+63][0 .. T) is 64*T contiguous fp32,
+// read as float4 and rounded to bf16 into LDS once; both layouts are then
+// written as 16-B rows (wp: 8 consecutive c of one (co, tap); wt: 8 consecutive
+// co of one (c, tap)).  The element-per-thread kernel above read every weight
+// twice with 36-B strided lanes (157 us per step for the 34 convs).
+constexpr int kPackRow = 64 * 9 + 8;   // LDS row pitch (bf16), padded
+__device__ __forceinline__ uint16_t bf16_bits(float x) { return __builtin_bit_cast(uint16_t, (bf16)x); }
+__global__ void __launch_bounds__(256) pack_conv_tile_kernel(PackBatch b) {
+  const PackDesc& d = b.d[blockIdx.y];
+  if (!d.tiled) return;
+  const int tco = d.Co / 64, tc = d.C / 64;
+  if ((int)blockIdx.x >= tco * tc) return;
+  extern __shared__ __attribute__((aligned(16))) uint16_t pk[];   // [64 co][kPackRow]
+  const int co0 = (blockIdx.x / tc) * 64, c0 = (blockIdx.x % tc) * 64;
+  const int T = d.T, RL = 64 * T;   // elements per tile row
+  const int tid = threadIdx.x;
+  // load: 64 rows x RL fp32 (RL % 4 == 0 since 64 * T is)
+  const int q4 = RL / 4;
+  for (int i = tid; i < 64 * q4; i += 256) {
+    const int r = i / q4, k = (i - r * q4) * 4;
+    const float4 v = *reinterpret_cast<const float4*>(d.w + ((size_t)(co0 + r) * d.C + c0) * T + k);
+    uint16_t* dst = pk + r * kPackRow + k;
+    dst[0] = bf16_bits(v.x); dst[1] = bf16_bits(v.y); dst[2] = bf16_bits(v.z); dst[3] = bf16_bits(v.w);
+  }
+  __syncthreads();
+  // wp[co][t][c]: chunk = (co, t, 8 c)
+  if (d.wp) {
+    uint16_t* wp = (uint16_t*)d.wp;
+    for (int i = tid; i < 64 * T * 8; i += 256) {
+      const int co = i / (T * 8), rem = i - co * T * 8, t = rem >> 3, cg = (rem & 7) * 8;
+      const uint16_t* src = pk + co * kPackRow + cg * T + t;
+      uint4 u;
+      u.x = (uint32_t)src[0] | ((uint32_t)src[T] << 16);
+      u.y = (uint32_t)src[2 * T] | ((uint32_t)src[3 * T] << 16);
+      u.z = (uint32_t)src[4 * T] | ((uint32_t)src[5 * T] << 16);
+      u.w = (uint32_t)src[6 * T] | ((uint32_t)src[7 * T] << 16);
+      *reinterpret_cast<uint4*>(wp + ((size_t)(co0 + co) * T + t) * d.C + c0 + cg) = u;
+    }
+  }
+  // wt[c][t][co]: chunk = (c, t, 8 co)
+  if (d.wt) {
+    uint16_t* wt = (uint16_t*)d.wt;
+    for (int i = tid; i < 64 * T * 8; i += 256) {
+      const int c = i / (T * 8), rem = i - c * T * 8, t = rem >> 3, og = (rem & 7) * 8;
+      const uint16_t* src = pk + og * kPackRow + c * T + t;
+      uint4 u;
+      u.x = (uint32_t)src[0] | ((uint32_t)src[kPackRow] << 16);
+      u.y = (uint32_t)src[2 * kPackRow] | ((uint32_t)src[3 * kPackRow] << 16);
+      u.z = (uint32_t)src[4 * kPackRow] | ((uint32_t)src[5 * kPackRow] << 16);
+      u.w = (uint32_t)src[6 * kPackRow] | ((uint32_t)src[7 * kPackRow] << 16);
+      *reinterpret_cast<uint4*>(wt + ((size_t)(c0 + c) * T + t) * d.Co + co0 + og) = u;
     }
   }
 }
@@ -137,19 +194,40 @@ VLP_EXPORT int vlp_adamw(long long n, float* p, const float* g, float* m, float*
 VLP_EXPORT int vlp_pack_conv_batch(int dtype, int n, const long long* desc, void* stream) {
   if (n < 1 || n > kPackMax) return (int)hipErrorInvalidValue;
   PackBatch b;
-  int maxn = 0;
+  int maxn = 0, maxt = 0, untiled = 0;
   for (int i = 0; i < n; ++i) {
     const long long* e = desc + 6 * i;
-    b.d[i] = PackDesc{(const float*)e[0], (void*)e[1], (void*)e[2], (int)e[3], (int)e[4], (int)e[5]};
-    if (e[3] * e[4] > maxn) maxn = (int)(e[3] * e[4]);
+    const int Co = (int)e[3], C = (int)e[4], T = (int)e[5];
+    const int tiled = dtype == VLP_BF16 && Co % 64 == 0 && C % 64 == 0 && T >= 1 && T <= 9 && (e[0] & 15) == 0 &&
+                      (e[1] & 15) == 0 && (e[2] & 15) == 0;
+    b.d[i] = PackDesc{(const float*)e[0], (void*)e[1], (void*)e[2], Co, C, T, tiled};
+    if (tiled) {
+      if ((Co / 64) * (C / 64) > maxt) maxt = (Co / 64) * (C / 64);
+    } else {
+      ++untiled;
+      if (e[3] * e[4] > maxn) maxn = (int)(e[3] * e[4]);
+    }
   }
-  int gx = (2 * maxn + 255) / 256;
-  if (gx > 2048) gx = 2048;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == VLP_BF16)
-    hipLaunchKernelGGL(pack_conv_batch_kernel<bf16>, dim3(gx, n), dim3(256), 0, st, b);
-  else
-    hipLaunchKernelGGL(pack_conv_batch_kernel<float>, dim3(gx, n), dim3(256), 0, st, b);
+  if (maxt > 0) {
+    constexpr int lds = 64 * kPackRow * 2;
+    // per call (the attribute is per device; a process may drive several)
+    if (hipFuncSetAttribute((const void*)&pack_conv_tile_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds) !=
+        hipSuccess)
+      return (int)hipGetLastError();
+    hipLaunchKernelGGL(pack_conv_tile_kernel, dim3(maxt, n), dim3(256), lds, st, b);
+    if (hipGetLastError() != hipSuccess) return (int)hipErrorLaunchFailure;
+  }
+  if (untiled > 0) {   // the element-per-thread kernel skips the tiled entries
+    for (int i = 0; i < n; ++i)
+      if (b.d[i].tiled) b.d[i].wp = b.d[i].wt = nullptr;
+    int gx = (2 * maxn + 255) / 256;
+    if (gx > 2048) gx = 2048;
+    if (dtype == VLP_BF16)
+      hipLaunchKernelGGL(pack_conv_batch_kernel<bf16>, dim3(gx, n), dim3(256), 0, st, b);
+    else
+      hipLaunchKernelGGL(pack_conv_batch_kernel<float>, dim3(gx, n), dim3(256), 0, st, b);
+  }
   return (int)hipGetLastError();
 }
 
