@@ -1793,6 +1793,12 @@ inline int balanced_ksplit(int tiles, int K, int slots, int min_k) {
   }
   return best;
 }
+// bit of the current device (per-device caches of per-function attributes)
+inline unsigned dev_bit() {
+  int d = 0;
+  (void)hipGetDevice(&d);
+  return 1u << (d & 31);
+}
 inline int device_cus() {
   static int n = 0;
   if (!n) {
@@ -1842,11 +1848,11 @@ inline int launch_gemm_ms(int M, int N, int K, int ksplit, const LA& la, const L
   constexpr int lds = S * (BM + BN) * 128;
   static_assert(lds <= 160 * 1024, "LDS budget");
   if constexpr (lds > 65536) {
-    static bool attr_set = false;
-    if (!attr_set) {
+    static unsigned attr_set = 0;   // one bit per device: the attribute is per device
+    if (!(attr_set & dev_bit())) {
       (void)hipFuncSetAttribute((const void*)&gemm_ms_kernel<BM, BN, WGM, WGN, S, LA, LB, EP>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      attr_set = true;
+      attr_set |= dev_bit();
     }
   }
   hipLaunchKernelGGL((gemm_ms_kernel<BM, BN, WGM, WGN, S, LA, LB, EP>), grid, dim3(WGM * WGN * 64), lds,
@@ -1895,11 +1901,11 @@ inline int launch_gemm_bk(int M, int N, int K, int ksplit, const LA& la, const L
   constexpr int lds = S * (BM + BN) * 128;
   static_assert(lds <= 160 * 1024, "LDS budget");
   if constexpr (lds > 65536) {
-    static bool attr_set = false;
-    if (!attr_set) {
+    static unsigned attr_set = 0;   // one bit per device: the attribute is per device
+    if (!(attr_set & dev_bit())) {
       (void)hipFuncSetAttribute((const void*)&gemm_bk_kernel<BM, BN, WGM, WGN, LA, LB, EP>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      attr_set = true;
+      attr_set |= dev_bit();
     }
   }
   hipLaunchKernelGGL((gemm_bk_kernel<BM, BN, WGM, WGN, LA, LB, EP>), grid, dim3(WGM * WGN * 64), lds,
@@ -1948,11 +1954,11 @@ inline int launch_gemm_big(int M, int N, int K, int ksplit, const LA& la, const 
   constexpr int lds = big_lds_bytes<BM, BN, EP>();
   static_assert(lds <= 160 * 1024, "LDS budget");
   if constexpr (lds > 65536) {
-    static bool attr_set = false;
-    if (!attr_set) {
+    static unsigned attr_set = 0;   // one bit per device: the attribute is per device
+    if (!(attr_set & dev_bit())) {
       (void)hipFuncSetAttribute((const void*)&gemm_big_kernel<BM, BN, WGM, WGN, LA, LB, EP, WPE>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      attr_set = true;
+      attr_set |= dev_bit();
     }
   }
   hipLaunchKernelGGL((gemm_big_kernel<BM, BN, WGM, WGN, LA, LB, EP, WPE>), grid, dim3(WGM * WGN * 64), lds,
@@ -2012,11 +2018,11 @@ inline int launch_gemm_pp(int M, int N, int K, int ksplit, const LA& la, const L
     }
   }
   if constexpr (lds > 65536) {
-    static bool attr_set = false;
-    if (!attr_set) {
+    static unsigned attr_set = 0;   // one bit per device: the attribute is per device
+    if (!(attr_set & dev_bit())) {
       (void)hipFuncSetAttribute((const void*)&gemm_pp_kernel<BM, BN, WGM, WGN, LA, LB, EP>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      attr_set = true;
+      attr_set |= dev_bit();
     }
   }
   hipLaunchKernelGGL((gemm_pp_kernel<BM, BN, WGM, WGN, LA, LB, EP>), grid, dim3(WGM * WGN * 64), lds, stream, sh,
@@ -2177,11 +2183,11 @@ inline int launch_gemm(int M, int N, int K, int ksplit, const LA& la, const LB& 
   dim3 grid(sh.tiles_m * sh.tiles_n, ksplit, 1);
   constexpr int lds = gemm_lds_bytes<T, BM, BN>();
   if constexpr (lds > 65536) {
-    static bool attr_set = false;
-    if (!attr_set) {
+    static unsigned attr_set = 0;   // one bit per device: the attribute is per device
+    if (!(attr_set & dev_bit())) {
       (void)hipFuncSetAttribute((const void*)&gemm_kernel<T, BM, BN, WGM, LA, LB, EP>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      attr_set = true;
+      attr_set |= dev_bit();
     }
   }
   hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WGM, LA, LB, EP>), grid, dim3(256), lds, stream, sh, la, lb, ep);
