@@ -172,24 +172,69 @@ template <> __device__ __forceinline__ void st4<float>(float* p, float a, float 
 // Register-staged tile copy (issue the global loads early, write the LDS
 // image after the barrier): rows [t0, t0+64) x 32 channels at column `col` of a
 // [rows][ld] tensor; rows >= N are zero in the image.  The loads are
-// unconditional (row index clamped to N-1) so nothing waits on them before the
-// store; the store applies the row mask.  256 threads.
+// unconditional (row index clamped to N-1); the store applies the row mask.
+// 256 threads.  The loads are inline asm, waited for by hand at the bottom of the
+// tile loop (vmcnt 0, tied to the loaded registers, so no copy of them can be
+// placed before the data lands -- waiting at the top let the loop's back-edge
+// copies read registers still in flight): as plain loads the compiler sank the
+// next tile's loads below the tile's MFMAs, to the loop header right in front of
+// their store, so every tile of the dK/dV kernel waited out a full global-load
+// round trip twice (r4 PMC: half of its wave cycles waiting).
+#ifndef VLP_ATTN_ASMLOAD   // 0: plain loads (the compiler places them), for A/B
+#define VLP_ATTN_ASMLOAD 1
+#endif
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+// early-clobber outputs: the destination must not share registers with the
+// address (the compiler would otherwise reuse them and copy the "result" early)
+__device__ __forceinline__ u32x4 ldg16_issue(const void* p) {
+  u32x4 r;
+#if VLP_ATTN_ASMLOAD
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(r) : "v"(p) : "memory");
+#else
+  r = *reinterpret_cast<const u32x4*>(p);
+#endif
+  return r;
+}
+__device__ __forceinline__ float ldg4_issue(const float* p) {
+#if VLP_ATTN_ASMLOAD
+  float r;
+  asm volatile("global_load_dword %0, %1, off" : "=&v"(r) : "v"(p) : "memory");
+  return r;
+#else
+  return *p;
+#endif
+}
+// make a value loaded by an ordinary (compiler-tracked) load opaque: the
+// compiler waits for the load once here instead of at its first use inside the
+// tile loop, where its waitcnt pass would put a vmcnt(0) on every iteration and
+// drain the hand-issued tile prefetch
+template <class X>
+__device__ __forceinline__ void launder(X& x) {
+  asm volatile("" : "+v"(x));
+}
 template <typename T>
 struct TileStage {
   static constexpr int EPC = 16 / (int)sizeof(T), CPR = kDh / EPC, CPT = kTileRows * CPR / 256;
-  uint4 v[CPT];
+  u32x4 v[CPT];
   __device__ __forceinline__ void load(const T* src, size_t ld, int col, int t0, int N) {
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
       const int q = threadIdx.x + 256 * c, r = q / CPR, ch = q % CPR;
-      v[c] = ldg16(src + (size_t)min(t0 + r, N - 1) * ld + col + ch * EPC);
+      v[c] = ldg16_issue(src + (size_t)min(t0 + r, N - 1) * ld + col + ch * EPC);
     }
+  }
+  // every vector-memory load of this thread retired (the staged registers tied in)
+  __device__ __forceinline__ void wait() {
+#pragma unroll
+    for (int c = 0; c < CPT; ++c)
+      if (VLP_ATTN_ASMLOAD) asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[c])::"memory");
   }
   __device__ __forceinline__ void store(T* img, int t0, int N) const {
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
       const int q = threadIdx.x + 256 * c, r = q / CPR, ch = q % CPR;
-      *reinterpret_cast<uint4*>(img + FA<T>::at(r, ch * EPC)) = t0 + r < N ? v[c] : zero4();
+      const u32x4 z = {0u, 0u, 0u, 0u};
+      *reinterpret_cast<u32x4*>(img + FA<T>::at(r, ch * EPC)) = t0 + r < N ? v[c] : z;
     }
   }
 };
@@ -257,9 +302,15 @@ nest_attn_fwd_kernel(int BT, int H, int N, const T* __restrict__ qkv, T* __restr
     lsum[u] = o[u][0] = o[u][1] = v4f{0.f, 0.f, 0.f, 0.f};
   }
   const int nt = (N + kTileRows - 1) / kTileRows;
+#pragma unroll
+  for (int u = 0; u < QW; ++u)
+#pragma unroll
+    for (int ks = 0; ks < KSN; ++ks) launder(qf[u][ks]);
   TileStage<T> stk, stv;
   stk.load(base, ld3, C + h * kDh, 0, N);
   stv.load(base, ld3, 2 * C + h * kDh, 0, N);
+  stk.wait();
+  stv.wait();
   for (int t = 0; t < nt; ++t) {
     __syncthreads();   // every wave is done with the previous tile
     stk.store(sK, t * kTileRows, N);
@@ -316,6 +367,8 @@ nest_attn_fwd_kernel(int BT, int H, int N, const T* __restrict__ qkv, T* __restr
         M::mma(lsum[u], one, pf);
       }
     }
+    stk.wait();   // the next tile's rows landed (issued before this tile's MFMAs)
+    stv.wait();
   }
 #pragma unroll
   for (int u = 0; u < QW; ++u) {
@@ -398,9 +451,21 @@ nest_attn_bwd_dq_kernel(int BT, int H, int N, const T* __restrict__ qkv, const T
 #pragma unroll
   for (int u = 0; u < QW; ++u) acc[u][0] = acc[u][1] = v4f{0.f, 0.f, 0.f, 0.f};
   const int nt = (N + kTileRows - 1) / kTileRows;
+#pragma unroll
+  for (int u = 0; u < QW; ++u) {
+#pragma unroll
+    for (int ks = 0; ks < KSN; ++ks) {
+      launder(qf[u][ks]);
+      launder(df[u][ks]);
+    }
+    launder(lq[u]);
+    launder(ndl[u]);
+  }
   TileStage<T> stk, stv;
   stk.load(base, ld3, C + h * kDh, 0, N);
   stv.load(base, ld3, 2 * C + h * kDh, 0, N);
+  stk.wait();
+  stv.wait();
   for (int t = 0; t < nt; ++t) {
     __syncthreads();
     stk.store(sK, t * kTileRows, N);
@@ -451,6 +516,8 @@ nest_attn_bwd_dq_kernel(int BT, int H, int N, const T* __restrict__ qkv, const T
         M::mma(acc[u][1], k1, pf);
       }
     }
+    stk.wait();
+    stv.wait();
   }
 #pragma unroll
   for (int u = 0; u < QW; ++u) {
@@ -504,16 +571,29 @@ nest_attn_bwd_dkdv_kernel(int BT, int H, int N, const T* __restrict__ qkv, const
   for (int u = 0; u < KW; ++u) dk[u][0] = dk[u][1] = dv[u][0] = dv[u][1] = v4f{0.f, 0.f, 0.f, 0.f};
   const size_t sb = ((size_t)bt * H + h) * N;
   const int nt = (N + kTileRows - 1) / kTileRows;
+#pragma unroll
+  for (int u = 0; u < KW; ++u)
+#pragma unroll
+    for (int ks = 0; ks < KSN; ++ks) {
+      launder(kf[u][ks]);
+      launder(vf[u][ks]);
+    }
   TileStage<T> stq, std_;
   float pl = 0.f, pd = 0.f;
   auto load_rows = [&](int t0) {
     stq.load(base, ld3, h * kDh, t0, N);
     std_.load(dbase, C, h * kDh, t0, N);
     const int q = min(t0 + (int)(threadIdx.x & (kTileRows - 1)), N - 1);   // every thread: no phi
-    pl = lse[sb + q];
-    pd = delta[sb + q];
+    pl = ldg4_issue(lse + sb + q);
+    pd = ldg4_issue(delta + sb + q);
+  };
+  auto wait_rows = [&]() {
+    stq.wait();
+    std_.wait();
+    if (VLP_ATTN_ASMLOAD) asm volatile("s_waitcnt vmcnt(0)" : "+v"(pl), "+v"(pd)::"memory");
   };
   load_rows(0);
+  wait_rows();
   for (int t = 0; t < nt; ++t) {
     __syncthreads();
     stq.store(sQ, t * kTileRows, N);
@@ -565,6 +645,7 @@ nest_attn_bwd_dkdv_kernel(int BT, int H, int N, const T* __restrict__ qkv, const
           M::mma(dk[u][db], qt_, M::pfrag(ds[u], hs));
         }
       }
+    wait_rows();   // the next tile's rows landed (issued before this tile's MFMAs)
   }
 #pragma unroll
   for (int u = 0; u < KW; ++u) {
