@@ -26,7 +26,6 @@ the strict fp32 envelope; both ranks hold bit-identical gradients after the
 all-reduce.
 """
 import os
-import socket
 import subprocess
 import sys
 
@@ -41,14 +40,6 @@ pytestmark = pytest.mark.gpu
 B, H, T, SEED = 4, 64, 12, 5
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def rel(a, b):
     a, b = a.double().cpu(), b.double().cpu()
     return ((a - b).norm() / (b.norm() + 1e-30)).item()
@@ -59,8 +50,11 @@ def ranks(tmp_path_factory):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     out = tmp_path_factory.mktemp("dp")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+    # --standalone: torchrun binds its own free rendezvous port on 127.0.0.1 (a port
+    # picked here and released before torchrun binds it can be taken in between:
+    # EADDRINUSE seen once on a shared box)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+           "--nnodes=1", "--nproc-per-node", "2",
            os.path.join(ROOT, "tests", "_dp_worker.py"), str(out), str(B), str(H), str(T), str(SEED)]
     env = dict(os.environ, OMP_NUM_THREADS="4")
     r = subprocess.run(cmd, env=env, timeout=300, capture_output=True, text=True)
