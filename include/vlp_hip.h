@@ -31,8 +31,9 @@
 extern "C" {
 #endif
 
-/* 2 since r4 (r3 added ws / ws_floats to vlp_clip_loss_fused and made it write its
- * outputs); the Python binding refuses any other value. */
+/* 3 since r5 (r4's 2 plus role_w on vlp_clip_loss_fused / vlp_ce_sym; the dy^T
+ * operands of vlp_conv_wgrad / vlp_stem_wgrad / vlp_bn_bwd_apply removed); the
+ * Python binding refuses any other value. */
 int vlp_abi_version(void);
 /* Diagnostic: register-only v_mfma_f32_16x16x32_bf16 chains (8 independent
  * accumulators per wave, 4 waves per block) to measure the card's dense bf16
@@ -140,12 +141,10 @@ int vlp_conv_wgrad_ws(int dtype, const void* dy, const void* x, float* split_ws,
 int vlp_conv_wgrad_fold(int Co, int C, int KH, int KW, int nsplit, const float* split_ws, float* grad,
                         void* stream);
 /* dw_ws[Co][KH][KW][C] += sum over pixels dy x_patch (fp32 atomics; zero first).
- * Optional BN+ReLU-on-load of x as in vlp_conv_fwd.  dyT (optional, bf16): the
- * same gradient transposed to [Co][N*Ho*Wo] (vlp_bn_bwd_apply writes it); when
- * given it is the GEMM's A operand instead of dy. */
+ * Optional BN+ReLU-on-load of x as in vlp_conv_fwd. */
 int vlp_conv_wgrad(int dtype, const void* dy, const void* x, float* dw_ws, int N, int H, int W,
                    int C, int Co, int KH, int KW, int S, int P, const float* in_scale,
-                   const float* in_shift, const void* dyT, void* stream);
+                   const float* in_shift, void* stream);
 
 /* stem conv 7x7/2 pad 3, 3 -> 64 channels (timm resnet34 conv1, called from
  * ImageEncoder.forward, VisionLanguageModule.py:34-35), on a zero-padded NHWC4
@@ -159,7 +158,7 @@ int vlp_stem_prep_u8(int dtype, const uint8_t* x_u8, void* xp, int N, int H, int
 int vlp_stem_fwd(int dtype, const void* xp, const void* wp, void* y, int N, int H, int W,
                  double* stat_sum, double* stat_sumsq, int stat_rep, void* stream);
 int vlp_stem_wgrad(int dtype, const void* dy, const void* xp, float* dw_ws, int N, int H, int W,
-                   const void* dyT, void* stream);
+                   void* stream);
 /* the same through per-split fp32 slabs split_ws[s][64][256] (plain stores, no
  * atomics; *nsplit receives the split count), then vlp_stem_wgrad_fold sums
  * them into grad[64][3][7][7] (timm conv1.weight layout), overwriting it */
@@ -256,15 +255,13 @@ int vlp_bn_bwd_reduce(int dtype, long long M, int C, const void* dout, const flo
  * sums already folded, as vlp_bn_bwd_apply reads them) */
 int vlp_bn_bwd_coef(long long M, int C, const float* gamma, const float* istd, const float* mean,
                     const double* sum_g, const double* sum_gx, float* coef, void* stream);
-/* dy_s = gamma_s*istd_s*(g - mean(g) - xhat_s*mean(g*xhat_s)) for sides a, b; g_out = g.
- * dyT_a / dyT_b (optional, bf16, C % 64 == 0, M % 8 == 0): also write dy_s
- * transposed to [C][M] (the weight-gradient GEMM's pixel-contiguous operand). */
+/* dy_s = gamma_s*istd_s*(g - mean(g) - xhat_s*mean(g*xhat_s)) for sides a, b; g_out = g. */
 int vlp_bn_bwd_apply(int dtype, long long M, int C, const void* dout, const float* dbc, int HW,
                      const void* mask, const void* ya, const float* mean_a, const float* istd_a,
                      const float* gamma_a, const double* sum_g_a, const double* sum_gx_a,
                      void* dy_a, const void* yb, const float* mean_b, const float* istd_b,
                      const float* gamma_b, const double* sum_g_b, const double* sum_gx_b,
-                     void* dy_b, void* g_out, void* dyT_a, void* dyT_b, void* stream);
+                     void* dy_b, void* g_out, void* stream);
 int vlp_bn_param_grad(int C, const double* sum_g, const double* sum_gx, float* dgamma,
                       float* dbeta, void* stream);
 /* out = maxpool3x3/2(relu(sc*y + sh)), idx = argmax tap (0..8) per element;
@@ -412,17 +409,21 @@ int vlp_clip_loss_finish(const float* parts, int N, float* out, void* stream);
  * [offset, offset+B).  Written (not accumulated): g_img_all/g_txt_all, d loss /
  * d embeddings for all N rows; d_logit_scale; loss_parts[0] the sum of the
  * image->text CE terms of the local rows, loss_parts[1] text->image; lse_out
- * (optional) [2][B].  ws: vlp_clip_loss_ws_floats(B, N, E) floats of scratch
+ * (optional) [2][B].  role_w (optional, device, 2 floats): the gradients are those
+ * of (role_w[0] image_loss + role_w[1] text_loss) / 2 (NULL: {1, 1}, the
+ * reference's loss; other weights carry gradients of image_loss / text_loss).  ws: vlp_clip_loss_ws_floats(B, N, E) floats of scratch
  * (cosines / softmax weights, split-key partials, dq slabs; every product on fp32
- * MFMA; no atomics, bitwise reproducible).  ABI 2 (vlp_abi_version). */
+ * MFMA; no atomics, bitwise reproducible).  ABI 3 (vlp_abi_version). */
 int vlp_clip_loss_ws_floats(int B, int N, int E, long long* n);
 int vlp_clip_loss_fused(int B, int N, int E, int offset, const float* img_all,
                         const float* txt_all, const float* logit_scale, float* g_img_all,
                         float* g_txt_all, float* d_logit_scale, float* loss_parts,
-                        float* lse_out, float* ws, long long ws_floats, void* stream);
+                        float* lse_out, const float* role_w, float* ws, long long ws_floats,
+                        void* stream);
 /* symmetric CE over explicit logits [B][B]: out = {loss, image_loss, text_loss} (+=);
- * dlogits (+=, optional) */
-int vlp_ce_sym(int B, const float* logits, float* out, float* dlogits, void* stream);
+ * dlogits (+=, optional) = d (role_w[0] image_loss + role_w[1] text_loss) / 2 / d logits
+ * (role_w NULL: {1, 1}, the reference's loss, :550-552) */
+int vlp_ce_sym(int B, const float* logits, float* out, float* dlogits, const float* role_w, void* stream);
 int vlp_matmul(int dtype, int M, int N, int K, const void* A, int lda, int a_kc, const void* B,
                int ldb, int b_kc, void* C, int ldc, int out_f32, float alpha, int accumulate,
                void* stream);

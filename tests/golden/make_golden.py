@@ -184,6 +184,28 @@ def head_case(ref, B, seed, logit_scale=None):
     return out
 
 
+def direction_case(ref, B=8, seed=1):
+    """Gradients of the per-direction losses (the reference returns image_loss /
+    text_loss as autograd tensors, :550-552): image_loss alone, and
+    0.7 * loss + 1.3 * text_loss, through the reference forward + _compute_loss."""
+    out = {"B": torch.tensor(B), "seed": torch.tensor(seed)}
+    for tag, wl, wi, wt in (("image_only", 0.0, 1.0, 0.0), ("mixed", 0.7, 0.0, 1.3)):
+        model = build_reference_model(ref, 0)
+        g = torch.Generator().manual_seed(1000 + seed)
+        f_img = torch.randn(B, 512, generator=g).requires_grad_()
+        f_txt = torch.randn(B, 312, generator=g).requires_grad_()
+        model.image_encoder = _Fixed(f_img)
+        model.text_encoder = _Fixed(f_txt)
+        logits, ie, te = model({"x-ray": None, "caption_tokenized": {}})
+        loss, li, lt = model._compute_loss(logits, deduplicate=False, masked=False)
+        (wl * loss + wi * li + wt * lt).backward()
+        out[tag] = {"weights": torch.tensor([wl, wi, wt]), "d_f_img": f_img.grad.clone(),
+                    "d_f_txt": f_txt.grad.clone(), "d_logit_scale": model.logit_scale.grad.clone(),
+                    "d_image_projection_rows16": model.image_projection.grad[:16].clone(),
+                    "d_text_projection_rows16": model.text_projection.grad[:16].clone()}
+    return out
+
+
 def head_inputs(B, seed):
     """Regenerate the head-case features exactly as head_case drew them."""
     g = torch.Generator().manual_seed(1000 + seed)
@@ -283,6 +305,9 @@ def known_answers(ref):
 
 def main():
     ref = import_reference()
+    if sys.argv[1:] == ["directions"]:   # r5: only the per-direction fixture
+        torch.save(direction_case(ref), os.path.join(HERE, "head_dir_B8_s1.pt"))
+        return
     torch.save(known_answers(ref), os.path.join(HERE, "known_answers.pt"))
     for B, seed, ls in ((4, 0, None), (8, 1, None), (8, 2, math.log(150.0)), (256, 3, None)):
         tag = f"head_B{B}_s{seed}"

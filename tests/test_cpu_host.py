@@ -45,7 +45,7 @@ def test_library_loads_with_typed_bindings():
         fn = L._fns[name]
         assert len(fn.argtypes) == len(p["args"]), name
     # pure-host entry point: no device work
-    assert L._dll.vlp_abi_version() == 2
+    assert L._dll.vlp_abi_version() == 3
 
 
 def test_every_declaration_cites_the_reference():
@@ -140,6 +140,12 @@ def test_constructor_contract():
     assert m.hparams["masked_loss"] is False
     with pytest.raises(ValueError):
         _module(text_encoder_model="gpt2")
+    # the HIP contrastive head takes 4 <= E <= 256, E % 4 == 0 (the reference configs
+    # use 32 and 128): anything else is refused at construction, not mid-step
+    assert _module(embedding_dim=32)._head.embedding_dim == 32
+    for bad in (30, 512):
+        with pytest.raises(ValueError, match="embedding_dim"):
+            _module(embedding_dim=bad)
 
 
 def test_validation_dataloader_index_contract(module):

@@ -44,6 +44,11 @@ def rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-30)).item()
 
 
+def cosine(a, b):
+    a, b = a.double().flatten().cpu(), b.double().flatten().cpu()
+    return (a @ b / (a.norm() * b.norm() + 1e-30)).item()
+
+
 def module_init_state():
     """The module's own init (what bench.py and a fresh training run start from)."""
     from src.models.pretrain.VisionLanguageModule import VisionLanguageModule
@@ -244,6 +249,16 @@ def test_bf16_live_residual_per_tensor_vs_autocast(bs, side, u8):
         qb = k.replace("key.bias", "query.bias")
         assert hip["grads"][k].norm() <= 2e-2 * hip["grads"][qb].norm() + 1e-9, (k, hip["grads"][k].norm())
     names = [k for k in ref["grads"] if k not in kb]
+    # a zeroed or non-finite HIP gradient fails here, whatever its rel-L2 gate says
+    bad = [k for k in names if hip["grads"][k].norm() == 0 or not torch.isfinite(hip["grads"][k]).all()]
+    assert not bad, bad
+    # direction: a sign-flipped or scrambled gradient has cos ~ -1 / ~0
+    c_hip = {k: cosine(hip["grads"][k], ref["grads"][k]) for k in names}
+    c_ac = {k: cosine(ac["grads"][k], ref["grads"][k]) for k in names}
+    worst_c = sorted(((c_hip[k] - (c_ac[k] - 0.05), k, c_hip[k], c_ac[k]) for k in names))
+    print("  cosine worst (margin, name, hip, autocast):",
+          [(round(a, 4), k, round(b, 4), round(c, 4)) for a, k, b, c in worst_c[:4]])
+    assert worst_c[0][0] >= 0, worst_c[:3]
     t_hip = {k: rel(hip["grads"][k], ref["grads"][k]) for k in names}
     t_ac = {k: rel(ac["grads"][k], ref["grads"][k]) for k in names}
     excess = sorted(((t_hip[k] - (1.5 * t_ac[k] + 0.02), k, t_hip[k], t_ac[k]) for k in names), reverse=True)

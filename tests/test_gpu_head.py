@@ -21,6 +21,7 @@ promotes its logits and loss to fp64):
   feature / projection / embedding gradients   rtol 1e-4, atol 1e-6 * max|golden|
   d logit_scale           rel 1e-4 (exactly 0 when clamped)
 """
+import math
 import os
 
 import pytest
@@ -67,8 +68,9 @@ def make_head(logit_scale):
     return head
 
 
-def run_head(head, f_img, f_txt):
-    """The ClipStepFn head, world = 1: forward + fused loss + backward."""
+def run_head(head, f_img, f_txt, role_w=None):
+    """The ClipStepFn head, world = 1: forward + fused loss + backward (role_w: the
+    per-direction weights of the image_loss / text_loss gradients)."""
     from vlp_amd import ops
     from vlp_amd.clip_model import _project_backward, _project_normalize
     dev = torch.device("cuda")
@@ -81,7 +83,7 @@ def run_head(head, f_img, f_txt):
     g_txt = torch.zeros(B, E, device=dev)
     small = torch.zeros(4, device=dev)
     ops.clip_loss_fused(B, B, E, 0, ie, te, head.arena.view("logit_scale"), g_img, g_txt, small[2:3],
-                        small[0:2])
+                        small[0:2], role_w=role_w)
     out = torch.empty(3, device=dev)
     ops.clip_loss_finish(small[0:2], B, out)
     gs = torch.ones(1, device=dev)
@@ -131,6 +133,28 @@ def test_clip_loss_fused_vs_reference(tag):
         assert "s2" in tag and dls == 0.0, dls
     else:
         assert abs(dls - gls) <= 1e-4 * abs(gls), (dls, gls)
+
+
+@pytest.mark.parametrize("case", ["image_only", "mixed"])
+def test_clip_loss_fused_per_direction_vs_reference(case):
+    """Gradients of image_loss alone and of 0.7 loss + 1.3 text_loss (the reference's
+    image_loss / text_loss are autograd tensors, :550-552), made by the reference in
+    tests/golden/make_golden.py (head_dir_B8_s1.pt): role weights w_r = w_loss + 2 w_r."""
+    from vlp_amd.clip_model import role_weights
+    gd = load("head_dir_B8_s1.pt")
+    B, seed = int(gd["B"]), int(gd["seed"])
+    c = gd[case]
+    f_img, f_txt = head_inputs(B, seed)
+    head = make_head(torch.tensor([math.log(1 / 0.07)]))   # the reference init (:111)
+    dev = torch.device("cuda")
+    wl, wi, wt = [torch.tensor(v, device=dev) for v in c["weights"].tolist()]
+    r = run_head(head, f_img, f_txt, role_w=role_weights(wl, wi, wt, dev))
+    close(r["d_f_img"], c["d_f_img"], 1e-4, 1e-6, "d_f_img")
+    close(r["d_f_txt"], c["d_f_txt"], 1e-4, 1e-6, "d_f_txt")
+    close(r["d_image_projection"][:16], c["d_image_projection_rows16"], 1e-4, 1e-6, "d_image_projection")
+    close(r["d_text_projection"][:16], c["d_text_projection_rows16"], 1e-4, 1e-6, "d_text_projection")
+    dls, gls = r["d_logit_scale"].item(), c["d_logit_scale"].item()
+    assert abs(dls - gls) <= 1e-4 * abs(gls), (dls, gls)
 
 
 def test_clip_loss_fused_global_batch_8_ranks():
@@ -209,3 +233,51 @@ def test_clip_loss_fused_deterministic_and_timed_N2048():
     ms = sorted(ts)[5]
     print(f"clip_loss_fused per rank at N = 2048: {ms * 1e3:.1f} us")
     assert ms < 0.5, ms
+
+
+@pytest.mark.parametrize("E", [32, 64, 200, 256])
+def test_clip_loss_fused_embedding_dims(E):
+    """ADVICE r4: every embedding width the kernels accept (E % 4 == 0, E <= 256;
+    E = 256 takes the 16-chunk register tiles and ~130 KB of LDS in clip_dq; 200
+    is not a multiple of 16) against a torch fp64 symmetric cross-entropy built
+    here (reference forward :441-461, _compute_loss :532-554).  N = 101 split over
+    three "ranks" of B = 37, 37, 27 (B not a multiple of 16, N not a multiple of
+    64): their summed partials and gradients are the global-batch loss and its
+    gradients, as the collectives of ClipStepFn form them."""
+    from vlp_amd import ops
+    F = torch.nn.functional
+    N, Bs = 101, [37, 37, 27]
+    g = torch.Generator().manual_seed(E)
+    ie = F.normalize(torch.randn(N, E, generator=g, dtype=torch.float64))
+    te = F.normalize(torch.randn(N, E, generator=g, dtype=torch.float64))
+    ls = torch.tensor([2.3], dtype=torch.float64)
+    x, y, l = ie.clone().requires_grad_(), te.clone().requires_grad_(), ls.clone().requires_grad_()
+    s = torch.clamp(l.exp(), max=100.0)
+    logits = s * x @ y.t()
+    lab = torch.arange(N)
+    li, lt = F.cross_entropy(logits, lab), F.cross_entropy(logits.t(), lab)
+    ((li + lt) / 2).backward()
+    parts = torch.zeros(2, dtype=torch.float64)
+    dls = 0.0
+    gi_all = torch.zeros(N, E, dtype=torch.float64)
+    gt_all = torch.zeros(N, E, dtype=torch.float64)
+    ied, ted = ie.float().cuda(), te.float().cuda()
+    lsd = ls.float().cuda()
+    off = 0
+    for B in Bs:
+        gi = torch.full((N, E), float("nan"), device="cuda")
+        gt = torch.full((N, E), float("nan"), device="cuda")
+        small = torch.zeros(4, device="cuda")
+        ops.clip_loss_fused(B, N, E, off, ied, ted, lsd, gi, gt, small[2:3], small[0:2])
+        torch.cuda.synchronize()
+        assert not torch.isnan(gi).any() and not torch.isnan(gt).any()
+        parts += small[0:2].double().cpu()
+        dls += small[2].item()
+        gi_all += gi.double().cpu()
+        gt_all += gt.double().cpu()
+        off += B
+    assert abs(parts[0].item() / N - li.item()) <= 1e-5, (parts[0].item() / N, li.item())
+    assert abs(parts[1].item() / N - lt.item()) <= 1e-5, (parts[1].item() / N, lt.item())
+    close(gi_all, x.grad, 1e-4, 1e-6, f"d img emb E={E}")
+    close(gt_all, y.grad, 1e-4, 1e-6, f"d txt emb E={E}")
+    assert abs(dls - l.grad.item()) <= 1e-4 * abs(l.grad.item()), (dls, l.grad.item())

@@ -181,6 +181,46 @@ def test_grads_vs_oracle_fp32(B, H, T):
             assert rel(sd[k], osd[k]) < 1e-4, k
 
 
+def _oracle_obj(batch, seed, dt, w):
+    o = make_oracle(seed).to(dt)
+    o.train()
+    b = dict(batch)
+    b["x-ray"] = batch["x-ray"].to(dt)
+    lg, _, _ = o(b)
+    lo, li, lt = compute_loss(lg)
+    (w[0] * lo + w[1] * li + w[2] * lt).backward()
+    return o
+
+
+@pytest.mark.parametrize("path", ["fused_step", "api"])
+@pytest.mark.parametrize("w", [(0.0, 1.0, 0.0), (0.7, 0.0, 1.3)], ids=["image_loss_only", "mixed"])
+def test_per_direction_loss_gradients_fp32(path, w):
+    """image_loss and text_loss are autograd tensors in the
+    reference (:550-552).  Backward of w0*loss + w1*image_loss + w2*text_loss
+    through the fused training step (ClipStepFn reruns the head with per-direction
+    weights) and through the API forward + _compute_loss (_SymCEFn), every
+    gradient in the strict fp64 envelope of the oracle's same objective."""
+    B, H, T = 4, 64, 12
+    batch = synth_batch(B, H, T, 0)
+    m = make_model("fp32")
+    m.train()
+    if path == "fused_step":
+        loss, li, lt, _, _ = m.training_step_outputs(batch)
+    else:
+        logits, _, _ = m(batch)
+        loss, li, lt = m._compute_loss(logits, deduplicate=False, masked=False)
+    obj = w[1] * li + w[2] * lt
+    if w[0]:
+        obj = obj + w[0] * loss
+    obj.backward()
+    torch.cuda.synchronize()
+    o32, o64 = _oracle_obj(batch, 0, torch.float32, w), _oracle_obj(batch, 0, torch.float64, w)
+    grads = [(k, p.grad) for k, p in m.named_parameters()]
+    assert all(g is not None and torch.isfinite(g).all() for k, g in grads if dict(o64.named_parameters())[k].grad
+               is not None)
+    grad_envelope_check(grads, o32, o64, strict=True)
+
+
 def test_api_forward_and_compute_loss_fp32():
     B, H, T = 4, 64, 12
     gd = torch.load(os.path.join(GOLD, "step_B4_H64_T12.pt"), weights_only=True)

@@ -242,3 +242,56 @@ def test_layernorm_fwd_bwd_add_rowscale(ops, dt, D):
     assert rel(dx.float(), dxref) < tol
     assert rel(dxs.float(), s.double().repeat_interleave(rps)[:, None] * dxref) < tol
     assert rel(dg, gd.grad) < 1e-5 and rel(db, bd.grad) < 1e-5
+
+
+@pytest.mark.parametrize("dt", DT)
+@pytest.mark.parametrize("BT,H,N,amp", [(2, 3, 1024, 1.0), (3, 2, 200, 3.0), (4, 12, 256, 1.0), (2, 1, 70, 1.0)])
+def test_attention_asm_loads_match_compiler_loads(ops, dt, BT, H, N, amp):
+    """the attention kernels issue their tile loads as inline asm and
+    wait for them by hand (csrc/nest_ops.hip, VLP_ATTN_ASMLOAD), which is only
+    correct while the compiler never copies an in-flight register before the
+    wait.  The build refuses scratch in those kernels (csrc/Makefile); here the
+    product library must be BIT-IDENTICAL to libvlp_nest_plainload.so, the same
+    source built with compiler-placed loads, for fwd, dQ and dK/dV."""
+    import ctypes
+    import os
+    from vlp_amd import _lib
+    path = os.path.join(os.path.dirname(_lib.__file__), "libvlp_nest_plainload.so")
+    plain = ctypes.CDLL(path)
+    protos = _lib.parse_header()
+    fns = {}
+    for name in ("vlp_nest_attn_fwd", "vlp_nest_attn_bwd"):
+        f = getattr(plain, name)
+        f.argtypes = [ctypes.c_void_p if t == "ptr" else _lib._CTYPE[t] for t, _ in protos[name]["args"]]
+        f.restype = ctypes.c_int
+        fns[name] = f
+    g = torch.Generator().manual_seed(7 * N + H)
+    C = 32 * H
+    qkv = torch.randn(BT * N, 3 * C, generator=g)
+    qkv[:, :2 * C] *= amp
+    qd = qkv.to(dt).cuda()
+    do = torch.randn(BT * N, C, generator=g).to(dt).cuda()
+    sc = 1 / math.sqrt(32)
+    code = _lib.BF16 if dt == torch.bfloat16 else _lib.F32
+    st = torch.cuda.current_stream().cuda_stream
+    res = []
+    for use_plain in (False, True):
+        out = torch.full((BT * N, C), float("nan"), dtype=dt, device="cuda")
+        lse = torch.full((BT * H * N,), float("nan"), device="cuda")
+        dqkv = torch.full_like(qd, float("nan"))
+        delta = torch.empty(BT * H * N, device="cuda")
+        if use_plain:
+            assert fns["vlp_nest_attn_fwd"](code, BT, H, N, 32, qd.data_ptr(), out.data_ptr(), lse.data_ptr(),
+                                            sc, st) == 0
+            assert fns["vlp_nest_attn_bwd"](code, BT, H, N, 32, qd.data_ptr(), out.data_ptr(), do.data_ptr(),
+                                            lse.data_ptr(), delta.data_ptr(), dqkv.data_ptr(), sc, st) == 0
+        else:
+            ops.nest_attn_fwd(qd, out, lse, BT, H, N, sc)
+            ops.nest_attn_bwd(qd, out, do, lse, delta, dqkv, BT, H, N, sc)
+        torch.cuda.synchronize()
+        res.append((out, lse, dqkv))
+    (o0, l0, d0), (o1, l1, d1) = res
+    assert torch.isfinite(o0.float()).all() and torch.isfinite(d0.float()).all()
+    assert torch.equal(o0, o1) and torch.equal(l0, l1)
+    assert torch.equal(d0[:, :C], d1[:, :C]), "dQ differs"
+    assert torch.equal(d0[:, C:], d1[:, C:]), "dK/dV differs"

@@ -3,6 +3,8 @@ reference's own code (tests/golden/make_golden.py) and the notebook
 known-answer values."""
 import os
 
+import math
+
 import pytest
 import torch
 
@@ -70,6 +72,31 @@ def test_head_against_reference(tag):
         torch.testing.assert_close(v.detach()[rows], gd[k + suffix], **tol)
     if "s2" in tag:  # clamped logit scale: exp(ln 150) > 100 => no gradient
         assert gd["d_logit_scale"].abs().item() == 0.0
+
+
+@pytest.mark.parametrize("case", ["image_only", "mixed"])
+def test_direction_gradients_against_reference(case):
+    """head_dir_B8_s1.pt: gradients of image_loss alone and of 0.7 loss + 1.3
+    text_loss, through the reference's forward + _compute_loss (:550-552)."""
+    gd = load("head_dir_B8_s1.pt")
+    B, seed = int(gd["B"]), int(gd["seed"])
+    c = gd[case]
+    f_img, f_txt = head_inputs(B, seed)
+    f_img.requires_grad_()
+    f_txt.requires_grad_()
+    Pi = W.value_for("image_projection", (512, 128)).requires_grad_()
+    Pt = W.value_for("text_projection", (312, 128)).requires_grad_()
+    ls = torch.tensor([math.log(1 / 0.07)], dtype=torch.float64).requires_grad_()
+    logits, ie, te = clip_forward(f_img, f_txt, Pi, Pt, ls)
+    loss, li, lt = compute_loss(logits)
+    wl, wi, wt = c["weights"].tolist()
+    (wl * loss + wi * li + wt * lt).backward()
+    tol = dict(rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(f_img.grad, c["d_f_img"], **tol)
+    torch.testing.assert_close(f_txt.grad, c["d_f_txt"], **tol)
+    torch.testing.assert_close(ls.grad, c["d_logit_scale"], **tol)
+    torch.testing.assert_close(Pi.grad[:16], c["d_image_projection_rows16"], **tol)
+    torch.testing.assert_close(Pt.grad[:16], c["d_text_projection_rows16"], **tol)
 
 
 def test_global_batch_definition():

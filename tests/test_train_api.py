@@ -61,6 +61,29 @@ def test_compose_defaults_and_errors():
     assert (c["data"]["batch_size"], c["data"]["image_size"], c["model"]["compute_dtype"]) == (256, 512, "bf16")
 
 
+def test_reference_experiment_keeps_fp32_arithmetic():
+    """the reference's own experiment sets no trainer precision
+    (configs/trainer/default.yaml: Lightning fp32), so its model computes in fp32;
+    only the _mi355x experiment opts into bf16, and trainer.precision selects it."""
+    import src.train as T
+    c = compose("train", ["experiment=pretrain/pretrain_resnet34_tinybert"])
+    mc = T.model_config(c, (1.0, 1.0))
+    assert "precision" not in c["trainer"] and mc["compute_dtype"] == "fp32"
+    mc["downstream_datamodule"] = None
+    m = instantiate(mc, device="cpu")
+    assert m.image_encoder.model.compute_dtype == "fp32" and m.text_encoder.model.compute_dtype == "fp32"
+    assert m._head.compute_dtype == "fp32"
+    c = compose("train", ["experiment=pretrain/pretrain_resnet34_tinybert", "+trainer.precision=bf16-mixed"])
+    assert T.model_config(c, (1.0, 1.0))["compute_dtype"] == "bf16"
+    c = compose("train", ["experiment=pretrain/pretrain_resnet34_tinybert_mi355x"])
+    assert T.model_config(c, (1.0, 1.0))["compute_dtype"] == "bf16"
+    with pytest.raises(ValueError):
+        T.compute_dtype_for("16-mixed")
+    from src.models.pretrain.VisionLanguageModule import VisionLanguageModule
+    import inspect
+    assert inspect.signature(VisionLanguageModule).parameters["compute_dtype"].default == "fp32"
+
+
 def test_datamodule_schema_and_normalisation():
     with pytest.raises(ValueError):
         PretrainDataModule(num_channels=2)

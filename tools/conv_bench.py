@@ -81,10 +81,6 @@ def main():
                 t1, t2 = torch.zeros(64 * C, dtype=torch.float64, device=dev), torch.zeros(64 * C, dtype=torch.float64, device=dev)
                 fn = lambda: ops.conv_dgrad_relu(dy, wt, H, W, C, KH, KW, S, P, mk, yb, mu, ist, t1, t2,  # noqa: E731
                                                  addend=ad, stat_rep=64)
-            elif op == "wgrad_t":      # dy^T [Co][pixels] as a K-contiguous A operand (atomic epilogue)
-                dyT = dy.reshape(-1, Co).t().contiguous()
-                gw0 = torch.zeros(Co * KH * KW * C, device=dev)
-                fn = lambda: ops.conv_wgrad(dy, x, KH, KW, S, P, gw0, dyT=dyT)  # noqa: E731
             elif op == "wgrad_a":      # the same atomic-epilogue engine on dy (MN operand)
                 gw0 = torch.zeros(Co * KH * KW * C, device=dev)
                 fn = lambda: ops.conv_wgrad(dy, x, KH, KW, S, P, gw0)  # noqa: E731

@@ -397,98 +397,6 @@ bn_bwd_apply_kernel(unsigned nchunks, int cpr, double count, const T* __restrict
   }
 }
 
-// Tiled bf16 variant that ALSO writes each side's transposed copy
-// dyT[c][p] (pixel-contiguous): the A operand of the weight-gradient GEMM,
-// which then streams K(=pixel)-contiguous 16-B chunks instead of transposing
-// in LDS.  Block = 64 pixels x 64 channels; the transpose goes through LDS
-// (row stride 66 bf16: at most 2-way bank conflicts on the scattered writes).
-template <bool HAS_B>
-__global__ void __launch_bounds__(256)
-bn_bwd_apply_t_kernel(long long M, int C, double count, const bf16* __restrict__ dout,
-                      const float* __restrict__ dbc, int HW, const bf16* __restrict__ mask,
-                      BnBwdSide A, BnBwdSide B, bf16* __restrict__ g_out, bf16* __restrict__ dyT_a,
-                      bf16* __restrict__ dyT_b) {
-  constexpr int LD = 66;
-  __shared__ bf16 ta[64 * LD];
-  __shared__ bf16 tb[HAS_B ? 64 * LD : 1];
-  const long long p0 = (long long)blockIdx.x * 64;
-  const int cb = blockIdx.y * 64;
-  const int t = threadIdx.x;
-  const int c8 = t & 7, c0 = cb + c8 * 8;
-  const float inv_count = (float)(1.0 / count);
-  const float inv_hw = 1.f / (float)HW;
-  float ka[8], ba[8], ca[8], kb[8], bb[8], cbv[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int c = c0 + j;
-    bn_bwd_coef(A.gamma[c], A.istd[c], A.mean[c], A.sum_g[c], A.sum_gx[c], inv_count, ka[j], ba[j], ca[j]);
-    if (HAS_B) bn_bwd_coef(B.gamma[c], B.istd[c], B.mean[c], B.sum_g[c], B.sum_gx[c], inv_count, kb[j], bb[j], cbv[j]);
-  }
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const int r = (t >> 3) + 32 * it;
-    const long long p = p0 + r;
-    float d[8], e[8];
-    if (p < M) {
-      const size_t i = (size_t)p * C + c0;
-      float g[8], mk[8], y[8];
-      if (dbc) {
-        const long long n = p / HW;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) g[j] = dbc[(size_t)n * C + c0 + j] * inv_hw;
-      } else {
-        Chunk<bf16>::unpack(ldg16(dout + i), g);
-      }
-      if (mask) {
-        Chunk<bf16>::unpack(ldg16(mask + i), mk);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) g[j] = mk[j] > 0.f ? g[j] : 0.f;
-      }
-      if (g_out) stg16(g_out + i, Chunk<bf16>::pack(g));
-      Chunk<bf16>::unpack(ldg16((const bf16*)A.y + i), y);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = bn_bwd_dy(ka[j], ba[j], ca[j], g[j], y[j]);
-      const uint4 pd = Chunk<bf16>::pack(d);
-      stg16((bf16*)A.dy + i, pd);
-      Chunk<bf16>::unpack(pd, d);   // transposed copy holds the same rounded values
-      if (HAS_B) {
-        Chunk<bf16>::unpack(ldg16((const bf16*)B.y + i), y);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) e[j] = bn_bwd_dy(kb[j], bb[j], cbv[j], g[j], y[j]);
-        const uint4 pe = Chunk<bf16>::pack(e);
-        stg16((bf16*)B.dy + i, pe);
-        Chunk<bf16>::unpack(pe, e);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = e[j] = 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      ta[(c8 * 8 + j) * LD + r] = (bf16)d[j];
-      if (HAS_B) tb[(c8 * 8 + j) * LD + r] = (bf16)e[j];
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const int q = t + 256 * it;
-    const int c = q >> 3, pc = (q & 7) * 8;
-    if (p0 + pc >= M) continue;
-    const size_t o = (size_t)(cb + c) * M + p0 + pc;
-    uint4 v;
-    bf16* vb = reinterpret_cast<bf16*>(&v);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) vb[j] = ta[c * LD + pc + j];
-    stg16(dyT_a + o, v);
-    if (HAS_B) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) vb[j] = tb[c * LD + pc + j];
-      stg16(dyT_b + o, v);
-    }
-  }
-}
-
 // dgamma = sum(g*xhat), dbeta = sum(g)
 __global__ void bn_param_grad_kernel(int C, const double* sum_g, const double* sum_gx, float* dgamma,
                                      float* dbeta) {
@@ -1062,23 +970,10 @@ VLP_EXPORT int vlp_bn_bwd_apply(int dtype, long long M, int C, const void* dout,
                                 void* dy_a,
                                 const void* yb, const float* mean_b, const float* istd_b,
                                 const float* gamma_b, const double* sum_g_b, const double* sum_gx_b,
-                                void* dy_b, void* g_out, void* dyT_a, void* dyT_b, void* stream) {
+                                void* dy_b, void* g_out, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   BnBwdSide A{ya, mean_a, istd_a, gamma_a, sum_g_a, sum_gx_a, dy_a};
   BnBwdSide B{yb, mean_b, istd_b, gamma_b, sum_g_b, sum_gx_b, dy_b};
-  if (dyT_a) {   // tiled variant with transposed copies (bf16, C % 64 == 0, M % 8 == 0)
-    if (dtype != VLP_BF16 || C % 64 || M % 8 || (dy_b && !dyT_b)) return (int)hipErrorInvalidValue;
-    dim3 g((unsigned)((M + 63) / 64), C / 64);
-    if (dy_b)
-      hipLaunchKernelGGL((bn_bwd_apply_t_kernel<true>), g, dim3(256), 0, st, M, C, (double)M,
-                         (const bf16*)dout, dbc, HW, (const bf16*)mask, A, B, (bf16*)g_out,
-                         (bf16*)dyT_a, (bf16*)dyT_b);
-    else
-      hipLaunchKernelGGL((bn_bwd_apply_t_kernel<false>), g, dim3(256), 0, st, M, C, (double)M,
-                         (const bf16*)dout, dbc, HW, (const bf16*)mask, A, B, (bf16*)g_out,
-                         (bf16*)dyT_a, (bf16*)nullptr);
-    return (int)hipGetLastError();
-  }
   int epc = dtype == VLP_BF16 ? 8 : 4;
   int cpr = C / epc;
   if (256 % cpr) return (int)hipErrorInvalidValue;

@@ -905,7 +905,6 @@ __device__ __forceinline__ void ld8f(const float* p, float (&o)[8]) {
 // raw conv output + BN batch statistics (sum, sum of squares)
 template <typename T>
 struct EpiConvFwd {
-  static constexpr int kDesync = 2;   // pp_desync kind (gemm.h)
   static constexpr bool kStats = true;
   double* stat1; double* stat2; int stat_rep;
   T* y; int Co;
@@ -939,7 +938,6 @@ __device__ __forceinline__ void stg16_row(void* p, const uint4& v) {
 }
 template <typename T>
 struct EpiDgradBN {
-  static constexpr int kDesync = 1;   // pp_desync kind (gemm.h)
   static constexpr bool kStats = true;
   double* stat1; double* stat2; int stat_rep;
   T* g_out; int C;
@@ -1019,7 +1017,6 @@ struct EpiDgradBN {
 // data gradient plus a residual-branch gradient
 template <typename T>
 struct EpiDgradAdd {
-  static constexpr int kDesync = 1;   // pp_desync kind (gemm.h)
   static constexpr bool kStats = false;
   double* stat1 = nullptr; double* stat2 = nullptr;
   T* dx; const T* addend; int C;
@@ -1063,7 +1060,6 @@ struct EpiDgradAdd {
 // a separate instantiation, so the activation path's registers are not shared
 template <typename T, bool BITS = false>
 struct EpiDgradRelu {
-  static constexpr int kDesync = 1;   // pp_desync kind (gemm.h)
   static constexpr bool kStats = true;
   double* stat1; double* stat2; int stat_rep;
   T* g_out; const T* addend; int C;
@@ -1161,7 +1157,6 @@ struct EpiDgradRelu {
 // Row-chunk epilogue only (the host routes it to the LDS-DMA kernels).
 template <typename T>
 struct EpiDgradRelu2 {
-  static constexpr int kDesync = 1;   // pp_desync kind (gemm.h)
   static constexpr bool kStats = true;
   static constexpr bool kStats3 = true;
   double* stat1; double* stat2; int stat_rep; double* stat3;
@@ -1197,10 +1192,19 @@ struct EpiDgradRelu2 {
     stg16_row(g_out + o, Chunk<bf16>::pack(g));
   }
   // non-row epilogue forms (instantiated by the dispatch, never launched: the
-  // host entry point refuses shapes that would not take a row-chunk kernel)
+  // host entry point refuses shapes that would not take a row-chunk kernel).
+  // They cannot form the three sums, so reaching one is a dispatch bug: trap
+  // (the launch fails loudly) instead of returning unmasked values and zero sums
   static constexpr bool kStage = false;
-  __device__ v4f value(int, int, v4f v, v4f& s1, v4f& s2) const { s1 = s2 = v4f{0.f, 0.f, 0.f, 0.f}; return v; }
-  __device__ void operator()(int, int, v4f, v4f& s1, v4f& s2) const { s1 = s2 = v4f{0.f, 0.f, 0.f, 0.f}; }
+  __device__ v4f value(int, int, v4f v, v4f& s1, v4f& s2) const {
+    __builtin_trap();
+    s1 = s2 = v4f{0.f, 0.f, 0.f, 0.f};
+    return v;
+  }
+  __device__ void operator()(int, int, v4f, v4f& s1, v4f& s2) const {
+    __builtin_trap();
+    s1 = s2 = v4f{0.f, 0.f, 0.f, 0.f};
+  }
   __device__ void store8(int row, int col, const uint4& u) const { stg16(g_out + (size_t)row * C + col, u); }
 };
 
@@ -1777,17 +1781,9 @@ static int conv_dgrad_relu_t(const void* dy, const void* wt, void* gout, ConvGeo
 
 template <typename T>
 static int conv_wgrad_t(const void* dy, const void* x, float* dw, ConvGeom g, const float* sc,
-                        const float* sh, hipStream_t st, const void* dyT = nullptr) {
+                        const float* sh, hipStream_t st) {
   g.M = g.N * g.Ho * g.Wo;        // pixels (reduction)
   g.K = g.KH * g.KW * g.C;        // columns
-  if constexpr (std::is_same<T, bf16>::value) {
-    if (dyT && !sc) {   // A = dy^T [Co][pixels]: K-contiguous, no transposing LDS reads
-      KMat<bf16> la{(const bf16*)dyT, g.M, g.Co, g.M};
-      EpiAtomic ep{nullptr, nullptr, dw, g.K, 1.0f};
-      ConvWgradB<bf16, false> lb{g, (const bf16*)x, nullptr, nullptr, g.K, make_pixstep(g, Elem<bf16>::BK)};
-      return gemm_wgrad<bf16>(g.Co, g.K, g.M, la, lb, ep, st);
-    }
-  }
   MNMat<T> la{(const T*)dy, g.Co, g.Co, g.M};
   EpiAtomic ep{nullptr, nullptr, dw, g.K, 1.0f};
   if (sc) {
@@ -2167,12 +2163,11 @@ VLP_EXPORT int vlp_conv_dgrad_relu_ds(int dtype, const void* dy, const void* dyd
 
 VLP_EXPORT int vlp_conv_wgrad(int dtype, const void* dy, const void* x, float* dw_ws, int N, int H,
                               int W, int C, int Co, int KH, int KW, int S, int P,
-                              const float* in_scale, const float* in_shift, const void* dyT,
-                              void* stream) {
+                              const float* in_scale, const float* in_shift, void* stream) {
   ConvGeom g = make_geom(N, H, W, C, Co, KH, KW, S, P);
   hipStream_t st = (hipStream_t)stream;
   if ((long long)N * H * W * C >= (1ll << 31)) return (int)hipErrorInvalidValue;   // 32-bit pixel walk
-  if (dtype == VLP_BF16) return conv_wgrad_t<bf16>(dy, x, dw_ws, g, in_scale, in_shift, st, dyT);
+  if (dtype == VLP_BF16) return conv_wgrad_t<bf16>(dy, x, dw_ws, g, in_scale, in_shift, st);
   return conv_wgrad_t<float>(dy, x, dw_ws, g, in_scale, in_shift, st);
 }
 
@@ -2246,7 +2241,7 @@ VLP_EXPORT int vlp_stem_fwd(int dtype, const void* xp, const void* wp, void* y, 
 
 // dW_ws[64][256] (kh:8, kw:8, c:4 layout), fp32, accumulated atomically.
 VLP_EXPORT int vlp_stem_wgrad(int dtype, const void* dy, const void* xp, float* dw_ws, int N, int H, int W,
-                              const void* dyT, void* stream);
+                              void* stream);
 // stem weight gradient through per-split fp32 slabs [ks][64][256] (no atomics),
 // folded straight into the parameter's [64][3][7][7] gradient:
 // 64 slab elements x 4 slab groups per block: every wave reads 256 contiguous
@@ -2283,7 +2278,7 @@ VLP_EXPORT int vlp_stem_wgrad_ws(int dtype, const void* dy, const void* xp, floa
   if (dtype != VLP_BF16 || gemm_variant() < 4) {   // other engines: atomics into slab 0
     if (hipMemsetAsync(split_ws, 0, slab * sizeof(float), st) != hipSuccess) return (int)hipGetLastError();
     *nsplit = 1;
-    return vlp_stem_wgrad(dtype, dy, xp, split_ws, N, H, W, nullptr, stream);
+    return vlp_stem_wgrad(dtype, dy, xp, split_ws, N, H, W, stream);
   }
   // <= 512 splits: the fold then reads <= 32 MB of slabs
   int mink = 2048;
@@ -2306,17 +2301,13 @@ VLP_EXPORT int vlp_stem_wgrad_fold(int nsplit, const float* split_ws, float* gra
 }
 
 VLP_EXPORT int vlp_stem_wgrad(int dtype, const void* dy, const void* xp, float* dw_ws, int N, int H,
-                              int W, const void* dyT, void* stream) {
+                              int W, void* stream) {
   StemGeom g = make_stem(N, H, W);
   hipStream_t st = (hipStream_t)stream;
   if ((long long)N * g.Hp * g.Wp * 4 >= (1ll << 31)) return (int)hipErrorInvalidValue;
   EpiAtomic ep{nullptr, nullptr, dw_ws, 256, 1.0f};
   if (dtype == VLP_BF16) {
     StemWgradB<bf16> lb{g, (const bf16*)xp, make_stem_pixstep(g, Elem<bf16>::BK)};
-    if (dyT) {   // dy^T [64][pixels]: K-contiguous A operand
-      KMat<bf16> la{(const bf16*)dyT, g.M, 64, g.M};
-      return gemm_wgrad<bf16>(64, 224, g.M, la, lb, ep, st);
-    }
     MNMat<bf16> la{(const bf16*)dy, 64, 64, g.M};
     return gemm_wgrad<bf16>(64, 224, g.M, la, lb, ep, st);
   }

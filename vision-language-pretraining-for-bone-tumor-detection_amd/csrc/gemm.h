@@ -50,11 +50,6 @@ struct GemmShape {
   int xsplit;   // 1: split-K grid is 1-D and every split's tiles share one XCD
   int dbg;      // reserved (0)
   int nsplit;   // K-splits (bk / big kernels: 1-D grid of nsplit * tiles)
-  // gemm_pp_kernel staggered rounds (pp_desync): split tiles per XCD run (0: off),
-  // the per-part fp32 accumulator images and one arrival counter per split tile
-  int sk = 0;
-  float* skp = nullptr;
-  unsigned* skc = nullptr;
 };
 
 // ---------------- LDS image addressing (bytes) ----------------
@@ -193,29 +188,6 @@ template <class E, class = void> struct SplitTrait { static constexpr bool value
 template <class E> struct SplitTrait<E, std::void_t<decltype(E::kSplitOut)>> {
   static constexpr bool value = E::kSplitOut;
 };
-// VLP_PP_DESYNC: bit mask of the epilogue kinds (DesyncTrait) whose launches
-// run staggered rounds when they span >= 2 rounds of the chip
-// Measured off (r4, conv_bench bs = 256, us per launch, d0 = off): layer 3
-// BN / ReLU epilogue 350 / 366 -> 402 / 425, layer 4 261 / 262 -> 315 / 327;
-// the schedule alone (hand-over skipped, wrong sums) already 363 / 383 and
-// 301 / 303, and a blockIdx -> XCD job order instead of the ticket was no
-// better (profiles/r4h..r4k_staggered_rounds_ab.json).
-#ifndef VLP_PP_DESYNC
-#define VLP_PP_DESYNC 0
-#endif
-#ifndef VLP_PP_DESYNC_DIV   // split tiles per XCD run = CUs / VLP_PP_DESYNC_DIV
-#define VLP_PP_DESYNC_DIV 16
-#endif
-// 16-B global store / load with the sc1 bit: performed at the agent's coherence
-// point (visible to another XCD's L2 without a fence); the caller waits vmcnt
-__device__ __forceinline__ void st_sc1_x4(void* p, v4f v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ v4f ld_sc1_x4(const void* p) {
-  v4f r;
-  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(r) : "v"(p) : "memory");
-  return r;
-}
 // A loader's per-chunk byte offset, computed once per tile, made opaque to the
 // compiler: otherwise it re-associates offset + per-K-step delta back into the
 // pixel coordinates and recomputes (v_mul_lo_u32 + v_mad_u64_u32 per chunk and
@@ -229,10 +201,6 @@ __device__ __forceinline__ unsigned opaque_base(unsigned v) {
 #endif
   return v;
 }
-// epilogues whose launches may run staggered rounds in gemm_pp_kernel
-// (E::kDesync: 1 data-gradient epilogues, 2 forward; enabled by VLP_PP_DESYNC)
-template <class E, class = void> struct DesyncTrait { static constexpr int value = 0; };
-template <class E> struct DesyncTrait<E, std::void_t<decltype(E::kDesync)>> { static constexpr int value = E::kDesync; };
 // K-step order: a loader with kKPerm maps the logical K offset of a 64-deep
 // step to the physical one (kperm); the buffer-protocol kernels apply the SAME
 // map to both operands, so the product is unchanged up to fp32 summation order
@@ -1457,60 +1425,17 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int nwg = sh.tiles_m * sh.tiles_n;
-  const int ntot = sh.sk > 0 ? nwg + sh.sk : nwg * sh.nsplit;
+  const int ntot = nwg * sh.nsplit;
   const int bid = blockIdx.x;
   int g = bid;
   if (ntot >= 16) {
     const int xcd = bid & 7, idx = bid >> 3, q = ntot >> 3, rr = ntot & 7;
     g = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
   }
-  int split = g / nwg;
-  int wid = g - split * nwg;
-  int kb = split * sh.kchunk;
+  const int split = g / nwg;
+  const int wid = g - split * nwg;
+  const int kb = split * sh.kchunk;
   int ke = kb + sh.kchunk;
-  // staggered rounds (pp_desync): the first 2S jobs alternate "first K-half of
-  // split tile i" / "whole tile S+i", the middle is whole tiles and the last S
-  // are the second K-halves; the workgroups that started on a half stay half a
-  // tile out of phase with the others, so the memory-bound epilogues of the two
-  // cohorts alternate instead of every CU reaching its epilogue in one round
-  int part = -1, sidx = 0;
-  if (sh.sk > 0) {
-    // jobs are handed out by an arrival ticket, so the order above is the order
-    // in which workgroups actually start (a fixed blockIdx -> XCD placement
-    // assumption measured 13-16 % slower even without the hand-over); the
-    // workgroup drawing the last ticket resets the counter for the next launch
-    unsigned* tk = reinterpret_cast<unsigned*>(smem);
-    if (threadIdx.x == 0) {
-      const unsigned t = __hip_atomic_fetch_add(sh.skc + sh.sk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t == (unsigned)ntot - 1u) __hip_atomic_store(sh.skc + sh.sk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      tk[0] = t;
-    }
-    __syncthreads();
-    const int t = __builtin_amdgcn_readfirstlane((int)tk[0]);
-    __syncthreads();
-    const int S = sh.sk;
-    const int hk = ((sh.K / BK) >> 1) * BK;
-    kb = 0;
-    ke = sh.K;
-    if (t < 2 * S) {
-      if (t & 1) {
-        wid = S + (t >> 1);
-      } else {
-        wid = t >> 1;
-        part = 0;
-        sidx = t >> 1;
-        ke = hk;
-      }
-    } else if (t < ntot - S) {
-      wid = t;
-    } else {
-      wid = t - (ntot - S);
-      part = 1;
-      sidx = wid;
-      kb = hk;
-    }
-    split = 0;
-  }
   const int tm = wid / sh.tiles_n, tn = wid - tm * sh.tiles_n;
   const int row0 = tm * BM, col0 = tn * BN;
   if (ke > sh.K) ke = sh.K;
@@ -1673,86 +1598,12 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
   if (grp == 0) run(std::integral_constant<int, 0>{});
   else run(std::integral_constant<int, 1>{});
   __syncthreads();   // ring drained (incl. the null-resource tail fetches) before LDS is reused
-  if constexpr ((DesyncTrait<EP>::value & VLP_PP_DESYNC) != 0) {
-    if (part >= 0) {
-      // each K-half stores its accumulators, then counts its arrival; the second
-      // to arrive adds the other half and runs the epilogue (a + b == b + a in
-      // fp32: the result does not depend on which). The halves may sit on
-      // different XCDs (separate L2s): the accumulators move by 16-B stores and
-      // loads with the sc1 (agent-coherent) bit and the counter as a relaxed
-      // agent-scope atomic -- no L2 write-back or invalidate, which a fence
-      // would issue (that version ran the launch 25-40 % slower) -- the stores
-      // retired (vmcnt 0) before the count
-      constexpr int NR = MB * NB;
-      v4f* mine = reinterpret_cast<v4f*>(sh.skp) + (size_t)(sidx * 2 + part) * NR * NT + threadIdx.x;
-#pragma unroll
-      for (int a = 0; a < MB; ++a)
-#pragma unroll
-        for (int b = 0; b < NB; ++b) st_sc1_x4(mine + (a * NB + b) * NT, acc[a][b]);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      unsigned* flag = reinterpret_cast<unsigned*>(smem);
-      if (threadIdx.x == 0)
-        flag[0] = __hip_atomic_fetch_add(sh.skc + sidx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-      const unsigned prev = flag[0];
-      __syncthreads();
-      if (prev == 0) return;
-      const v4f* other = reinterpret_cast<const v4f*>(sh.skp) + (size_t)(sidx * 2 + (1 - part)) * NR * NT + threadIdx.x;
-      v4f o[MB][NB];
-#pragma unroll
-      for (int a = 0; a < MB; ++a)
-#pragma unroll
-        for (int b = 0; b < NB; ++b) o[a][b] = ld_sc1_x4(other + (a * NB + b) * NT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int a = 0; a < MB; ++a)
-#pragma unroll
-        for (int b = 0; b < NB; ++b) acc[a][b] += o[a][b];
-      if (threadIdx.x == 0) __hip_atomic_store(sh.skc + sidx, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
   if constexpr (SplitTrait<EP>::value) {
     ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep.at_split(split), acc, row0, col0, wid, wm, wn, smem);
   } else {
     ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep, acc, row0, col0, wid, wm, wn, smem);
   }
 }
-
-// ---------------- staggered rounds for gemm_pp_kernel ----------------
-// per (device, stream) workspace: 2 fp32 accumulator images per split tile, one
-// arrival counter each and the job ticket (all return to 0 by the end of a launch)
-struct PpDesyncWs { float* part; unsigned* cnt; size_t part_bytes; int nslot; };
-inline PpDesyncWs pp_desync_ws(hipStream_t st, size_t part_bytes, int nslot) {
-  static std::mutex mu;
-  static std::vector<std::pair<std::pair<int, hipStream_t>, PpDesyncWs>> tab;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  std::lock_guard<std::mutex> lk(mu);
-  for (auto& e : tab)
-    if (e.first.first == dev && e.first.second == st) {
-      if (e.second.part_bytes >= part_bytes && e.second.nslot >= nslot) return e.second;
-      (void)hipStreamSynchronize(st);
-      (void)hipFree(e.second.part);
-      (void)hipFree(e.second.cnt);
-      e.second = PpDesyncWs{nullptr, nullptr, 0, 0};
-      if (hipMalloc(&e.second.part, part_bytes * 2 * nslot) != hipSuccess ||
-          hipMalloc(&e.second.cnt, sizeof(unsigned) * nslot) != hipSuccess ||
-          hipMemset(e.second.cnt, 0, sizeof(unsigned) * nslot) != hipSuccess)
-        return PpDesyncWs{nullptr, nullptr, 0, 0};
-      e.second.part_bytes = part_bytes;
-      e.second.nslot = nslot;
-      return e.second;
-    }
-  PpDesyncWs w{nullptr, nullptr, part_bytes, nslot};
-  if (hipMalloc(&w.part, part_bytes * 2 * nslot) != hipSuccess ||
-      hipMalloc(&w.cnt, sizeof(unsigned) * nslot) != hipSuccess ||
-      hipMemset(w.cnt, 0, sizeof(unsigned) * nslot) != hipSuccess)
-    return PpDesyncWs{nullptr, nullptr, 0, 0};
-  tab.push_back({{dev, st}, w});
-  return w;
-}
-
 
 // Split-K count for a reduction of K over `tiles` output tiles, given the
 // number of workgroups the chip holds at once (`slots`).  Workgroups of one
@@ -1793,20 +1644,45 @@ inline int balanced_ksplit(int tiles, int K, int slots, int min_k) {
   }
   return best;
 }
-// bit of the current device (per-device caches of per-function attributes)
-inline unsigned dev_bit() {
+// current device index (per-device caches of per-function launch state)
+inline int cur_dev() {
   int d = 0;
   (void)hipGetDevice(&d);
-  return 1u << (d & 31);
+  return d & 31;
 }
 inline int device_cus() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  static int n[32] = {};
+  const int d = cur_dev();
+  if (!n[d]) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || v <= 0) v = 256;
+    n[d] = v;
   }
-  return n;
+  return n[d];
+}
+// Launch state of one kernel instantiation, per device: the dynamic-LDS limit is
+// raised once per device (its error returned, not dropped), and the resident
+// workgroups per CU are queried once per device (the split-K choice uses them)
+struct KernelDevState {
+  unsigned attr_set = 0;
+  int occ[32] = {};
+};
+inline int prepare_kernel(KernelDevState& s, const void* fn, int lds, int threads, int* occ) {
+  const int d = cur_dev();
+  if (lds > 65536 && !(s.attr_set & (1u << d))) {
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return (int)e;
+    s.attr_set |= 1u << d;
+  }
+  if (occ) {
+    if (!s.occ[d]) {
+      int o = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, fn, threads, lds) != hipSuccess || o <= 0) o = 1;
+      s.occ[d] = o;
+    }
+    *occ = s.occ[d];
+  }
+  return 0;
 }
 
 template <int BM, int BN, int WGM, int WGN, int S, class LA, class LB, class EP>
@@ -1821,18 +1697,13 @@ inline int launch_gemm_ms(int M, int N, int K, int ksplit, const LA& la, const L
   sh.M = M; sh.N = N; sh.K = K;
   sh.tiles_m = (M + BM - 1) / BM;
   sh.tiles_n = (N + BN - 1) / BN;
+  constexpr int lds = S * (BM + BN) * 128;
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  static KernelDevState kst;
   if (ksplit <= 0) {   // auto: fill whole rounds of resident workgroups
-    static int occ = 0;
-    if (!occ) {
-      constexpr int lds_b = S * (BM + BN) * 128;
-      if (lds_b > 65536)
-        (void)hipFuncSetAttribute((const void*)&gemm_ms_kernel<BM, BN, WGM, WGN, S, LA, LB, EP>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_b);
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-              &occ, (const void*)&gemm_ms_kernel<BM, BN, WGM, WGN, S, LA, LB, EP>, WGM * WGN * 64,
-              lds_b) != hipSuccess || occ <= 0)
-        occ = 1;
-    }
+    int occ = 1;
+    const int e = prepare_kernel(kst, (const void*)&gemm_ms_kernel<BM, BN, WGM, WGN, S, LA, LB, EP>, lds, WGM * WGN * 64, &occ);
+    if (e) return e;
     ksplit = balanced_ksplit(sh.tiles_m * sh.tiles_n, K, occ * device_cus(), -ksplit > 0 ? -ksplit : 2048);
   }
   if (ksplit < 1) ksplit = 1;
@@ -1845,15 +1716,9 @@ inline int launch_gemm_ms(int M, int N, int K, int ksplit, const LA& la, const L
   sh.xsplit = (ksplit >= 8 && ksplit % 8 == 0) ? 1 : 0;
   dim3 grid = sh.xsplit ? dim3(sh.tiles_m * sh.tiles_n * ksplit, 1, 1)
                         : dim3(sh.tiles_m * sh.tiles_n, ksplit, 1);
-  constexpr int lds = S * (BM + BN) * 128;
-  static_assert(lds <= 160 * 1024, "LDS budget");
-  if constexpr (lds > 65536) {
-    static unsigned attr_set = 0;   // one bit per device: the attribute is per device
-    if (!(attr_set & dev_bit())) {
-      (void)hipFuncSetAttribute((const void*)&gemm_ms_kernel<BM, BN, WGM, WGN, S, LA, LB, EP>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      attr_set |= dev_bit();
-    }
+  {
+    const int e = prepare_kernel(kst, (const void*)&gemm_ms_kernel<BM, BN, WGM, WGN, S, LA, LB, EP>, lds, 0, nullptr);
+    if (e) return e;
   }
   hipLaunchKernelGGL((gemm_ms_kernel<BM, BN, WGM, WGN, S, LA, LB, EP>), grid, dim3(WGM * WGN * 64), lds,
                      stream, sh, la, lb, ep);
@@ -1873,18 +1738,13 @@ inline int launch_gemm_bk(int M, int N, int K, int ksplit, const LA& la, const L
   sh.M = M; sh.N = N; sh.K = K;
   sh.tiles_m = (M + BM - 1) / BM;
   sh.tiles_n = (N + BN - 1) / BN;
+  constexpr int lds = S * (BM + BN) * 128;
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  static KernelDevState kst;
   if (ksplit <= 0) {   // auto: fill whole rounds of resident workgroups
-    static int occ = 0;
-    if (!occ) {
-      constexpr int lds_b = S * (BM + BN) * 128;
-      if (lds_b > 65536)
-        (void)hipFuncSetAttribute((const void*)&gemm_bk_kernel<BM, BN, WGM, WGN, LA, LB, EP>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_b);
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-              &occ, (const void*)&gemm_bk_kernel<BM, BN, WGM, WGN, LA, LB, EP>, WGM * WGN * 64,
-              lds_b) != hipSuccess || occ <= 0)
-        occ = 1;
-    }
+    int occ = 1;
+    const int e = prepare_kernel(kst, (const void*)&gemm_bk_kernel<BM, BN, WGM, WGN, LA, LB, EP>, lds, WGM * WGN * 64, &occ);
+    if (e) return e;
     ksplit = balanced_ksplit(sh.tiles_m * sh.tiles_n, K, occ * device_cus(), -ksplit > 0 ? -ksplit : 2048);
   }
   if (ksplit < 1) ksplit = 1;
@@ -1898,15 +1758,9 @@ inline int launch_gemm_bk(int M, int N, int K, int ksplit, const LA& la, const L
   sh.nsplit = ksplit;
   last_ksplit() = ksplit;
   dim3 grid(sh.tiles_m * sh.tiles_n * ksplit, 1, 1);
-  constexpr int lds = S * (BM + BN) * 128;
-  static_assert(lds <= 160 * 1024, "LDS budget");
-  if constexpr (lds > 65536) {
-    static unsigned attr_set = 0;   // one bit per device: the attribute is per device
-    if (!(attr_set & dev_bit())) {
-      (void)hipFuncSetAttribute((const void*)&gemm_bk_kernel<BM, BN, WGM, WGN, LA, LB, EP>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      attr_set |= dev_bit();
-    }
+  {
+    const int e = prepare_kernel(kst, (const void*)&gemm_bk_kernel<BM, BN, WGM, WGN, LA, LB, EP>, lds, 0, nullptr);
+    if (e) return e;
   }
   hipLaunchKernelGGL((gemm_bk_kernel<BM, BN, WGM, WGN, LA, LB, EP>), grid, dim3(WGM * WGN * 64), lds,
                      stream, sh, la, lb, ep);
@@ -1926,18 +1780,13 @@ inline int launch_gemm_big(int M, int N, int K, int ksplit, const LA& la, const 
   sh.M = M; sh.N = N; sh.K = K;
   sh.tiles_m = (M + BM - 1) / BM;
   sh.tiles_n = (N + BN - 1) / BN;
+  constexpr int lds = big_lds_bytes<BM, BN, EP>();
+  static_assert(lds <= 160 * 1024, "LDS budget");
+  static KernelDevState kst;
   if (ksplit <= 0) {   // auto: fill whole rounds of resident workgroups
-    static int occ = 0;
-    if (!occ) {
-      constexpr int lds_b = big_lds_bytes<BM, BN, EP>();
-      if (lds_b > 65536)
-        (void)hipFuncSetAttribute((const void*)&gemm_big_kernel<BM, BN, WGM, WGN, LA, LB, EP, WPE>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds_b);
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-              &occ, (const void*)&gemm_big_kernel<BM, BN, WGM, WGN, LA, LB, EP, WPE>, WGM * WGN * 64,
-              lds_b) != hipSuccess || occ <= 0)
-        occ = 1;
-    }
+    int occ = 1;
+    const int e = prepare_kernel(kst, (const void*)&gemm_big_kernel<BM, BN, WGM, WGN, LA, LB, EP, WPE>, lds, WGM * WGN * 64, &occ);
+    if (e) return e;
     ksplit = balanced_ksplit(sh.tiles_m * sh.tiles_n, K, occ * device_cus(), -ksplit > 0 ? -ksplit : 2048);
   }
   if (ksplit < 1) ksplit = 1;
@@ -1951,15 +1800,9 @@ inline int launch_gemm_big(int M, int N, int K, int ksplit, const LA& la, const 
   sh.nsplit = ksplit;
   last_ksplit() = ksplit;
   dim3 grid(sh.tiles_m * sh.tiles_n * ksplit, 1, 1);
-  constexpr int lds = big_lds_bytes<BM, BN, EP>();
-  static_assert(lds <= 160 * 1024, "LDS budget");
-  if constexpr (lds > 65536) {
-    static unsigned attr_set = 0;   // one bit per device: the attribute is per device
-    if (!(attr_set & dev_bit())) {
-      (void)hipFuncSetAttribute((const void*)&gemm_big_kernel<BM, BN, WGM, WGN, LA, LB, EP, WPE>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      attr_set |= dev_bit();
-    }
+  {
+    const int e = prepare_kernel(kst, (const void*)&gemm_big_kernel<BM, BN, WGM, WGN, LA, LB, EP, WPE>, lds, 0, nullptr);
+    if (e) return e;
   }
   hipLaunchKernelGGL((gemm_big_kernel<BM, BN, WGM, WGN, LA, LB, EP, WPE>), grid, dim3(WGM * WGN * 64), lds,
                      stream, sh, la, lb, ep);
@@ -1979,17 +1822,11 @@ inline int launch_gemm_pp(int M, int N, int K, int ksplit, const LA& la, const L
   sh.tiles_n = (N + BN - 1) / BN;
   constexpr int lds = big_lds_bytes<BM, BN, EP>() + (XformTrait<LA>::value ? 4096 : 0);
   static_assert(lds <= 160 * 1024, "LDS budget");
-  if (ksplit <= 0) {   // auto: fill whole rounds of resident workgroups (one per CU)
-    static int occ = 0;
-    if (!occ) {
-      if (lds > 65536)
-        (void)hipFuncSetAttribute((const void*)&gemm_pp_kernel<BM, BN, WGM, WGN, LA, LB, EP>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-              &occ, (const void*)&gemm_pp_kernel<BM, BN, WGM, WGN, LA, LB, EP>, WGM * WGN * 64, lds) != hipSuccess ||
-          occ <= 0)
-        occ = 1;
-    }
+  static KernelDevState kst;
+  if (ksplit <= 0) {   // auto: fill whole rounds of resident workgroups
+    int occ = 1;
+    const int e = prepare_kernel(kst, (const void*)&gemm_pp_kernel<BM, BN, WGM, WGN, LA, LB, EP>, lds, WGM * WGN * 64, &occ);
+    if (e) return e;
     ksplit = balanced_ksplit(sh.tiles_m * sh.tiles_n, K, occ * device_cus(), -ksplit > 0 ? -ksplit : 2048);
   }
   if (ksplit < 1) ksplit = 1;
@@ -2002,28 +1839,9 @@ inline int launch_gemm_pp(int M, int N, int K, int ksplit, const LA& la, const L
   sh.nsplit = ksplit;
   last_ksplit() = ksplit;
   dim3 grid(sh.tiles_m * sh.tiles_n * ksplit, 1, 1);
-  if constexpr ((DesyncTrait<EP>::value & VLP_PP_DESYNC) != 0 && !SplitTrait<EP>::value) {
-    // >= 2 rounds of one workgroup per CU and >= 2 K-steps per half: half of
-    // each XCD's CUs start on a K-half (pp_desync above)
-    const int cus = device_cus();
-    const int s = cus / VLP_PP_DESYNC_DIV;
-    if (ksplit == 1 && s > 0 && cus % 8 == 0 && sh.tiles_m * sh.tiles_n >= 2 * cus && K >= 4 * BK) {
-          const PpDesyncWs w = pp_desync_ws(stream, (size_t)BM * BN * 4, 8 * s + 1);   // + the ticket
-      if (w.part) {
-        sh.sk = 8 * s;
-        sh.skp = w.part;
-        sh.skc = w.cnt;
-        grid = dim3(sh.tiles_m * sh.tiles_n + 8 * s, 1, 1);
-      }
-    }
-  }
-  if constexpr (lds > 65536) {
-    static unsigned attr_set = 0;   // one bit per device: the attribute is per device
-    if (!(attr_set & dev_bit())) {
-      (void)hipFuncSetAttribute((const void*)&gemm_pp_kernel<BM, BN, WGM, WGN, LA, LB, EP>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      attr_set |= dev_bit();
-    }
+  {
+    const int e = prepare_kernel(kst, (const void*)&gemm_pp_kernel<BM, BN, WGM, WGN, LA, LB, EP>, lds, 0, nullptr);
+    if (e) return e;
   }
   hipLaunchKernelGGL((gemm_pp_kernel<BM, BN, WGM, WGN, LA, LB, EP>), grid, dim3(WGM * WGN * 64), lds, stream, sh,
                      la, lb, ep);
@@ -2182,13 +2000,10 @@ inline int launch_gemm(int M, int N, int K, int ksplit, const LA& la, const LB& 
   sh.kchunk = kc;
   dim3 grid(sh.tiles_m * sh.tiles_n, ksplit, 1);
   constexpr int lds = gemm_lds_bytes<T, BM, BN>();
-  if constexpr (lds > 65536) {
-    static unsigned attr_set = 0;   // one bit per device: the attribute is per device
-    if (!(attr_set & dev_bit())) {
-      (void)hipFuncSetAttribute((const void*)&gemm_kernel<T, BM, BN, WGM, LA, LB, EP>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      attr_set |= dev_bit();
-    }
+  static KernelDevState kst;
+  {
+    const int e = prepare_kernel(kst, (const void*)&gemm_kernel<T, BM, BN, WGM, LA, LB, EP>, lds, 0, nullptr);
+    if (e) return e;
   }
   hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WGM, LA, LB, EP>), grid, dim3(256), lds, stream, sh, la, lb, ep);
   return (int)hipGetLastError();

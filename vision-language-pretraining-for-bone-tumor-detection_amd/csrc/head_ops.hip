@@ -139,7 +139,7 @@ template <int NCH>
 __global__ void __launch_bounds__(256)
 clip_dq_kernel(int B, int N, int E, int offset, const float* __restrict__ img_all,
                const float* __restrict__ txt_all, const float* __restrict__ logit_scale,
-               float* __restrict__ ws) {
+               const float* __restrict__ role_w, float* __restrict__ ws) {
   constexpr int EP = NCH * 16 + 4;                       // LDS row stride (floats)
   __shared__ __attribute__((aligned(16))) float lds[4 * 32 * EP];
   __shared__ float red_ds[4];
@@ -155,7 +155,9 @@ clip_dq_kernel(int B, int N, int E, int offset, const float* __restrict__ img_al
   const bool qvalid = q0 + x < B;
   const float* ksrc = role == 0 ? txt_all : img_all;
   const float s = fminf(expf(logit_scale[0]), 100.f);
-  const float inv2n = 0.5f / (float)N;
+  // W = d loss / d logit with loss = sum_r role_w[r] * CE_r / 2 (role_w = {1, 1}: the
+  // reference's (image_loss + text_loss) / 2); W carries the weight into dq, dk and d s
+  const float inv2n = (role_w ? role_w[role] : 1.f) * 0.5f / (float)N;
   // this query's log-sum-exp from the 64-key partials (lane groups g stride them)
   float m = -INFINITY, sl = 0.f;
   if (qvalid) {
@@ -381,7 +383,7 @@ __global__ void l2norm_bwd_kernel(int R, int E, const float* __restrict__ y, con
 // symmetric CE over an explicit [B][B] logits matrix (API path: _compute_loss)
 // out[0] = loss, out[1] = image loss, out[2] = text loss; dlogits = d loss / d logits
 __global__ void ce_sym_kernel(int B, const float* __restrict__ logits, float* __restrict__ out,
-                              float* __restrict__ dlogits) {
+                              float* __restrict__ dlogits, const float* __restrict__ role_w) {
   // role 0: rows, role 1: columns; one wave per row/column
   int w = blockIdx.x * 4 + (threadIdx.x >> 6);
   int l = threadIdx.x & 63;
@@ -399,11 +401,12 @@ __global__ void ce_sym_kernel(int B, const float* __restrict__ logits, float* __
     atomicAdd(out + 1 + role, (lse - diag) / B);
     atomicAdd(out, 0.5f * (lse - diag) / B);
   }
-  if (dlogits) {
+  if (dlogits) {   // d (sum_r role_w[r] * CE_r / 2) / d logits
+    const float wr = (role_w ? role_w[role] : 1.f) * 0.5f / B;
     for (int j = l; j < B; j += 64) {
       size_t o = role ? (size_t)j * B + i : (size_t)i * B + j;
       float p = expf(logits[o] - lse);
-      atomicAdd(dlogits + o, 0.5f * (p - (i == j ? 1.f : 0.f)) / B);
+      atomicAdd(dlogits + o, wr * (p - (i == j ? 1.f : 0.f)));
     }
   }
 }
@@ -443,7 +446,8 @@ VLP_EXPORT int vlp_clip_loss_ws_floats(int B, int N, int E, long long* n) {
 VLP_EXPORT int vlp_clip_loss_fused(int B, int N, int E, int offset, const float* img_all,
                                    const float* txt_all, const float* logit_scale, float* g_img_all,
                                    float* g_txt_all, float* d_logit_scale, float* loss_parts,
-                                   float* lse_out, float* ws, long long ws_floats, void* stream) {
+                                   float* lse_out, const float* role_w, float* ws, long long ws_floats,
+                                   void* stream) {
   if (B < 1 || N < B || E < 4 || E > kMaxE || E % 4 || offset < 0 || offset + B > N)
     return (int)hipErrorInvalidValue;
   const ClipWs L = clip_ws_layout(B, N, E);
@@ -452,10 +456,12 @@ VLP_EXPORT int vlp_clip_loss_fused(int B, int N, int E, int offset, const float*
   const dim3 g12(2 * L.nqb * L.nkc);
   if (E <= 128) {
     hipLaunchKernelGGL(clip_scores_kernel<8>, g12, dim3(256), 0, st, B, N, E, offset, img_all, txt_all, logit_scale, ws);
-    hipLaunchKernelGGL(clip_dq_kernel<8>, g12, dim3(256), 0, st, B, N, E, offset, img_all, txt_all, logit_scale, ws);
+    hipLaunchKernelGGL(clip_dq_kernel<8>, g12, dim3(256), 0, st, B, N, E, offset, img_all, txt_all, logit_scale,
+                       role_w, ws);
   } else {
     hipLaunchKernelGGL(clip_scores_kernel<16>, g12, dim3(256), 0, st, B, N, E, offset, img_all, txt_all, logit_scale, ws);
-    hipLaunchKernelGGL(clip_dq_kernel<16>, g12, dim3(256), 0, st, B, N, E, offset, img_all, txt_all, logit_scale, ws);
+    hipLaunchKernelGGL(clip_dq_kernel<16>, g12, dim3(256), 0, st, B, N, E, offset, img_all, txt_all, logit_scale,
+                       role_w, ws);
   }
   const int ncg = (E + 16 * kETW - 1) / (16 * kETW);
   hipLaunchKernelGGL(clip_dk_kernel, dim3(2 * (L.Np / kKB) * ncg), dim3(256), 0, st, B, N, E, offset, img_all,
@@ -495,9 +501,10 @@ VLP_EXPORT int vlp_clip_loss_finish(const float* parts, int N, float* out, void*
   return (int)hipGetLastError();
 }
 
-VLP_EXPORT int vlp_ce_sym(int B, const float* logits, float* out, float* dlogits, void* stream) {
+VLP_EXPORT int vlp_ce_sym(int B, const float* logits, float* out, float* dlogits, const float* role_w,
+                          void* stream) {
   hipLaunchKernelGGL(ce_sym_kernel, dim3((2 * B + 3) / 4), dim3(256), 0, (hipStream_t)stream, B, logits,
-                     out, dlogits);
+                     out, dlogits, role_w);
   return (int)hipGetLastError();
 }
 

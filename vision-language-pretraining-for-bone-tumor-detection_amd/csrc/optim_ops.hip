@@ -269,4 +269,4 @@ VLP_EXPORT int vlp_unpack_stem_grad(const float* ws, float* g, void* stream) {
 
 // 2: vlp_clip_loss_fused takes (ws, ws_floats) and writes (not adds) its outputs (r3);
 //    MFMA head kernels, E <= 256 with E % 4 == 0 (r4)
-VLP_EXPORT int vlp_abi_version() { return 2; }
+VLP_EXPORT int vlp_abi_version() { return 3; }

@@ -52,7 +52,7 @@ supported_models = ["vit_base_patch16_224", "vit_large_patch16_224", "resnet50",
 class ResNet34Classifier(ResNet34Tower):
     """timm resnet34(num_classes) on the HIP tower: forward_features / forward_head / forward."""
 
-    def __init__(self, num_classes: int = 10, compute_dtype: str = "bf16", device=None):
+    def __init__(self, num_classes: int = 10, compute_dtype: str = "fp32", device=None):
         super().__init__(drop_rate=0.0, compute_dtype=compute_dtype, device=device)
         self.fc = nn.Linear(512, num_classes, device=device)
 
@@ -81,7 +81,7 @@ class FusionModule(_Base):
         coral_lambda: float = 0.0,
         pretrained_vlp_module: str = None,
         vision_encoder_lr: float = None,
-        compute_dtype: str = "bf16",
+        compute_dtype: str = "fp32",
         device=None,
         **kwargs,
     ):

@@ -57,7 +57,7 @@ supported_models = ["vit_base_patch16_224", "vit_large_patch16_224", "resnet50",
 class NestClassifier(NestTower):
     """timm nest_small(num_classes) on the HIP tower: forward_features / forward_head / forward."""
 
-    def __init__(self, num_classes: int = 1, img_size: int = 224, compute_dtype: str = "bf16", device=None,
+    def __init__(self, num_classes: int = 1, img_size: int = 224, compute_dtype: str = "fp32", device=None,
                  drop_path_rate: float = 0.5):
         super().__init__("nest_small", img_size=img_size, drop_path_rate=drop_path_rate,
                          compute_dtype=compute_dtype, device=device)
@@ -139,7 +139,7 @@ class OnlyImagingModule(_Base):
         label_weights: Tuple[float] = (1.0, 1.0),
         coral_lambda: float = 0.0,
         pretrained_vlp_module: str = None,
-        compute_dtype: str = "bf16",
+        compute_dtype: str = "fp32",
         image_size: int = 224,
         device=None,
         **kwargs,

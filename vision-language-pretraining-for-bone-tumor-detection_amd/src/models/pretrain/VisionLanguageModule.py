@@ -10,7 +10,8 @@ image_projection, text_projection, logit_scale).  All arithmetic runs in the
 HIP kernels of libvlp_hip.so (vlp_amd); there is no CPU fallback.
 
 Additions (keyword-only, defaults keep reference behaviour where possible):
-  compute_dtype  "bf16" (throughput mode, default) | "fp32" (parity mode)
+  compute_dtype  "fp32" (the reference's arithmetic, default) | "bf16" (throughput mode,
+                 the _mi355x experiments; src/train.py also derives it from trainer.precision)
   text_dropout   TinyBERT hidden/attention dropout (reference: 0.1 from the hub config)
   fused_optimizer  build vlp_amd.FusedAdamW when the configured optimizer is
                    torch.optim.AdamW (same hyper-parameters / param groups)
@@ -35,7 +36,7 @@ if _PKG not in sys.path:
     sys.path.insert(0, _PKG)
 
 from vlp_amd import ops  # noqa: E402
-from vlp_amd.clip_model import ClipHead, ClipStepFn, _project_normalize  # noqa: E402
+from vlp_amd.clip_model import ClipHead, ClipStepFn, _project_normalize, role_weights  # noqa: E402
 from vlp_amd.optim import FusedAdamW  # noqa: E402
 from vlp_amd.nest import NEST_CFGS, NestTower  # noqa: E402
 from vlp_amd.resnet34 import ResNet34Tower  # noqa: E402
@@ -88,7 +89,7 @@ class ImageEncoder(nn.Module):
     """:27-35 — `timm.create_model(model, pretrained=False, num_classes=0,
     global_pool="avg", **kwargs)`; here the MI355X ResNet34 tower."""
 
-    def __init__(self, model, compute_dtype="bf16", device=None, **kwargs):
+    def __init__(self, model, compute_dtype="fp32", device=None, **kwargs):
         super().__init__()
         if model == "resnet34":
             self.model = ResNet34Tower(drop_rate=kwargs.get("drop_rate", 0.0), compute_dtype=compute_dtype,
@@ -111,7 +112,7 @@ class ImageEncoder(nn.Module):
 class TextEncoder(nn.Module):
     """:38-60 — TinyBERT; returns the CLS token's last hidden state."""
 
-    def __init__(self, text_encoder_model, compute_dtype="bf16", device=None, dropout=0.1):
+    def __init__(self, text_encoder_model, compute_dtype="fp32", device=None, dropout=0.1):
         super().__init__()
         if text_encoder_model == "distilbert":
             raise NotImplementedError("TextEncoder: distilbert is outside the MI355X hot path (use tinybert)")
@@ -187,7 +188,8 @@ class _LogitsFn(torch.autograd.Function):
 
 
 class _SymCEFn(torch.autograd.Function):
-    """(CE(logits, arange) + CE(logits^T, arange)) / 2, image, text (:550-552)."""
+    """(CE(logits, arange) + CE(logits^T, arange)) / 2, image, text (:550-552).
+    All three outputs are differentiable, as the reference's autograd tensors are."""
 
     @staticmethod
     def forward(ctx, logits):
@@ -195,16 +197,23 @@ class _SymCEFn(torch.autograd.Function):
         out = torch.zeros(3, dtype=torch.float32, device=lg.device)
         dl = torch.zeros_like(lg)
         ops.ce_sym(lg, out, dl)
-        ctx.save_for_backward(dl)
+        ctx.save_for_backward(dl, lg)
+        ctx.set_materialize_grads(False)
         return out[0], out[1], out[2]
 
     @staticmethod
     def backward(ctx, gl, gi, gt):
-        (dl,) = ctx.saved_tensors
-        if gi is not None and gi.abs().sum() != 0 or gt is not None and gt.abs().sum() != 0:
-            raise NotImplementedError("gradients of the per-direction losses are not supported")
-        out = torch.empty_like(dl)
-        ops.scale(dl, gl.reshape(1).float().contiguous(), out)
+        dl, lg = ctx.saved_tensors
+        if gi is None and gt is None:
+            if gl is None:
+                return None
+            out = torch.empty_like(dl)
+            ops.scale(dl, gl.reshape(1).float().contiguous(), out)
+            return out
+        # gl*loss + gi*image_loss + gt*text_loss = sum_r (gl + 2 g_r) * CE_r / 2
+        w = role_weights(gl, gi, gt, lg.device)
+        out = torch.zeros_like(lg)
+        ops.ce_sym(lg, torch.zeros(3, dtype=torch.float32, device=lg.device), out, role_w=w)
         return out
 
 
@@ -239,7 +248,7 @@ class VisionLanguageModule(_Base):
         image_encoder_lr: float = None,
         projections_lr: float = None,
         image_encoder_droupout: float = 0.0,
-        compute_dtype: str = "bf16",
+        compute_dtype: str = "fp32",
         text_dropout: float = 0.1,
         fused_optimizer: bool = True,
         device=None,

@@ -88,6 +88,39 @@ def instantiate_loggers(lg_cfg) -> List[Any]:
     return out
 
 
+_PRECISION_DTYPE = {None: "fp32", "32": "fp32", "32-true": "fp32", "bf16": "bf16", "bf16-mixed": "bf16",
+                    "bf16-true": "bf16"}
+
+
+def compute_dtype_for(precision) -> str:
+    """HIP compute dtype for a Lightning `trainer.precision`.  The reference sets no
+    precision (configs/trainer/default.yaml), i.e. Lightning's fp32: its experiments
+    keep fp32 arithmetic unless they opt in (the _mi355x experiments name
+    model.compute_dtype: bf16).  The HIP towers have no fp16 path."""
+    key = None if precision is None else str(precision)
+    if key not in _PRECISION_DTYPE:
+        raise ValueError(f"trainer.precision={precision!r}: the MI355X build computes in fp32 or bf16 "
+                         f"(use 32-true or bf16-mixed)")
+    return _PRECISION_DTYPE[key]
+
+
+def model_config(cfg: Dict[str, Any], label_weights) -> Dict[str, Any]:
+    """The model node train() instantiates for one fold (src/train.py:109-116)."""
+    model_cfg = dict(cfg["model"])
+    if not model_cfg.get("scheduler"):
+        model_cfg["scheduler"] = None
+    model_cfg["label_weights"] = label_weights
+    if "compute_dtype" not in model_cfg:   # the reference's arithmetic unless the run opts in
+        model_cfg["compute_dtype"] = compute_dtype_for((cfg.get("trainer") or {}).get("precision"))
+    if "FusionModule" in model_cfg["_target_"]:
+        model_cfg.pop("downstream_datamodule", None)
+    elif not isinstance(model_cfg.get("downstream_datamodule"), dict) or not model_cfg["downstream_datamodule"]:
+        # model/vision_language.yaml names the group option ("downstream"); the experiments
+        # interpolate the composed ${downstream_data} node, anything else means none
+        model_cfg["downstream_datamodule"] = None
+    return model_cfg
+
+
 def train(cfg: Dict[str, Any]) -> Tuple[Dict[str, Any], Dict[str, Any]]:
     if cfg.get("k_fold_cross_validation", False):
         log.info("Train: Doing k-fold cross validation.")
@@ -99,16 +132,7 @@ def train(cfg: Dict[str, Any]) -> Tuple[Dict[str, Any], Dict[str, Any]]:
     all_fold_metrics: List[Dict[str, Any]] = []
     objects: Dict[str, Any] = {"cfg": cfg, "datamodule": datamodule}
     for i, (fold_dm, label_weights) in enumerate(datamodule.get_cv_splits()):
-        model_cfg = dict(cfg["model"])
-        if not model_cfg.get("scheduler"):
-            model_cfg["scheduler"] = None
-        model_cfg["label_weights"] = label_weights
-        if "FusionModule" in model_cfg["_target_"]:
-            model_cfg.pop("downstream_datamodule", None)
-        elif not isinstance(model_cfg.get("downstream_datamodule"), dict) or not model_cfg["downstream_datamodule"]:
-            # model/vision_language.yaml names the group option ("downstream"); the experiments
-            # interpolate the composed ${downstream_data} node, anything else means none
-            model_cfg["downstream_datamodule"] = None
+        model_cfg = model_config(cfg, label_weights)
         log.info("Train: Instantiating model <%s>", model_cfg["_target_"])
         model = instantiate(model_cfg)
         callbacks = instantiate_callbacks(cfg.get("callbacks"))

@@ -137,10 +137,12 @@ def compose(config_name: str = "train", overrides: Optional[List[str]] = None,
         k, _, v = o.partition("=")
         if not _:
             raise ValueError(f"override {o!r} is not key=value")
-        if "." not in k and (k in choices or os.path.isdir(os.path.join(config_dir, k))):
+        add = len(k) - len(k.lstrip("+"))   # Hydra: +key appends a new key, ++key adds or sets
+        k = k.lstrip("+")
+        if add == 0 and "." not in k and (k in choices or os.path.isdir(os.path.join(config_dir, k))):
             cli_choice[k] = v
         else:
-            plain.append((k, v))
+            plain.append((k, v, add))
     choices.update(cli_choice)
     if choices.get("experiment") not in (None, "null"):
         exp = _load(_group_file(config_dir, "experiment", choices["experiment"]))
@@ -172,7 +174,14 @@ def compose(config_name: str = "train", overrides: Optional[List[str]] = None,
                 merge(cfg.setdefault(pkg, {}), node)
             else:
                 cfg[pkg] = {} if node is None else node
-    for k, v in plain:
+    for k, v, add in plain:
+        if add == 1:
+            try:
+                _get_path(cfg, k)
+            except KeyError:
+                pass
+            else:
+                raise ValueError(f"override +{k}: the key already exists (use ++{k}= or {k}=)")
         _set_path(cfg, k, yaml.safe_load(v))
     return resolve(cfg)
 

@@ -22,7 +22,7 @@ LIB_PATH = os.environ.get("VLP_HIP_LIB", os.path.join(_HERE, "libvlp_hip.so"))
 HEADER_PATH = os.path.join(_REPO, "include", "vlp_hip.h")
 
 F32, BF16 = 0, 1
-ABI_VERSION = 2     # vlp_abi_version() of the library this binding was written against
+ABI_VERSION = 3     # vlp_abi_version() of the library this binding was written against
 
 _CTYPE = {
     "int": ctypes.c_int,

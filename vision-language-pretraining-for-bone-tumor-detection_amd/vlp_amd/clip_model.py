@@ -27,10 +27,19 @@ from . import ops
 from .arena import ArenaModule
 
 
+# the fused loss kernels (csrc/head_ops.hip) keep a query's embedding in registers
+# and a 32-key slab in LDS: 4 <= E <= 256, E % 4 == 0 (the reference configs use
+# 32 and 128, configs/experiment/pretrain/*.yaml)
+MAX_EMBEDDING_DIM = 256
+
+
 class ClipHead(ArenaModule):
     def __init__(self, image_dim=512, text_dim=312, embedding_dim=256, compute_dtype="bf16",
                  device=None):
         super().__init__()
+        if embedding_dim % 4 or not 4 <= embedding_dim <= MAX_EMBEDDING_DIM:
+            raise ValueError(f"embedding_dim={embedding_dim}: the HIP contrastive head supports multiples of 4 "
+                             f"up to {MAX_EMBEDDING_DIM} (vlp_clip_loss_fused)")
         self.image_dim, self.text_dim, self.embedding_dim = image_dim, text_dim, embedding_dim
         self.compute_dtype = compute_dtype
         self._init_arena([("image_projection", (image_dim, embedding_dim)),
@@ -109,6 +118,17 @@ def _text_stream(dev):
     return s
 
 
+def role_weights(gl, gi, gt, device):
+    """Per-direction weights w of sum_r w_r * CE_r / 2 whose gradient is that of
+    gl*loss + gi*image_loss + gt*text_loss (loss = (image_loss + text_loss) / 2,
+    reference :550-552): w_r = gl + 2 g_r (None = 0).  A device tensor [2]."""
+    z = torch.zeros((), dtype=torch.float32, device=device)
+    a = gl.reshape(()).float() if gl is not None else z
+    wi = a + 2 * gi.reshape(()).float() if gi is not None else a
+    wt = a + 2 * gt.reshape(()).float() if gt is not None else a
+    return torch.stack([wi, wt]).contiguous()
+
+
 class ClipStepFn(torch.autograd.Function):
     """loss, image_loss, text_loss, img_emb, txt_emb = f(batch; all parameters)."""
 
@@ -153,8 +173,9 @@ class ClipStepFn(torch.autograd.Function):
         ops.clip_loss_finish(small[0:2], N, out)
         ctx.model = model
         ctx.state = (sv_img, sv_txt, wT, feat_img, h_last, ie, inorm, te, tnorm, g_img_all, g_txt_all,
-                     small, B, Tn, D, E)
+                     small, B, Tn, D, E, (ie_all, te_all, N, rank))
         ctx.mark_non_differentiable(ie, te)
+        ctx.set_materialize_grads(False)   # an unused image_loss / text_loss costs nothing
         return out[0], out[1], out[2], ie, te
 
     @staticmethod
@@ -162,13 +183,25 @@ class ClipStepFn(torch.autograd.Function):
         model = ctx.model
         img_t, txt_t, head = model.image_tower, model.text_tower, model.head
         (sv_img, sv_txt, wT, feat_img, h_last, ie, inorm, te, tnorm, g_img_all, g_txt_all, small,
-         B, Tn, D, E) = ctx.state
+         B, Tn, D, E, (ie_all, te_all, N, rank)) = ctx.state
         ctx.state = None
         for t in (head, img_t, txt_t):
             t.begin_backward()
+        if dli is None and dlt is None:
+            # the training step's loss alone: the forward's fused kernel already
+            # formed d loss / d embeddings, scaled by dloss below
+            gs = (dloss.reshape(1).float().contiguous() if dloss is not None
+                  else torch.zeros(1, dtype=torch.float32, device=ie.device))
+        else:
+            # gradients of image_loss / text_loss (reference :550-552 returns them as
+            # autograd tensors): rerun the head with per-direction weights
+            w = role_weights(dloss, dli, dlt, ie.device)
+            scratch = torch.zeros(2, dtype=torch.float32, device=ie.device)
+            ops.clip_loss_fused(B, N, E, rank * B, ie_all, te_all, head.arena.view("logit_scale"), g_img_all,
+                                g_txt_all, small[2:3], scratch, role_w=w)
+            gs = torch.ones(1, dtype=torch.float32, device=ie.device)
         g_img = vdist.reduce_scatter_rows(g_img_all)
         g_txt = vdist.reduce_scatter_rows(g_txt_all)
-        gs = dloss.reshape(1).float().contiguous()
         head.arena.grad.zero_()
         ops.scale(small[2:3], gs, head.arena.gview("logit_scale"))
         Di = head.image_dim

@@ -184,14 +184,14 @@ def conv_dgrad_relu2(dy, wt, H, W, C, KH, KW, S, P, relu_mask, y, mean, invstd, 
     return g
 
 
-def conv_wgrad(dy, x, KH, KW, S, P, dw_ws, in_scale=None, in_shift=None, dyT=None):
+def conv_wgrad(dy, x, KH, KW, S, P, dw_ws, in_scale=None, in_shift=None):
     N, H, W, C = x.shape
     Co = dy.shape[-1]
     Ho, Wo = dy.shape[1], dy.shape[2]
     tk = ktimer.begin(f"conv_wgrad[{'xf' if in_scale is not None else 'raw'}]{_tile_wgrad(Co)}",
                       2.0 * N * Ho * Wo * Co * C * KH * KW)
     lib().vlp_conv_wgrad(dcode(dy), ptr(dy), ptr(x), ptr(dw_ws), N, H, W, C, Co, KH, KW, S, P,
-                         ptr(in_scale), ptr(in_shift), ptr(dyT), _s())
+                         ptr(in_scale), ptr(in_shift), _s())
     ktimer.end(tk)
     return dw_ws
 
@@ -346,9 +346,9 @@ def stem_fwd(xp, wp, N, H, W, y, stat_sum, stat_sumsq, stat_rep=1):
     ktimer.end(tk)
 
 
-def stem_wgrad(dy, xp, N, H, W, dw_ws, dyT=None):
+def stem_wgrad(dy, xp, N, H, W, dw_ws):
     tk = ktimer.begin("stem_wgrad", 2.0 * dy.numel() * 147)
-    lib().vlp_stem_wgrad(dcode(dy), ptr(dy), ptr(xp), ptr(dw_ws), N, H, W, ptr(dyT), _s())
+    lib().vlp_stem_wgrad(dcode(dy), ptr(dy), ptr(xp), ptr(dw_ws), N, H, W, _s())
     ktimer.end(tk)
 
 
@@ -396,14 +396,12 @@ def bn_bwd_reduce(M, C, dout, dbc, HW, mask, ya, mean_a, istd_a, yb, mean_b, ist
                             ptr(sum_ga), ptr(sum_gb), int(stat_rep), _s())
 
 
-def bn_bwd_apply(M, C, dout, dbc, HW, mask, A, B, g_out, dtype_ref, dyT_a=None, dyT_b=None):
-    """A/B = (y, mean, istd, gamma, sum_g, sum_gx, dy_out) or None.  dyT_a/dyT_b:
-    optional [C][M] transposed copies of the dy outputs (bf16)."""
+def bn_bwd_apply(M, C, dout, dbc, HW, mask, A, B, g_out, dtype_ref):
+    """A/B = (y, mean, istd, gamma, sum_g, sum_gx, dy_out) or None."""
     a = A if A is not None else (None,) * 7
     b = B if B is not None else (None,) * 7
     lib().vlp_bn_bwd_apply(dcode(dtype_ref), M, C, ptr(dout), ptr(dbc), HW, ptr(mask),
-                           *[ptr(t) for t in a], *[ptr(t) for t in b], ptr(g_out), ptr(dyT_a),
-                           ptr(dyT_b), _s())
+                           *[ptr(t) for t in a], *[ptr(t) for t in b], ptr(g_out), _s())
 
 
 def bn_param_grad(sum_g, sum_gx, dgamma, dbeta):
@@ -546,7 +544,7 @@ def clip_loss_finish(parts, N, out):
 
 
 def clip_loss_fused(B, N, E, offset, img_all, txt_all, logit_scale, g_img_all, g_txt_all, d_ls,
-                    loss_parts, lse_out=None):
+                    loss_parts, lse_out=None, role_w=None):
     """Global-batch symmetric InfoNCE + gradients (three launches, split over key
     chunks; the scratch is a per-(device, stream) cached workspace)."""
     import ctypes
@@ -555,11 +553,11 @@ def clip_loss_fused(B, N, E, offset, img_all, txt_all, logit_scale, g_img_all, g
     ws = _stream_ws("clip", img_all.device, n.value)
     lib().vlp_clip_loss_fused(B, N, E, offset, ptr(img_all), ptr(txt_all), ptr(logit_scale),
                               ptr(g_img_all), ptr(g_txt_all), ptr(d_ls), ptr(loss_parts),
-                              ptr(lse_out), ptr(ws), ws.numel(), _s())
+                              ptr(lse_out), ptr(role_w), ptr(ws), ws.numel(), _s())
 
 
-def ce_sym(logits, out, dlogits=None):
-    lib().vlp_ce_sym(logits.shape[0], ptr(logits), ptr(out), ptr(dlogits), _s())
+def ce_sym(logits, out, dlogits=None, role_w=None):
+    lib().vlp_ce_sym(logits.shape[0], ptr(logits), ptr(out), ptr(dlogits), ptr(role_w), _s())
 
 
 def matmul(A, B, C, M, N, K, lda, a_kc, ldb, b_kc, ldc, alpha=1.0, accumulate=False, dtype_ref=None):

@@ -38,7 +38,6 @@ LAYERS = (3, 4, 6, 3)
 WIDTHS = (64, 128, 256, 512)
 BN_EPS = 1e-5
 BN_MOMENTUM = 0.1
-_USE_DYT = os.environ.get("VLP_WGRAD_DYT", "0") != "0"
 # weight gradients on a side stream: they are off the data-gradient chain, so
 # the MFMA-bound wgrad GEMMs overlap the HBM-bound BN / elementwise passes and
 # the data-gradient epilogue bursts (r2 driver: +2.4 % pairs/s).  Each side-
@@ -47,7 +46,7 @@ _USE_DYT = os.environ.get("VLP_WGRAD_DYT", "0") != "0"
 # split-K workspace (ops.wgrad_ws), so the main-stream stem weight gradient
 # never shares slabs with the side stream's.
 _USE_WG_STREAM = True
-_WG_STREAMS = {}   # measured: the extra transposed write costs more than it saves
+_WG_STREAMS = {}
 STAT_REP = 64   # replicas of per-channel fp64 sums (see vlp_stat_reduce)
 # single-channel stem for the uint8 upload (VLP_STEM1=0: always the 3-channel NHWC4 path)
 _USE_STEM1 = os.environ.get("VLP_STEM1", "1") != "0"
@@ -470,13 +469,58 @@ class ResNet34Tower(ArenaModule):
         hi = max(o + n for o, n in spans)
         cb(lo, hi - lo)
 
-    def _run_backward(self, saved, dfeat, ws, T, dev, on_stage_done=None):
+    # ---------------- block ranges (tests/test_gpu_blocks.py) ----------------
+    def run_block_range_forward(self, x: torch.Tensor, lo: int, hi: int, training: bool = True):
+        """Forward of BasicBlocks [lo, hi) on a given NHWC input in the compute
+        dtype (the output of a ReLU, as every block input is).  The same kernels
+        and fusions the whole tower picks at these shapes run; returns (out,
+        saved) for run_block_range_backward."""
+        ws = self.pack_weights()
+        T = self.tdtype
+        dev = self.arena.data.device
+        if x.dtype != T or x.dim() != 4 or x.shape[-1] != self._convs[self._blocks[lo][0] + ".conv1"].C:
+            raise ValueError(f"block range input must be NHWC {T} with the block's channel count, got "
+                             f"{tuple(x.shape)} {x.dtype}")
+        ws["fstat"].zero_()
+        bits = training and T == torch.bfloat16
+        xmask = None
+        if bits:   # sign bits of the block input, as maxpool_fwd / bn_add_relu write them
+            xmask = torch.empty(x.numel() // 8, dtype=torch.uint8, device=dev)
+            C = x.shape[-1]
+            one = torch.ones(C, dtype=torch.float32, device=dev)
+            xr = torch.empty_like(x)
+            ops.bn_add_relu(x, one, torch.zeros_like(one), None, None, None, xr, relu_mask=xmask)
+        blocks = [None] * lo
+        xcur = x
+        for pre, has_ds in self._blocks[lo:hi]:
+            blk, xcur, xmask = self._block_fwd(ws, T, dev, pre, has_ds, xcur, xmask, training, bits)
+            blocks.append(blk)
+        return xcur, {"blocks": blocks, "range": (lo, hi), "training": training}
+
+    def run_block_range_backward(self, saved, dout: torch.Tensor):
+        """Backward of run_block_range_forward for the gradient `dout` of the
+        range's output.  Returns the gradient of its input; the parameter
+        gradients of blocks [lo, hi) are written into the grad arena."""
+        ws = self._workspace()
+        dev = self.arena.data.device
+        self._sw = _side_stream(dev) if (_USE_WG_STREAM and dev.type == "cuda") else None
+        try:
+            lo, hi = saved["range"]
+            return self._run_backward(saved, None, ws, self.tdtype, dev, None, lo=lo, hi=hi,
+                                      dout0=dout.to(self.tdtype).contiguous())
+        finally:
+            if self._sw is not None:
+                torch.cuda.current_stream(dev).wait_stream(self._sw)
+            self._sw = None
+
+    def _run_backward(self, saved, dfeat, ws, T, dev, on_stage_done=None, lo=0, hi=None, dout0=None):
         ws["bstat"].zero_()
-        dfeat = dfeat.float().contiguous()
+        dfeat = dfeat.float().contiguous() if dfeat is not None else None
         blocks = saved["blocks"]
-        dout = None
+        hi = len(self._blocks) if hi is None else hi
+        dout = dout0
         dout_masked = False   # dout already = g (ReLU-masked) with bn2 sums accumulated by the dgrad epilogue
-        for bi in range(len(self._blocks) - 1, -1, -1):
+        for bi in range(hi - 1, lo - 1, -1):
             pre, has_ds = self._blocks[bi]
             B = blocks[bi]
             x, y1, y2, yd, out = B["x"], B["y1"], B["y2"], B["yd"], B["out"]
@@ -510,9 +554,10 @@ class ResNet34Tower(ArenaModule):
             dy2 = torch.empty_like(y2)
             A = (y2, mu2, is2, self.arena.view(k2 + ".weight"), sg2, sgx2, dy2)
             Bside, g_id = None, None
-            prev = self._blocks[bi - 1] if bi > 0 else None
+            prev = self._blocks[bi - 1] if bi > lo else None
+            # (dy1 | dyd) is one 32-bit buffer resource in vlp_conv_dgrad_relu_ds: 2 bf16 tensors < 4 GiB
             ds_fold = (_USE_DS_FOLD and has_ds and T == torch.bfloat16 and c1.S == 2 and prev is not None
-                       and not prev[1] and tuple(y1.shape) == tuple(yd.shape))
+                       and not prev[1] and tuple(y1.shape) == tuple(yd.shape) and 4 * y1.numel() < 2 ** 32)
             dy_pair = None
             if has_ds:
                 if ds_fold:   # dy1 and dyd in one allocation (dyd second): one GEMM reads both
@@ -525,11 +570,13 @@ class ResNet34Tower(ArenaModule):
                 g_id = dout          # the identity branch's gradient is g itself
             else:
                 g_id = torch.empty_like(out)
-            tA = self._tbuf(ws, "tA", C, M)
-            tB = self._tbuf(ws, "tB", C, M) if (has_ds and tA is not None) else None
-            # layer 1: both BN backward applies move into the rows kernels' rings
-            fuse_in = (_USE_BWD_ACT and T == torch.bfloat16 and dout_masked and not has_ds and tA is None
-                       and c1.S == 1 and ops.conv_dgrad_act_ok(dout, C, 3, 3, 1, 1))
+            # layer 1: both BN backward applies move into the rows kernels' rings -- only where
+            # conv1's data gradient then runs a fused-input epilogue (the stem-sums or the
+            # previous-block branch below); otherwise the plain path applies dy1 itself
+            stem_sums = bi == 0 and lo == 0 and saved.get("yarg") is not None
+            fuse_in = (_USE_BWD_ACT and T == torch.bfloat16 and dout_masked and not has_ds
+                       and c1.S == 1 and (stem_sums or (prev is not None and not prev[1]))
+                       and ops.conv_dgrad_act_ok(dout, C, 3, 3, 1, 1))
             sc1, sh1, mu1, is1 = self._coef(ws, k1)
             sg1f, sgx1f = self._bstat(ws, k1, full=True)
             if fuse_in:
@@ -542,31 +589,29 @@ class ResNet34Tower(ArenaModule):
                                            y1, (sc1, sh1, mu1, is1), sg1f, sgx1f, stat_rep=STAT_REP)
             else:
                 ops.bn_bwd_apply(M, C, dout, dbc, HW, None if dout_masked else out, A, Bside,
-                                 None if dout_masked else g_id, out, dyT_a=tA, dyT_b=tB)
+                                 None if dout_masked else g_id, out)
                 # conv2: dgrad through relu(bn1(y1)) with BN1 backward sums; wgrad on relu(bn1(y1))
                 g1 = ops.conv_dgrad(dy2, ws[c2.key + ".wt"], Hh, Ww, C, 3, 3, 1, 1, y_bn=y1,
                                     bn=(sc1, sh1, mu1, is1), stat1=sg1f, stat2=sgx1f, stat_rep=STAT_REP)
             ops.bn_grad_rep(STAT_REP, C, sg1f, sgx1f, self.arena.gview(k1 + ".weight"),
                             self.arena.gview(k1 + ".bias"))
             sg1, sgx1 = sg1f[:C], sgx1f[:C]
-            self._wgrad(ws, c2, dy2, B["a1"], dyT=tA)
+            self._wgrad(ws, c2, dy2, B["a1"])
             dy1 = dy_pair[0] if dy_pair is not None else torch.empty_like(y1)
             if fuse_in:
                 ops.bn_bwd_coef(M, self.arena.view(k1 + ".weight"), is1, mu1, sg1, sgx1, coef[1])
             else:
                 ops.bn_bwd_apply(M, C, g1, None, 1, None,
-                                 (y1, mu1, is1, self.arena.view(k1 + ".weight"), sg1, sgx1, dy1), None, None, y1,
-                                 dyT_a=tA)
+                                 (y1, mu1, is1, self.arena.view(k1 + ".weight"), sg1, sgx1, dy1), None, None, y1)
             Hi, Wi = x.shape[1], x.shape[2]
             addend = g_id
             if has_ds:
                 cd = self._convs[pre + ".downsample.0"]
                 if not ds_fold:
                     addend = ops.conv_dgrad(dyd, ws[cd.key + ".wt"], Hi, Wi, Cin, 1, 1, cd.S, 0)
-                self._wgrad(ws, cd, dyd, x, dyT=tB)
+                self._wgrad(ws, cd, dyd, x)
             # the gradient reaching block bi-1 passes its output ReLU and feeds its bn2:
             # when that block has no downsample branch, mask + reduce in this epilogue
-            stem_sums = bi == 0 and saved.get("yarg") is not None
             if stem_sums:
                 # block 0's input is the maxpool output p = relu(bn1(y0)) at each window's
                 # argmax: its mask and the stem BN's backward sums (xhat of y0 at the
@@ -616,10 +661,11 @@ class ResNet34Tower(ArenaModule):
                                           sgpf, sgxpf, sgxdpf, addend=addend, stat_rep=STAT_REP)
                 dout_masked = True
             else:
-                assert not fuse_in
+                if fuse_in:   # dy1 was never applied: the branches above are the only consumers of coef
+                    raise RuntimeError(f"{pre}: fused BN-backward input without a fused data-gradient epilogue")
                 dx = ops.conv_dgrad(dy1, ws[c1.key + ".wt"], Hi, Wi, Cin, 3, 3, c1.S, 1, addend=addend)
                 dout_masked = False
-            self._wgrad(ws, c1, dy1, x, dyT=tA)
+            self._wgrad(ws, c1, dy1, x)
             if self._dbg is not None:
                 self._dbg[pre + "/dy2"] = (dy2.detach().clone(), False)
                 self._dbg[pre + "/g1"] = (g1.detach().clone(), False)
@@ -630,6 +676,8 @@ class ResNet34Tower(ArenaModule):
                 # first block of a stage: every gradient of that stage is final
                 # (its bn2 sums came from the block above, already folded)
                 self._stage_done([stage], on_stage_done, dev)
+        if dout0 is not None:   # a block range (run_block_range_backward): the input gradient
+            return dout
         self._stem_backward(saved, dout, ws, dev, on_stage_done)
 
     def _stem_backward(self, saved, dout, ws, dev, on_stage_done):
@@ -661,20 +709,8 @@ class ResNet34Tower(ArenaModule):
                                 self.arena.gview("conv1.weight"))
         self._stage_done(["layer1", "stem"], on_stage_done, dev)
 
-    def _tbuf(self, ws, name, C, M):
-        """[C][M] bf16 scratch for a transposed output gradient (the weight-gradient
-        GEMM's pixel-contiguous A operand), or None where the transposing BN
-        backward does not apply (fp32 parity mode, odd shapes)."""
-        if self.tdtype != torch.bfloat16 or C % 64 or M % 8 or not _USE_DYT:
-            return None
-        buf = ws.get(name)
-        if buf is None or buf.numel() < C * M:
-            buf = torch.empty(C * M, dtype=torch.bfloat16, device=self.arena.data.device)
-            ws[name] = buf
-        return buf[:C * M].view(C, M)
-
-    def _wgrad(self, ws, c, dy, x, sc=None, sh=None, dyT=None):
-        if sc is None and dyT is None:
+    def _wgrad(self, ws, c, dy, x, sc=None, sh=None):
+        if sc is None:
             sw = getattr(self, "_sw", None)
             if sw is not None:
                 # fork onto the weight-gradient stream; the allocator must not
@@ -690,7 +726,7 @@ class ResNet34Tower(ArenaModule):
         o, n = self._wg_off[c.key]
         buf = ws["wgrad"][o:o + n]
         buf.zero_()
-        ops.conv_wgrad(dy, x, c.KH, c.KW, c.S, c.P, buf, sc, sh, dyT=dyT)
+        ops.conv_wgrad(dy, x, c.KH, c.KW, c.S, c.P, buf, sc, sh)
         ops.unpack_conv_grad(buf, self.arena.gview(c.key + ".weight"))
 
     # ---------------- autograd entry ----------------
