@@ -424,6 +424,10 @@ int vlp_clip_loss_fused(int B, int N, int E, int offset, const float* img_all,
  * dlogits (+=, optional) = d (role_w[0] image_loss + role_w[1] text_loss) / 2 / d logits
  * (role_w NULL: {1, 1}, the reference's loss, :550-552) */
 int vlp_ce_sym(int B, const float* logits, float* out, float* dlogits, const float* role_w, void* stream);
+/* C[M][N] (=|+=) alpha * sum_k A(m,k) B(n,k) on MFMA; a_kc / b_kc: K-contiguous
+ * operand ([rows][ld]) else MN-contiguous ([K][ld]).  Every contiguous extent and
+ * leading dimension a multiple of 16 B (4 fp32 / 8 bf16), N and ldc multiples of 4;
+ * otherwise hipErrorInvalidValue */
 int vlp_matmul(int dtype, int M, int N, int K, const void* A, int lda, int a_kc, const void* B,
                int ldb, int b_kc, void* C, int ldc, int out_f32, float alpha, int accumulate,
                void* stream);

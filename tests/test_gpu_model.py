@@ -200,9 +200,9 @@ def test_per_direction_loss_gradients_fp32(path, w):
     through the fused training step (ClipStepFn reruns the head with per-direction
     weights) and through the API forward + _compute_loss (_SymCEFn), every
     gradient in the strict fp64 envelope of the oracle's same objective."""
-    B, H, T = 4, 64, 12
-    batch = synth_batch(B, H, T, 0)
-    m = make_model("fp32")
+    B, H, T = 6, 96, 16     # test_grads_vs_oracle_fp32's strict configuration
+    batch = synth_batch(B, H, T, 3)
+    m = make_model("fp32", seed=1)
     m.train()
     if path == "fused_step":
         loss, li, lt, _, _ = m.training_step_outputs(batch)
@@ -214,7 +214,7 @@ def test_per_direction_loss_gradients_fp32(path, w):
         obj = obj + w[0] * loss
     obj.backward()
     torch.cuda.synchronize()
-    o32, o64 = _oracle_obj(batch, 0, torch.float32, w), _oracle_obj(batch, 0, torch.float64, w)
+    o32, o64 = _oracle_obj(batch, 1, torch.float32, w), _oracle_obj(batch, 1, torch.float64, w)
     grads = [(k, p.grad) for k, p in m.named_parameters()]
     assert all(g is not None and torch.isfinite(g).all() for k, g in grads if dict(o64.named_parameters())[k].grad
                is not None)

@@ -528,6 +528,13 @@ VLP_EXPORT int vlp_matmul(int dtype, int M, int N, int K, const void* A, int lda
                           const void* Bm, int ldb, int b_kc, void* C, int ldc, int out_f32,
                           float alpha, int accumulate, void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  // the loaders move 16-B chunks along the contiguous dimension and the epilogues
+  // store 4-column groups: every contiguous extent and leading dimension must be a
+  // whole number of chunks (a ragged tail would read the next row's elements)
+  const int epc = dtype == VLP_BF16 ? 8 : 4;
+  if (M < 0 || N < 0 || K < 0 || (a_kc ? K : M) % epc || lda % epc || (b_kc ? K : N) % epc || ldb % epc ||
+      N % 4 || ldc % 4)
+    return (int)hipErrorInvalidValue;
   auto run = [&](auto tag) -> int {
     using T = decltype(tag);
     auto go = [&](const auto& la, const auto& lb) -> int {

@@ -155,6 +155,14 @@ class _EmbedFn(torch.autograd.Function):
         return None, dfeat.float(), None, dP
 
 
+def _pad_rows4(t):
+    """Zero rows up to a multiple of 4 (vlp_matmul moves 16-B chunks along every
+    contiguous extent; zero rows add nothing to the products)."""
+    r = (-t.shape[0]) % 4
+    t = t.float().contiguous()
+    return t if r == 0 else torch.cat([t, t.new_zeros((r,) + tuple(t.shape[1:]))])
+
+
 class _LogitsFn(torch.autograd.Function):
     """logits = clamp(exp(logit_scale), max=100) * img @ txt^T (:456-459)."""
 
@@ -163,28 +171,33 @@ class _LogitsFn(torch.autograd.Function):
         B, E = ie.shape
         Nt = te.shape[0]
         s = torch.clamp(ls.detach().exp(), max=100).float()
-        cos = torch.empty(B, Nt, dtype=torch.float32, device=ie.device)
-        ops.matmul(ie.contiguous(), te.contiguous(), cos, B, Nt, E, E, 1, E, 1, Nt)
+        iep, tep = _pad_rows4(ie), _pad_rows4(te)
+        Bp, Np = iep.shape[0], tep.shape[0]
+        cos = torch.empty(Bp, Np, dtype=torch.float32, device=ie.device)
+        ops.matmul(iep, tep, cos, Bp, Np, E, E, 1, E, 1, Np)
         logits = torch.empty_like(cos)
         ops.scale(cos, s, logits)
-        ctx.save_for_backward(ie, te, ls, cos, s)
-        return logits
+        ctx.save_for_backward(iep, tep, ls, cos, s)
+        ctx.shape = (B, Nt)
+        return logits[:B, :Nt]
 
     @staticmethod
     def backward(ctx, g):
-        ie, te, ls, cos, s = ctx.saved_tensors
-        B, E = ie.shape
-        Nt = te.shape[0]
-        g = g.float().contiguous()
-        gs = torch.empty_like(g)
-        ops.scale(g, s, gs)
-        die = torch.empty_like(ie)
-        ops.matmul(gs, te.contiguous(), die, B, E, Nt, Nt, 1, E, 0, E)       # gs @ te
-        dte = torch.empty_like(te)
-        ops.matmul(gs, ie.contiguous(), dte, Nt, E, B, Nt, 0, E, 0, E)       # gs^T @ ie
+        iep, tep, ls, cos, s = ctx.saved_tensors
+        B, Nt = ctx.shape
+        Bp, Np = cos.shape
+        E = iep.shape[1]
+        gp = torch.zeros(Bp, Np, dtype=torch.float32, device=g.device)
+        gp[:B, :Nt] = g
+        gs = torch.empty_like(gp)
+        ops.scale(gp, s, gs)
+        die = torch.empty_like(iep)
+        ops.matmul(gs, tep, die, Bp, E, Np, Np, 1, E, 0, E)       # gs @ te
+        dte = torch.empty_like(tep)
+        ops.matmul(gs, iep, dte, Np, E, Bp, Np, 0, E, 0, E)       # gs^T @ ie
         # d logit_scale = sum(g * cos) * s  (zero when clamped)
-        dls = (g * cos).sum().reshape(1) * s * (ls.detach().exp() <= 100).float()
-        return die, dte, dls.to(ls.dtype)
+        dls = (gp * cos).sum().reshape(1) * s * (ls.detach().exp() <= 100).float()
+        return die[:B], dte[:Nt], dls.to(ls.dtype)
 
 
 class _SymCEFn(torch.autograd.Function):

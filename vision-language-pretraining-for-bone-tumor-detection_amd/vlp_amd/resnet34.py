@@ -670,6 +670,8 @@ class ResNet34Tower(ArenaModule):
                 self._dbg[pre + "/dy2"] = (dy2.detach().clone(), False)
                 self._dbg[pre + "/g1"] = (g1.detach().clone(), False)
                 self._dbg[pre + "/dy1"] = (dy1.detach().clone(), False)
+                if has_ds:
+                    self._dbg[pre + "/dyd"] = (dyd.detach().clone(), False)
             dout = dx
             stage = pre.split(".", 1)[0]
             if pre.endswith(".0") and stage != "layer1":
