@@ -64,6 +64,13 @@ CONV_CASES = [
     (4, 8, 8, 320, 256, 3, 3, 1, 1),
     (2, 12, 12, 128, 128, 3, 3, 1, 1),  # Co = 128 weight gradient: 128x384 ping-pong tiles
     (3, 9, 11, 256, 320, 3, 3, 1, 1),
+    # LDS-window kernel (bf16 3x3 stride 1, W in {16, 32, 64}, C and the GEMM N multiples of 128):
+    # one window per 256-pixel tile of whole rows, several N tiles, NC = 2 / 4 / 8 channel chunks
+    (2, 8, 64, 128, 128, 3, 3, 1, 1),
+    (3, 4, 64, 256, 128, 3, 3, 1, 1),
+    (2, 8, 64, 128, 256, 3, 3, 1, 1),
+    (2, 16, 32, 256, 256, 3, 3, 1, 1),
+    (2, 16, 16, 512, 512, 3, 3, 1, 1),
 ]
 
 
@@ -101,15 +108,17 @@ def test_conv_fwd(ops, dt, case, xform):
     assert rel(s2.cpu(), (ref * ref).sum((0, 2, 3))) < 1e-4
 
 
-@pytest.mark.parametrize("N,H", [(3, 5), (2, 128), (300, 4)])
-def test_conv_fwd_act_matches_pass_then_conv(ops, N, H):
-    """vlp_conv_fwd_act (bn1 + ReLU in the layer-1 rows kernel's ring) against the
-    separate bn_add_relu pass + conv_fwd: a1 and y bit-identical, BN sums equal up
-    to fp64 atomic order; N = 300 > CUs puts two images on some workgroups."""
+@pytest.mark.parametrize("N,H,W,C", [(3, 5, 128, 64), (2, 128, 128, 64), (300, 4, 128, 64),
+                                     (2, 8, 64, 128), (3, 16, 32, 256), (2, 16, 16, 512)])
+def test_conv_fwd_act_matches_pass_then_conv(ops, N, H, W, C):
+    """vlp_conv_fwd_act (bn1 + ReLU applied once per input element: in the layer-1
+    rows kernel's ring, W = 128; in the window of the LDS-window kernel, layers
+    2-4) against the separate bn_add_relu pass + conv_fwd: a1 and y bit-identical,
+    BN sums equal up to fp64 atomic order; N = 300 > CUs puts two images on some
+    workgroups; C = 256 / 512 has several N tiles (one writes a1)."""
     torch.manual_seed(11)
-    C = 64
     dev = torch.device("cuda")
-    y1 = torch.randn(N, H, 128, C, device=dev).to(torch.bfloat16)
+    y1 = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
     sc = (torch.rand(C, device=dev) + 0.5) * torch.where(torch.arange(C, device=dev) % 5 == 0, -1.0, 1.0)
     sh = torch.randn(C, device=dev) * 0.3
     w = (torch.randn(C, C, 3, 3) * (9 * C) ** -0.5).to(torch.bfloat16).float()
@@ -133,9 +142,9 @@ def test_conv_fwd_act_matches_pass_then_conv(ops, N, H):
     ref = F.conv2d(xin, w, padding=1)
     assert rel(nchw(y.float().cpu()), ref) < tol(torch.bfloat16)
     # other shapes are refused, not silently rerouted
-    assert not ops.conv_fwd_act_ok(y1[:, :, :64].contiguous(), C, 3, 3, 1, 1)
+    assert not ops.conv_fwd_act_ok(y1[:, :, :W - 8].contiguous(), C, 3, 3, 1, 1)
     with pytest.raises(RuntimeError):
-        ops.conv_fwd_act(y1[:, :, :64].contiguous(), wp, C, 3, 3, 1, 1, sc, sh, a[:, :, :64].contiguous(),
+        ops.conv_fwd_act(y1[:, :, :W - 8].contiguous(), wp, C, 3, 3, 1, 1, sc, sh, a[:, :, :W - 8].contiguous(),
                          t1, t2, stat_rep=4)
 
 
@@ -409,7 +418,8 @@ def test_conv_wgrad_split_slabs(ops, case, ws_floats):
 
 
 @pytest.mark.parametrize("dt", DT)
-@pytest.mark.parametrize("N,H,W,C", [(2, 10, 10, 64), (2, 4, 128, 64), (4, 7, 7, 512), (2, 14, 14, 256)])
+@pytest.mark.parametrize("N,H,W,C", [(2, 10, 10, 64), (2, 4, 128, 64), (4, 7, 7, 512), (2, 14, 14, 256),
+                                     (2, 8, 64, 128), (2, 16, 16, 512)])
 def test_conv_dgrad_bn_epilogue(ops, dt, N, H, W, C):
     Co, KH, KW, S, P = C, 3, 3, 1, 1
     torch.manual_seed(3)
@@ -438,7 +448,8 @@ def test_conv_dgrad_bn_epilogue(ops, dt, N, H, W, C):
 
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("case", [(2, 10, 10, 64, 64, 1), (2, 4, 128, 64, 64, 1), (2, 12, 12, 64, 128, 2),
-                                  (4, 7, 7, 512, 512, 1), (4, 14, 14, 256, 512, 2)])
+                                  (4, 7, 7, 512, 512, 1), (4, 14, 14, 256, 512, 2), (2, 8, 64, 128, 128, 1),
+                                  (2, 16, 32, 256, 256, 1)])
 @pytest.mark.parametrize("with_add", [False, True])
 @pytest.mark.parametrize("bits", [False, True])
 def test_conv_dgrad_relu_epilogue(ops, dt, case, with_add, bits):

@@ -21,6 +21,10 @@ LAYERS = {
     "l2": (256, 64, 64, 128, 128, 3, 3, 1, 1),
     "l3": (256, 32, 32, 256, 256, 3, 3, 1, 1),
     "l4": (256, 16, 16, 512, 512, 3, 3, 1, 1),
+    # stride-2 stage entries (conv1 of layer2.0 / 3.0 / 4.0; dgrad_relu_ds folds the 1x1/2 downsample)
+    "l2s": (256, 128, 128, 64, 128, 3, 3, 2, 1),
+    "l3s": (256, 64, 64, 128, 256, 3, 3, 2, 1),
+    "l4s": (256, 32, 32, 256, 512, 3, 3, 2, 1),
 }
 
 
@@ -45,8 +49,9 @@ def main():
         s1 = torch.zeros(64 * Co, dtype=torch.float64, device=dev)
         s2 = torch.zeros_like(s1)
         dws = torch.zeros(Co, KH * KW * C, device=dev)
-        flop = 2.0 * N * Ho * Wo * Co * C * KH * KW
+        flop0 = 2.0 * N * Ho * Wo * Co * C * KH * KW
         for op in args.ops.split(","):
+            flop = flop0
             if op == "fwd":
                 fn = lambda: ops.conv_fwd(x, wp, Co, KH, KW, S, P, stat_sum=s1, stat_sumsq=s2, stat_rep=64)  # noqa: E731
             elif op == "fwd_bn":       # BN-apply + ReLU of the input on load (in_scale / in_shift)
@@ -81,6 +86,41 @@ def main():
                 t1, t2 = torch.zeros(64 * C, dtype=torch.float64, device=dev), torch.zeros(64 * C, dtype=torch.float64, device=dev)
                 fn = lambda: ops.conv_dgrad_relu(dy, wt, H, W, C, KH, KW, S, P, mk, yb, mu, ist, t1, t2,  # noqa: E731
                                                  addend=ad, stat_rep=64)
+            elif op == "dgrad_bn_act":   # layer 1: dy = k*g + b*y + c formed in the ring + EpiDgradBN
+                coef = torch.randn(3, Co, device=dev) * 0.1
+                yin = (torch.randn(N, Ho, Wo, Co, device=dev)).to(torch.bfloat16)
+                dyo = torch.empty_like(dy)
+                yb = (torch.randn(N, H, W, C, device=dev)).to(torch.bfloat16)
+                bn = (torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1, torch.zeros(C, device=dev),
+                      torch.ones(C, device=dev))
+                t1, t2 = torch.zeros(64 * C, dtype=torch.float64, device=dev), torch.zeros(64 * C, dtype=torch.float64, device=dev)
+                fn = lambda: ops.conv_dgrad_bn_act(dy, yin, coef, dyo, wt, H, W, C, KH, KW, S, P, yb, bn, t1, t2,  # noqa: E731
+                                                   stat_rep=64)
+            elif op == "dgrad_relu_act":  # layer 1: ring-formed dy + addend, ReLU bits, BN sums
+                coef = torch.randn(3, Co, device=dev) * 0.1
+                yin = (torch.randn(N, Ho, Wo, Co, device=dev)).to(torch.bfloat16)
+                dyo = torch.empty_like(dy)
+                yb = (torch.randn(N, H, W, C, device=dev)).to(torch.bfloat16)
+                ad = (torch.randn(N, H, W, C, device=dev)).to(torch.bfloat16)
+                mk = torch.randint(0, 255, (N * H * W * C // 8,), dtype=torch.uint8, device=dev)
+                mu, ist = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+                t1, t2 = torch.zeros(64 * C, dtype=torch.float64, device=dev), torch.zeros(64 * C, dtype=torch.float64, device=dev)
+                fn = lambda: ops.conv_dgrad_relu_act(dy, yin, coef, dyo, wt, H, W, C, KH, KW, S, P, mk, yb, mu,  # noqa: E731
+                                                     ist, t1, t2, addend=ad, stat_rep=64)
+            elif op == "dgrad_relu_ds":   # stride-2 entry: conv1 + downsample data gradients in one GEMM
+                pair = (torch.randn(2, N, Ho, Wo, Co, device=dev) * 0.5).to(torch.bfloat16)
+                wpair = torch.empty(C * KH * KW * Co + C * Co, dtype=torch.bfloat16, device=dev)
+                wpair[:C * KH * KW * Co].copy_(wt.reshape(-1))
+                wpair[C * KH * KW * Co:].normal_(0, 0.05)
+                wt1 = wpair[:C * KH * KW * Co].view(C, KH, KW, Co)
+                wtd = wpair[C * KH * KW * Co:].view(C, 1, 1, Co)
+                act = torch.relu(torch.randn(N, H, W, C, device=dev)).to(torch.bfloat16)
+                yb = (torch.randn(N, H, W, C, device=dev)).to(torch.bfloat16)
+                mu, ist = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+                t1, t2 = torch.zeros(64 * C, dtype=torch.float64, device=dev), torch.zeros(64 * C, dtype=torch.float64, device=dev)
+                fn = lambda: ops.conv_dgrad_relu_ds(pair[0], pair[1], wt1, wtd, H, W, C, KH, KW, S, P, act, yb,  # noqa: E731
+                                                    mu, ist, t1, t2, stat_rep=64)
+                flop = 2.0 * N * Ho * Wo * Co * C * (KH * KW + 1)
             elif op == "wgrad_a":      # the same atomic-epilogue engine on dy (MN operand)
                 gw0 = torch.zeros(Co * KH * KW * C, device=dev)
                 fn = lambda: ops.conv_wgrad(dy, x, KH, KW, S, P, gw0)  # noqa: E731

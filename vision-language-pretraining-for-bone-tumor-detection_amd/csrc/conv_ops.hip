@@ -1645,6 +1645,278 @@ static int launch_rows_c64(const ConvGeom& g, const void* x, const void* w, int 
   return (int)hipGetLastError();
 }
 
+// ---------------- LDS-window implicit GEMM: 3x3, stride 1, 64-channel chunks ----------------
+// The im2col GEMMs fetch every input pixel once per filter tap: 9 copies of the
+// A operand per 64-channel chunk pass through the LDS-DMA path, whose intake
+// bounds those kernels (no-DMA timing experiment 299 -> 185 us on
+// layer 3).  Here a workgroup owns 256 output pixels = TH full image rows of
+// width TW; per 64-channel chunk it stages the tile's input WINDOW -- (TH+2) x
+// (TW+2) pixels with the halo, zero outside the image -- once, and all 9 taps
+// read their A fragments from it at a compile-time pixel offset (tap (kh, kw):
+// +(kh * (TW+2) + kw); the data gradient, FLIP, reads the flipped tap).  Only
+// the B operand (the filter slice of the tap) streams per K-step, through a
+// 4-slot ring of 32-deep half-tiles (HStager, as the ping-pong kernel).  A
+// bytes per chunk: ~1.5 tiles instead of 9.
+// Window layout: 160 B per pixel (128 B of channels + 32 B of padding).  A
+// ds_read_b128 is serviced in 4 lane groups of 16 that mix the fragment's
+// pixels li in {0-3, 12-15} of one 16-B chunk with li in {4-11} of the next
+// chunk: at a stride of 10 16-B units the first set lands on the even and the
+// second on the odd bank slots, all distinct, for ANY first pixel -- every tap
+// offset reads conflict-free (a 128-B stride with an XOR swizzle cannot be
+// conflict-free for all 3 column offsets).  The LDS-DMA pieces (1 KiB per wave
+// instruction, lane -> 16 B) fill the padding from past the buffer resource
+// (zeros), as they do pixels outside the image.  Two window buffers: chunk
+// c+1's pieces are issued one per half-step over the first PPW half-steps of
+// chunk c, so the in-order vmcnt wait for each B half-tile never waits on a
+// whole window.
+// XF = 1 (forward): the window holds the raw output of the previous conv; at the
+// chunk's first half-step every thread turns its own pieces into
+// relu(sc * x + sh) (interior pixels only -- the zero padding stays zero) and
+// stores the tile's own pixels to xin.out, the activation the weight gradient
+// reads (BN-apply + ReLU without a separate pass, as the layer-1 rows kernel).
+// 8 waves: 4 (M) x 2 (N), 64 x BN/2 per wave (MFMA 16x16x32), the epilogue is the
+// multi-stage kernels' ms_epilogue<256, BN, 4, 2>.
+// timing experiments only (wrong results): 1 = no B fetches in the loop, 2 = no
+// window fetches, 3 = neither, 4 = no MFMAs, 5 = no barriers, 6 = no epilogue
+#ifndef VLP_WIN_EXP
+#define VLP_WIN_EXP 0
+#endif
+template <int TW>
+struct WinGeom {
+  static constexpr int TH = 256 / TW;                  // image rows per tile
+  static constexpr int WR = TH + 2, WC = TW + 2;       // window rows / columns
+  static constexpr int PS = 160;                       // LDS bytes per window pixel
+  static constexpr int BYTES = WR * WC * PS;
+  static constexpr int PPW = ((BYTES + 1023) / 1024 + 7) / 8;   // 1-KiB pieces per wave
+  static constexpr int SLOT = PPW * 8 * 1024;          // one window buffer
+};
+struct WinXIn {
+  const float* sc; const float* sh;   // XF 1: per-channel BN scale / shift of the input
+  bf16* out;                          // XF 1: relu(sc * x + sh) of the tile's pixels
+};
+template <int TW, int BN>
+constexpr int win_lds_bytes() { return 2 * WinGeom<TW>::SLOT + 4 * BN * 64; }
+
+template <int TW, int BN, bool FLIP, int XF, class EP>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsigned xbytes, KMat<bf16> lb, EP ep,
+                   WinXIn xin) {
+  using WG = WinGeom<TW>;
+  constexpr int BM = 256, WGM = 4, WGN = 2, NT = 512;
+  constexpr int WTN = BN / WGN;
+  constexpr int MB = 4, NB = WTN / 16;
+  constexpr int BSLOT = BN * 64;
+  constexpr int PPW = WG::PPW;
+  using SB = HStager<BN, KMat<bf16>, NT>;
+  static_assert(PPW <= 16, "window pieces are issued over the first half-steps of a chunk");
+  static_assert(win_lds_bytes<TW, BN>() <= 160 * 1024 && BM * BN * 2 + 4096 <= win_lds_bytes<TW, BN>(), "LDS budget");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const win = smem;
+  char* const ring = smem + 2 * WG::SLOT;
+
+  const int nwg = sh.tiles_m * sh.tiles_n;
+  const int bid = blockIdx.x;
+  int g = bid;
+  if (nwg >= 16) {   // consecutive tiles (shared halo rows) on one XCD
+    const int xcd = bid & 7, idx = bid >> 3, q = nwg >> 3, rr = nwg & 7;
+    g = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
+  }
+  const int tm = g / sh.tiles_n, tn = g - tm * sh.tiles_n;
+  const int row0 = tm * BM, col0 = tn * BN;
+  const int n = row0 / (H * TW), h0 = (row0 - n * H * TW) / TW;
+  const int NC = C / 64;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wv / WGN, wn = wv - wm * WGN;
+  const int li = lane & 15, lg = lane >> 4;
+
+  // this thread's window pieces: LDS byte -> (pixel, 16-B chunk) -> source
+  // offset in channel chunk 0 (kOOB for padding and outside the image)
+  const rsrc_t rx = buf_rsrc(x, xbytes);
+  const rsrc_t rb = lb.rsrc();
+  const rsrc_t rz = null_rsrc(zero_page());
+  unsigned woff[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int off = (wv * PPW + i) * 1024 + lane * 16;
+    const int p = off / WG::PS, c = (off - p * WG::PS) >> 4;
+    const int wr = p / WG::WC, wc = p - wr * WG::WC;
+    const int hh = h0 - 1 + wr, ww = wc - 1;
+    const bool ok = c < 8 && p < WG::WR * WG::WC && hh >= 0 && hh < H && ww >= 0 && ww < TW;
+    woff[i] = ok ? (unsigned)((((n * H + hh) * TW + ww) * C) * 2 + c * 16) : kOOB;
+  }
+  SB sb;
+  sb.init(lb, col0, 0, wv);
+  // B half-tile hc of tap t, channel chunk cc (cc == NC: past the end, zeros)
+  auto bfetch = [&](auto hc, int t, int cc, char* slot) __attribute__((always_inline)) {
+    if constexpr (VLP_WIN_EXP == 1 || VLP_WIN_EXP == 3) if (t + cc > 0) return;
+    sb.template issue<decltype(hc)::value>(lb, cc < NC ? rb : rz, t * C + cc * 64, slot, wv);
+  };
+
+  v4f acc[MB][NB];
+#pragma unroll
+  for (int a = 0; a < MB; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[a][b] = v4f{0.f, 0.f, 0.f, 0.f};
+  // A fragment of lane (li, lg): pixel li of the fragment's 16, 16-B chunk lg
+  // of the half-step's 32 channels (tap and half: compile-time offsets)
+  const int aoff = li * WG::PS + lg * 16;
+  const int wpx = wm * 64;   // the wave's first pixel in the tile
+  const char* const bbase = ring + li * 64 + (pp_chunk(li, lg) << 4) + wn * WTN * 64;
+
+  // XF 1: this thread's own pieces of window cc (landed) -> relu(sc * x + sh) in
+  // place, the tile's own pixels to xin.out (one N tile writes them)
+  auto xform = [&](int cc, char* wb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      if (woff[i] == kOOB) continue;
+      const int off = (wv * PPW + i) * 1024 + lane * 16;
+      const int p = off / WG::PS;
+      const int wr = p / WG::WC;
+      const int c0 = cc * 64 + ((off - p * WG::PS) >> 4) * 8;
+      uint4* q = reinterpret_cast<uint4*>(wb + off);
+      float f[8];
+      Chunk<bf16>::unpack(*q, f);
+      const v4f s0 = *reinterpret_cast<const v4f*>(xin.sc + c0), s1 = *reinterpret_cast<const v4f*>(xin.sc + c0 + 4);
+      const v4f t0 = *reinterpret_cast<const v4f*>(xin.sh + c0), t1 = *reinterpret_cast<const v4f*>(xin.sh + c0 + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f[j] = fmaxf(fmaf(f[j], s0[j], t0[j]), 0.f);
+        f[4 + j] = fmaxf(fmaf(f[4 + j], s1[j], t1[j]), 0.f);
+      }
+      const uint4 v = Chunk<bf16>::pack(f);
+      *q = v;
+      if (tn == 0 && wr >= 1 && wr <= WG::TH) stg16(reinterpret_cast<char*>(xin.out) + woff[i] + (unsigned)cc * 128u, v);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  // fragments of half-step (tap t, half hh) from window buffer wb, ring slot sl
+  v8bf fa[2][MB], fb[2][NB];
+  auto rd = [&](auto setc, auto sc_, char* wb, int sl) __attribute__((always_inline)) {
+    constexpr int R = decltype(setc)::value, S = decltype(sc_)::value;
+    constexpr int T = S >> 1, HH = S & 1;
+    constexpr int KH = FLIP ? 2 - T / 3 : T / 3, KW = FLIP ? 2 - T % 3 : T % 3;
+#pragma unroll
+    for (int a = 0; a < MB; ++a) {
+      const int px = wpx + a * 16;   // wave-uniform
+      const int wrow = px / TW + KH, wcol = px % TW;
+      fa[R][a] = *reinterpret_cast<const v8bf*>(wb + aoff + (wrow * WG::WC + wcol + KW) * WG::PS + HH * 64);
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) fb[R][b] = *reinterpret_cast<const v8bf*>(bbase + sl * BSLOT + b * 16 * 64);
+  };
+
+  using H0 = std::integral_constant<int, 0>;
+  using H1 = std::integral_constant<int, 1>;
+  using Z = std::integral_constant<int, 0>;
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) dma16(rx, woff[i], win + (wv * PPW + i) * 1024);
+  bfetch(H0{}, 0, 0, ring);
+  bfetch(H1{}, 0, 0, ring + BSLOT);
+  bfetch(H0{}, 1, 0, ring + 2 * BSLOT);
+  wait_vmcnt<2 * SB::P>();   // window 0 and B(0)
+  if constexpr (XF == 1) xform(0, win);
+  raw_barrier();
+  rd(Z{}, Z{}, win, 0);
+
+  // one 64-channel chunk; PC (= cc & 1) selects the window buffer.  Half-step
+  // u = cc * 18 + S computes with the fragment set S & 1 read one half-step
+  // earlier, reads the next set, and fetches B(u + 3) into ring slot (u + 3) & 3
+  // (slot of B(v) = v & 3 = (S + 2 * PC) & 3).
+  auto chunk = [&](auto pc, int cc) __attribute__((always_inline)) {
+    constexpr int PC = decltype(pc)::value;
+    char* const wbuf = win + PC * WG::SLOT;
+    char* const wnext = win + (1 - PC) * WG::SLOT;
+    const rsrc_t rn = cc + 1 < NC ? rx : rz;
+    static_for<0, 18>([&](auto sc_) {
+      constexpr int S = decltype(sc_)::value;
+      constexpr int R = S & 1;
+      constexpr int SL = (S + 2 * PC) & 3;
+      // B(u+1) landed: issued after it are the previous half-step's window piece
+      // (half-steps 1..PPW) and B(u+2)
+      if constexpr (S >= 1 && S <= PPW) wait_vmcnt<SB::P + 1>();
+      else wait_vmcnt<SB::P>();
+      if constexpr (XF == 1 && S == 17) {
+        if (cc + 1 < NC) xform(cc + 1, wnext);   // window cc+1 landed by half-step PPW + 1
+      }
+      if constexpr (VLP_WIN_EXP != 5) raw_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (S < PPW && VLP_WIN_EXP != 2 && VLP_WIN_EXP != 3) dma16(rn, woff[S] + (unsigned)(cc + 1) * 128u, wnext + (wv * PPW + S) * 1024);
+      constexpr int S3 = S + 3 < 18 ? S + 3 : S + 3 - 18;   // half-step u + 3 = (chunk, S3)
+      bfetch(std::integral_constant<int, S3 & 1>{}, S3 >> 1, S + 3 < 18 ? cc : cc + 1, ring + ((SL + 3) & 3) * BSLOT);
+      if constexpr (S + 1 < 18) rd(std::integral_constant<int, 1 - R>{}, std::integral_constant<int, S + 1>{}, wbuf, (SL + 1) & 3);
+      else rd(std::integral_constant<int, 1 - R>{}, Z{}, wnext, (SL + 1) & 3);
+      __builtin_amdgcn_sched_barrier(0);
+#if VLP_PP_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
+      if constexpr (VLP_WIN_EXP == 4) {
+#pragma unroll
+        for (int a = 0; a < MB; ++a) acc[a][0][0] += (float)fa[R][a][0] + (float)fb[R][a][0];
+      } else {
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[R][b], fa[R][a], acc[a][b], 0, 0, 0);
+      }
+#if VLP_PP_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  for (int cc = 0; cc < NC; cc += 2) {
+    chunk(std::integral_constant<int, 0>{}, cc);
+    chunk(std::integral_constant<int, 1>{}, cc + 1);
+  }
+  wait_vmcnt<0>();
+  __syncthreads();   // ring and windows drained (incl. the null-resource tail fetches) before LDS is reused
+  if constexpr (VLP_WIN_EXP == 6) if (sh.dbg != 7) return;
+  ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep, acc, row0, col0, g, wm, wn, smem);
+}
+
+// 3x3 / stride 1 / pad 1 with C and the GEMM N both multiples of 128, 256-pixel
+// tiles of whole rows, widths 16 / 32 / 64 (ResNet34 layers 2-4 at 512 x 512)
+static bool win_ok(const ConvGeom& g, int cin, int nout) {
+  return g.KH == 3 && g.KW == 3 && g.S == 1 && g.P == 1 && (g.W == 16 || g.W == 32 || g.W == 64) &&
+         g.H % (256 / g.W) == 0 && cin % 128 == 0 && nout % 128 == 0 &&
+         (size_t)g.N * g.H * g.W * cin * 2 < (1ull << 31);
+}
+template <int TW, bool FLIP, int XF, class EP>
+static int launch_win_t(const ConvGeom& g, int cin, int nout, const void* x, const void* w, const EP& ep,
+                        hipStream_t st, const WinXIn& xin) {
+  constexpr int BN = 128;
+  constexpr int lds = win_lds_bytes<TW, BN>();
+  static KernelDevState kst;
+  const int e = prepare_kernel(kst, (const void*)&conv3x3_win_kernel<TW, BN, FLIP, XF, EP>, lds, 0, nullptr);
+  if (e) return e;
+  GemmShape sh;
+  sh.M = g.N * g.H * g.W;
+  sh.N = nout;
+  sh.K = 9 * cin;
+  sh.kchunk = sh.K;
+  sh.tiles_m = sh.M / 256;
+  sh.tiles_n = nout / BN;
+  sh.xsplit = 0;
+  sh.dbg = 0;
+  sh.nsplit = 1;
+  KMat<bf16> lb{(const bf16*)w, sh.K, nout, sh.K};
+  hipLaunchKernelGGL((conv3x3_win_kernel<TW, BN, FLIP, XF, EP>), dim3(sh.tiles_m * sh.tiles_n), dim3(512), lds, st, sh,
+                     g.H, cin, (const bf16*)x, (unsigned)((size_t)g.N * g.H * g.W * cin * 2), lb, ep, xin);
+  return (int)hipGetLastError();
+}
+#ifndef VLP_WIN
+#define VLP_WIN 1   // the LDS-window kernel for the 3x3 stride-1 GEMMs of layers 2-4 (0: im2col GEMMs)
+#endif
+template <bool FLIP, int XF = 0, class EP>
+static int launch_win(const ConvGeom& g, int cin, int nout, const void* x, const void* w, const EP& ep,
+                      hipStream_t st, const WinXIn& xin = WinXIn{}) {
+  if (g.W == 64) return launch_win_t<64, FLIP, XF>(g, cin, nout, x, w, ep, st, xin);
+  if (g.W == 32) return launch_win_t<32, FLIP, XF>(g, cin, nout, x, w, ep, st, xin);
+  return launch_win_t<16, FLIP, XF>(g, cin, nout, x, w, ep, st, xin);
+}
+
 #ifndef VLP_FWD_BN_PP
 #define VLP_FWD_BN_PP 1   // bf16 BN-on-load forward on the ping-pong kernel (fragment transform)
 #endif
@@ -1670,6 +1942,7 @@ static int conv_fwd_t(const void* x, const void* wp, void* y, ConvGeom g, const 
   ConvFwdA<T, false> la{g, (const T*)x, nullptr, nullptr};
   if constexpr (std::is_same<T, bf16>::value) {
     if (rows_c64_ok(g)) return launch_rows_c64(g, x, wp, 0, ep, st);
+    if (VLP_WIN && win_ok(g, g.C, g.Co)) return launch_win<false>(g, g.C, g.Co, x, wp, ep, st);
     // the LDS-DMA loaders take ONE filter tap per 64-deep K-step; a channel
     // count that is not a multiple of 64 (NesT's 96-channel ConvPool input)
     // takes the register-staged engine, which resolves the tap per 16-B chunk
@@ -1715,16 +1988,19 @@ static int conv_dgrad_t(const void* dy, const void* wt, void* dx, ConvGeom g, co
   KMat<T> lb{(const T*)wt, g.K, g.C, g.K};
   // stride-1 dgrad = forward conv of dy with the flipped, transposed filter
   const bool rows = std::is_same<T, bf16>::value && rows_c64_ok(g);
+  const bool win = std::is_same<T, bf16>::value && VLP_WIN && win_ok(g, g.Co, g.C);
   if (ybn) {
     EpiDgradBN<T> ep{s1, s2, rep, (T*)dx, g.C, (const T*)ybn, sc, sh, mean, invstd};
     if constexpr (std::is_same<T, bf16>::value) {
       if (rows) return launch_rows_c64(g, dy, wt, 1, ep, st);
+      if (win) return launch_win<true>(g, g.Co, g.C, dy, wt, ep, st);
     }
     return gemm_auto<T>(g.M, g.C, g.K, 1, la, lb, ep, st);
   }
   EpiDgradAdd<T> ep{nullptr, nullptr, (T*)dx, (const T*)addend, g.C};
   if constexpr (std::is_same<T, bf16>::value) {
     if (rows) return launch_rows_c64(g, dy, wt, 1, ep, st);
+    if (win) return launch_win<true>(g, g.Co, g.C, dy, wt, ep, st);
   }
   return gemm_auto<T>(g.M, g.C, g.K, 1, la, lb, ep, st);
 }
@@ -1763,6 +2039,7 @@ static int conv_dgrad_relu_impl(const void* dy, const void* wt, void* gout, Conv
   }
   if constexpr (std::is_same<T, bf16>::value) {
     if (rows_c64_ok(g)) return launch_rows_c64(g, dy, wt, 1, in, st);
+    if (VLP_WIN && win_ok(g, g.Co, g.C)) return launch_win<true>(g, g.Co, g.C, dy, wt, in, st);
   }
   ConvDgradA<T> la{g, (const T*)dy};
   KMat<T> lb{(const T*)wt, g.K, g.C, g.K};
@@ -2004,7 +2281,9 @@ VLP_EXPORT int vlp_conv_fwd(int dtype, const void* x, const void* wp, void* y, i
 
 VLP_EXPORT int vlp_conv_fwd_act_ok(int dtype, int N, int H, int W, int C, int Co, int KH, int KW, int S,
                                   int P) {
-  return dtype == VLP_BF16 && N >= 1 && rows_c64_ok(make_geom(N, H, W, C, Co, KH, KW, S, P)) ? 1 : 0;
+  if (dtype != VLP_BF16 || N < 1) return 0;
+  const ConvGeom g = make_geom(N, H, W, C, Co, KH, KW, S, P);
+  return rows_c64_ok(g) || (VLP_WIN && win_ok(g, C, Co)) ? 1 : 0;
 }
 
 VLP_EXPORT int vlp_conv_fwd_act(int dtype, const void* x, const void* wp, void* y, void* x_act, int N,
@@ -2018,6 +2297,10 @@ VLP_EXPORT int vlp_conv_fwd_act(int dtype, const void* x, const void* wp, void* 
   g.M = g.N * g.Ho * g.Wo;
   g.K = g.KH * g.KW * g.C;
   EpiConvFwd<bf16> ep{stat_sum, stat_sumsq, stat_rep, (bf16*)y, g.Co};
+  if (!rows_c64_ok(g)) {   // layers 2-4: the window kernel transforms each window chunk once
+    WinXIn wx{in_scale, in_shift, (bf16*)x_act};
+    return launch_win<false, 1>(g, g.C, g.Co, x, wp, ep, (hipStream_t)stream, wx);
+  }
   RowsXIn xin{};
   xin.t0 = in_scale;
   xin.t1 = in_shift;
@@ -2038,7 +2321,7 @@ static RowsXIn rows_bwd_xin(const void* y_in, const float* in_coef, void* dy_out
 
 VLP_EXPORT int vlp_conv_dgrad_act_ok(int dtype, int N, int H, int W, int C, int Co, int KH, int KW, int S,
                                     int P) {
-  return vlp_conv_fwd_act_ok(dtype, N, H, W, C, Co, KH, KW, S, P);
+  return dtype == VLP_BF16 && N >= 1 && rows_c64_ok(make_geom(N, H, W, C, Co, KH, KW, S, P)) ? 1 : 0;
 }
 
 VLP_EXPORT int vlp_conv_dgrad_bn_act(int dtype, const void* g_in, const void* y_in, const float* in_coef,
@@ -2132,6 +2415,7 @@ VLP_EXPORT int vlp_conv_dgrad_relu2(int dtype, const void* dy, const void* wt, v
   g1.K = g1.KH * g1.KW * g1.Co;
   EpiDgradRelu2<bf16> ep{stat1, stat2, stat_rep, stat3, (bf16*)g, (const bf16*)addend, g1.C, relu_mask,
                          (const bf16*)y, (const bf16*)yd, mean, invstd, meand, invstdd};
+  if (VLP_WIN && win_ok(g1, g1.Co, g1.C)) return launch_win<true>(g1, g1.Co, g1.C, dy, wt, ep, (hipStream_t)stream);
   ConvDgradA<bf16> la{g1, (const bf16*)dy};
   KMat<bf16> lb{(const bf16*)wt, g1.K, g1.C, g1.K};
   return gemm_auto<bf16>(g1.M, g1.C, g1.K, 1, la, lb, ep, (hipStream_t)stream);

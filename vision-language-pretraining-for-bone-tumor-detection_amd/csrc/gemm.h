@@ -1360,6 +1360,11 @@ constexpr int big_lds_bytes() {
 #ifndef VLP_PP_PRIO
 #define VLP_PP_PRIO 1
 #endif
+// timing experiments only (wrong results): 1 = no LDS-DMA issue, 2 = no fragment
+// reads, 3 = no MFMAs (tools/build_variant.sh; never in the product library)
+#ifndef VLP_PP_EXP
+#define VLP_PP_EXP 0
+#endif
 __device__ __forceinline__ int pp_chunk(int r, int c) { return c ^ (((r >> 3) & 1) << 1); }
 template <int BM, class L, int NTG, bool KC = L::kKContig>
 struct HStager;
@@ -1502,7 +1507,10 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
     if constexpr (G == 0) ss.init(la, row0, kb, wg);
     else ss.init(lb, col0, kb, wg);
     auto fetch = [&](auto hc, int u, char* slot) __attribute__((always_inline)) {
-      const int k0 = kperm_of(la, kb + (u >> 1) * BK);
+      if constexpr (VLP_PP_EXP == 1) return;
+      if constexpr (VLP_PP_EXP == 6 && G == 0) if (((u >> 1) % 9) != 0) return;   // A bytes / 9
+      if constexpr (VLP_PP_EXP == 7 && G == 1) if (((u >> 1) % 9) != 0) return;   // B bytes / 9
+      const int k0 = VLP_PP_EXP == 5 ? kb + (u >> 1) * BK : kperm_of(la, kb + (u >> 1) * BK);
       if constexpr (G == 0) ss.template issue<decltype(hc)::value>(la, u < nh ? ra : rz, k0, slot, wg);
       else ss.template issue<decltype(hc)::value>(lb, u < nh ? rb : rz, k0, slot + HA, wg);
     };
@@ -1526,6 +1534,12 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
       constexpr int SL = decltype(slc)::value;
       constexpr int SO = (SL & 1) * SLOT;   // offset inside the slot pair
       v8bf fa[MB], fb[NB];
+      if constexpr (VLP_PP_EXP == 2) {
+#pragma unroll
+        for (int a = 0; a < MB; ++a) fa[a] = v8bf{};
+#pragma unroll
+        for (int b = 0; b < NB; ++b) fb[b] = v8bf{};
+      } else {
       static_for<0, MB>([&](auto ac) {
         constexpr int a = decltype(ac)::value;
         if constexpr (LA::kKContig)
@@ -1540,6 +1554,7 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
         else
           fb[b] = frag_tr_at<SO + (b >> 2) * 1024>(bbase[SL >> 1][b & 3]);
       });
+      }
       v4f xs0, xs1, xh0, xh1;
       unsigned xtap = 0;
       if constexpr (XA) {
@@ -1568,11 +1583,26 @@ gemm_pp_kernel(GemmShape sh, LA la, LB lb, EP ep) {
 #pragma unroll
         for (int a = 0; a < MB; ++a) fa[a] = bn_relu_frag(fa[a], xs0, xs1, xh0, xh1, (xm[a / 3] >> (xtap + 9 * (a % 3))) & 1u);
       }
+      if constexpr (VLP_PP_EXP == 4 && NB == 4) {   // 32x32x16 issue pattern (wrong layout)
+        typedef float v16f_ __attribute__((ext_vector_type(16)));
+#pragma unroll
+        for (int a = 0; a < MB; ++a) {
+          v16f_ t = *reinterpret_cast<v16f_*>(&acc[a][0]);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[a & 3], fa[a], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[(a + 1) & 3], fa[a], t, 0, 0, 0);
+          *reinterpret_cast<v16f_*>(&acc[a][0]) = t;
+        }
+      } else if constexpr (VLP_PP_EXP != 3) {
 #pragma unroll
       for (int a = 0; a < MB; ++a)
 #pragma unroll
         for (int b = 0; b < NB; ++b)
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], acc[a][b], 0, 0, 0);
+      } else {
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+        acc[a][0][0] += (float)fa[a][0] + (float)fb[0][0];
+      }
 #if VLP_PP_PRIO
       __builtin_amdgcn_s_setprio(0);
 #endif
