@@ -1744,7 +1744,25 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
     const int hh = h0 - 1 + wr, ww = wc - 1;
     const bool ok = c < 8 && p < WG::WR * WG::WC && hh >= 0 && hh < H && ww >= 0 && ww < TW;
     woff[i] = ok ? (unsigned)((((n * H + hh) * TW + ww) * C) * 2 + c * 16) : kOOB;
+    // XF 1: the window's two spare pieces (wave 7's last two) carry the chunk's
+    // 64 BN scales / shifts (lanes 0-15, 16 B each) into the window buffer
+    if (XF == 1 && wv == 7 && i >= PPW - 2) woff[i] = lane < 16 ? (unsigned)lane * 16u : kOOB;
   }
+  const rsrc_t rsc = XF == 1 ? buf_rsrc(xin.sc, (unsigned)C * 4u) : rz;
+  const rsrc_t rsh = XF == 1 ? buf_rsrc(xin.sh, (unsigned)C * 4u) : rz;
+  // window piece i of chunk cc into buffer wb (chunk cc >= NC: zeros)
+  auto wpiece = [&](auto ic, int cc, char* wb) __attribute__((always_inline)) {
+    constexpr int I = decltype(ic)::value;
+    rsrc_t r = cc < NC ? rx : rz;
+    unsigned inc = 128u;
+    if constexpr (XF == 1 && I >= PPW - 2) {
+      if (wv == 7) {
+        r = cc < NC ? (I == PPW - 2 ? rsc : rsh) : rz;
+        inc = 256u;
+      }
+    }
+    dma16(r, woff[I] + (unsigned)cc * inc, wb + (wv * PPW + I) * 1024);
+  };
   SB sb;
   sb.init(lb, col0, 0, wv);
   // B half-tile hc of tap t, channel chunk cc (cc == NC: past the end, zeros)
@@ -1764,31 +1782,62 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
   const int wpx = wm * 64;   // the wave's first pixel in the tile
   const char* const bbase = ring + li * 64 + (pp_chunk(li, lg) << 4) + wn * WTN * 64;
 
-  // XF 1: this thread's own pieces of window cc (landed) -> relu(sc * x + sh) in
-  // place, the tile's own pixels to xin.out (one N tile writes them)
-  auto xform = [&](int cc, char* wb) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      if (woff[i] == kOOB) continue;
-      const int off = (wv * PPW + i) * 1024 + lane * 16;
-      const int p = off / WG::PS;
-      const int wr = p / WG::WC;
-      const int c0 = cc * 64 + ((off - p * WG::PS) >> 4) * 8;
-      uint4* q = reinterpret_cast<uint4*>(wb + off);
+  // XF 1: element k of a window for this thread = 16-B chunk c16 = tid & 7 of
+  // window pixel (tid >> 3) + 64 k; interior pixels become relu(sc * x + sh) in
+  // place (the zero padding stays zero), k = 0 .. KX-1.  The transform of window
+  // cc+1 runs one element per half-step over half-steps X0 .. X0+KX-1 of chunk cc
+  // (all pieces landed and visible from half-step PPW + 1), the stores of the
+  // tile's own pixels to xin.out over half-steps 1 .. KX of chunk cc+1 (read back
+  // from the window; one N tile stores).
+  constexpr int KX = (WG::WR * WG::WC + 63) / 64;
+  constexpr int X0 = PPW + 1;
+  static_assert(XF == 0 || (X0 + KX <= 17 && KX <= 16 && (WG::BYTES + 1023) / 1024 <= 8 * PPW - 2), "XF schedule");
+  const int c16 = tid & 7;
+  v4f xs0, xs1, xh0, xh1;
+  auto xcoef = [&](const char* wb) __attribute__((always_inline)) {
+    const float* t = reinterpret_cast<const float*>(wb + (8 * PPW - 2) * 1024) + c16 * 8;
+    xs0 = *reinterpret_cast<const v4f*>(t);
+    xs1 = *reinterpret_cast<const v4f*>(t + 4);
+    xh0 = *reinterpret_cast<const v4f*>(t + 256);
+    xh1 = *reinterpret_cast<const v4f*>(t + 260);
+  };
+  // window pixel of element k -> (inside the image, inside the tile's rows)
+  auto xpix = [&](int k, bool& img, bool& own) __attribute__((always_inline)) {
+    int t = tid;
+    asm volatile("" : "+v"(t));   // recomputed where used: not hoisted into registers across the chunk loop
+    const int p = (t >> 3) + 64 * k;
+    const int wr = p / WG::WC, wc = p - wr * WG::WC;
+    const int hh = h0 - 1 + wr;
+    img = p < WG::WR * WG::WC && hh >= 0 && hh < H && wc >= 1 && wc <= TW;
+    own = img && wr >= 1 && wr <= WG::TH;
+    return p;
+  };
+  auto xelem = [&](int k, char* wb) __attribute__((always_inline)) {
+    bool img, own;
+    const int p = xpix(k, img, own);
+    if (img) {
+      uint4* q = reinterpret_cast<uint4*>(wb + p * WG::PS + c16 * 16);
       float f[8];
       Chunk<bf16>::unpack(*q, f);
-      const v4f s0 = *reinterpret_cast<const v4f*>(xin.sc + c0), s1 = *reinterpret_cast<const v4f*>(xin.sc + c0 + 4);
-      const v4f t0 = *reinterpret_cast<const v4f*>(xin.sh + c0), t1 = *reinterpret_cast<const v4f*>(xin.sh + c0 + 4);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        f[j] = fmaxf(fmaf(f[j], s0[j], t0[j]), 0.f);
-        f[4 + j] = fmaxf(fmaf(f[4 + j], s1[j], t1[j]), 0.f);
+        f[j] = fmaxf(fmaf(f[j], xs0[j], xh0[j]), 0.f);
+        f[4 + j] = fmaxf(fmaf(f[4 + j], xs1[j], xh1[j]), 0.f);
       }
-      const uint4 v = Chunk<bf16>::pack(f);
-      *q = v;
-      if (tn == 0 && wr >= 1 && wr <= WG::TH) stg16(reinterpret_cast<char*>(xin.out) + woff[i] + (unsigned)cc * 128u, v);
+      *q = Chunk<bf16>::pack(f);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  // one buffer store per thread and half-step whatever the lane's pixel (others
+  // past the resource: dropped), so every wave's vmcnt bookkeeping is the same
+  const rsrc_t rxo = XF == 1 ? buf_rsrc(xin.out, xbytes) : rz;
+  auto xstore = [&](int k, int cc, const char* wb) __attribute__((always_inline)) {
+    bool img, own;
+    const int p = xpix(k, img, own);
+    const int wr = p / WG::WC, wc = p - wr * WG::WC;
+    const unsigned e = (unsigned)((((n * H + h0 - 1 + wr) * TW + (wc - 1)) * C + cc * 64 + c16 * 8) * 2);
+    typedef unsigned v4u_ __attribute__((__vector_size__(16)));
+    const v4u_ v = *reinterpret_cast<const v4u_*>(wb + p * WG::PS + c16 * 16);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rxo, own && tn == 0 ? e : kOOB, 0, 0);
   };
   // fragments of half-step (tap t, half hh) from window buffer wb, ring slot sl
   v8bf fa[2][MB], fb[2][NB];
@@ -1809,14 +1858,19 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
   using H0 = std::integral_constant<int, 0>;
   using H1 = std::integral_constant<int, 1>;
   using Z = std::integral_constant<int, 0>;
-#pragma unroll
-  for (int i = 0; i < PPW; ++i) dma16(rx, woff[i], win + (wv * PPW + i) * 1024);
+  static_for<0, PPW>([&](auto ic) { wpiece(ic, 0, win); });
   bfetch(H0{}, 0, 0, ring);
   bfetch(H1{}, 0, 0, ring + BSLOT);
   bfetch(H0{}, 1, 0, ring + 2 * BSLOT);
   wait_vmcnt<2 * SB::P>();   // window 0 and B(0)
-  if constexpr (XF == 1) xform(0, win);
   raw_barrier();
+  if constexpr (XF == 1) {
+    xcoef(win);
+#pragma unroll
+    for (int k = 0; k < KX; ++k) xelem(k, win);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
+  }
   rd(Z{}, Z{}, win, 0);
 
   // one 64-channel chunk; PC (= cc & 1) selects the window buffer.  Half-step
@@ -1827,21 +1881,22 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
     constexpr int PC = decltype(pc)::value;
     char* const wbuf = win + PC * WG::SLOT;
     char* const wnext = win + (1 - PC) * WG::SLOT;
-    const rsrc_t rn = cc + 1 < NC ? rx : rz;
     static_for<0, 18>([&](auto sc_) {
       constexpr int S = decltype(sc_)::value;
       constexpr int R = S & 1;
       constexpr int SL = (S + 2 * PC) & 3;
       // B(u+1) landed: issued after it are the previous half-step's window piece
       // (half-steps 1..PPW) and B(u+2)
-      if constexpr (S >= 1 && S <= PPW) wait_vmcnt<SB::P + 1>();
-      else wait_vmcnt<SB::P>();
-      if constexpr (XF == 1 && S == 17) {
-        if (cc + 1 < NC) xform(cc + 1, wnext);   // window cc+1 landed by half-step PPW + 1
-      }
+      // (XF 1: and its x_act store, half-steps 2 .. KX+1; vmcnt retires in issue order)
+      constexpr int NPRE = (S >= 1 && S <= PPW ? 1 : 0) + (XF == 1 && S >= 2 && S <= KX + 1 ? 1 : 0);
+      wait_vmcnt<SB::P + NPRE>();
+      if constexpr (XF == 1 && S == 17) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // transformed window cc+1
       if constexpr (VLP_WIN_EXP != 5) raw_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (S < PPW && VLP_WIN_EXP != 2 && VLP_WIN_EXP != 3) dma16(rn, woff[S] + (unsigned)(cc + 1) * 128u, wnext + (wv * PPW + S) * 1024);
+      if constexpr (S < PPW && VLP_WIN_EXP != 2 && VLP_WIN_EXP != 3) wpiece(std::integral_constant<int, S < PPW ? S : 0>{}, cc + 1, wnext);
+      // XF 1: the stores of window cc's own pixels, one element per half-step
+      // (issued right after the barrier: the next half-step's wait retires them)
+      if constexpr (XF == 1 && S >= 1 && S <= KX) xstore(S - 1, cc, wbuf);
       constexpr int S3 = S + 3 < 18 ? S + 3 : S + 3 - 18;   // half-step u + 3 = (chunk, S3)
       bfetch(std::integral_constant<int, S3 & 1>{}, S3 >> 1, S + 3 < 18 ? cc : cc + 1, ring + ((SL + 3) & 3) * BSLOT);
       if constexpr (S + 1 < 18) rd(std::integral_constant<int, 1 - R>{}, std::integral_constant<int, S + 1>{}, wbuf, (SL + 1) & 3);
@@ -1864,6 +1919,12 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
       __builtin_amdgcn_s_setprio(0);
 #endif
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (XF == 1 && S >= X0 && S < X0 + KX) {
+        if (cc + 1 < NC) {
+          if constexpr (S == X0) xcoef(wnext);
+          xelem(S - X0, wnext);
+        }
+      }
     });
   };
   for (int cc = 0; cc < NC; cc += 2) {
@@ -1878,8 +1939,20 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
 
 // 3x3 / stride 1 / pad 1 with C and the GEMM N both multiples of 128, 256-pixel
 // tiles of whole rows, widths 16 / 32 / 64 (ResNet34 layers 2-4 at 512 x 512)
+// image widths routed to the window kernel (bit W / 16): r5 A/B at the bench
+// shapes (profiles/r5w_window_ab.txt) -- layer 2 (W 64) -8..-16 %, layer 4 (W 16)
+// -1..-3 %, layer 3 (W 32) +1..+7 % against the 256 x 256 ping-pong tiles
+#ifndef VLP_WIN_WIDTHS
+#define VLP_WIN_WIDTHS ((1 << 1) | (1 << 4))
+#endif
+// BN-apply + ReLU of the input in the window (vlp_conv_fwd_act for layers 2-4):
+// off -- r5 A/B: the in-window transform costs more than the separate pass
+#ifndef VLP_WIN_ACT
+#define VLP_WIN_ACT 0
+#endif
 static bool win_ok(const ConvGeom& g, int cin, int nout) {
   return g.KH == 3 && g.KW == 3 && g.S == 1 && g.P == 1 && (g.W == 16 || g.W == 32 || g.W == 64) &&
+         ((VLP_WIN_WIDTHS >> (g.W / 16)) & 1) &&
          g.H % (256 / g.W) == 0 && cin % 128 == 0 && nout % 128 == 0 &&
          (size_t)g.N * g.H * g.W * cin * 2 < (1ull << 31);
 }
@@ -2283,7 +2356,7 @@ VLP_EXPORT int vlp_conv_fwd_act_ok(int dtype, int N, int H, int W, int C, int Co
                                   int P) {
   if (dtype != VLP_BF16 || N < 1) return 0;
   const ConvGeom g = make_geom(N, H, W, C, Co, KH, KW, S, P);
-  return rows_c64_ok(g) || (VLP_WIN && win_ok(g, C, Co)) ? 1 : 0;
+  return rows_c64_ok(g) || (VLP_WIN && VLP_WIN_ACT && win_ok(g, C, Co)) ? 1 : 0;
 }
 
 VLP_EXPORT int vlp_conv_fwd_act(int dtype, const void* x, const void* wp, void* y, void* x_act, int N,
