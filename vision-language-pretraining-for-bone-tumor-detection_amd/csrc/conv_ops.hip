@@ -1681,39 +1681,53 @@ static int launch_rows_c64(const ConvGeom& g, const void* x, const void* w, int 
 #ifndef VLP_WIN_EXP
 #define VLP_WIN_EXP 0
 #endif
-template <int TW>
+#ifndef VLP_WIN_NW
+#define VLP_WIN_NW 8   // waves per window workgroup (8: two per SIMD; 4: one per SIMD, 128 x 64 per wave)
+#endif
+#ifndef VLP_WIN_STAMP
+#define VLP_WIN_STAMP 0   // diagnostic build: in-kernel s_memtime stamps (tools/build_variant.sh)
+#endif
+template <int TW, int NW = 8>
 struct WinGeom {
   static constexpr int TH = 256 / TW;                  // image rows per tile
   static constexpr int WR = TH + 2, WC = TW + 2;       // window rows / columns
   static constexpr int PS = 160;                       // LDS bytes per window pixel
   static constexpr int BYTES = WR * WC * PS;
-  static constexpr int PPW = ((BYTES + 1023) / 1024 + 7) / 8;   // 1-KiB pieces per wave
-  static constexpr int SLOT = PPW * 8 * 1024;          // one window buffer
+  static constexpr int PPW = ((BYTES + 1023) / 1024 + NW - 1) / NW;   // 1-KiB pieces per wave
+  static constexpr int SLOT = PPW * NW * 1024;         // one window buffer
 };
 struct WinXIn {
   const float* sc; const float* sh;   // XF 1: per-channel BN scale / shift of the input
   bf16* out;                          // XF 1: relu(sc * x + sh) of the tile's pixels
 };
-template <int TW, int BN>
-constexpr int win_lds_bytes() { return 2 * WinGeom<TW>::SLOT + 4 * BN * 64; }
+template <int TW, int BN, int NW = 8>
+constexpr int win_lds_bytes() { return 2 * WinGeom<TW, NW>::SLOT + 4 * BN * 64; }
 
-template <int TW, int BN, bool FLIP, int XF, class EP>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+// NW = 8: 4 x 2 waves of 64 x BN/2, two waves per SIMD; NW = 4: 2 x 2 waves of
+// 128 x BN/2, one wave per SIMD (up to 512 registers: operand sets
+// double-buffered, half the LDS fragment reads per MFMA)
+template <int TW, int BN, int NW, bool FLIP, int XF, class EP>
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 8 ? 2 : 1)))
 conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsigned xbytes, KMat<bf16> lb, EP ep,
                    WinXIn xin) {
-  using WG = WinGeom<TW>;
-  constexpr int BM = 256, WGM = 4, WGN = 2, NT = 512;
+  using WG = WinGeom<TW, NW>;
+  constexpr int BM = 256, WGN = 2, WGM = NW / WGN, NT = NW * 64;
   constexpr int WTN = BN / WGN;
-  constexpr int MB = 4, NB = WTN / 16;
+  constexpr int MB = BM / WGM / 16, NB = WTN / 16;
   constexpr int BSLOT = BN * 64;
   constexpr int PPW = WG::PPW;
   using SB = HStager<BN, KMat<bf16>, NT>;
+  static_assert(XF == 0 || NW == 8, "the in-window transform schedule assumes 8 waves");
   static_assert(PPW <= 16, "window pieces are issued over the first half-steps of a chunk");
-  static_assert(win_lds_bytes<TW, BN>() <= 160 * 1024 && BM * BN * 2 + 4096 <= win_lds_bytes<TW, BN>(), "LDS budget");
+  static_assert(win_lds_bytes<TW, BN, NW>() <= 160 * 1024 && BM * BN * 2 + 4096 <= win_lds_bytes<TW, BN, NW>(),
+                "LDS budget");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const win = smem;
   char* const ring = smem + 2 * WG::SLOT;
 
+#if VLP_WIN_STAMP
+  const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+#endif
   const int nwg = sh.tiles_m * sh.tiles_n;
   const int bid = blockIdx.x;
   int g = bid;
@@ -1746,7 +1760,7 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
     woff[i] = ok ? (unsigned)((((n * H + hh) * TW + ww) * C) * 2 + c * 16) : kOOB;
     // XF 1: the window's two spare pieces (wave 7's last two) carry the chunk's
     // 64 BN scales / shifts (lanes 0-15, 16 B each) into the window buffer
-    if (XF == 1 && wv == 7 && i >= PPW - 2) woff[i] = lane < 16 ? (unsigned)lane * 16u : kOOB;
+    if (XF == 1 && wv == NW - 1 && i >= PPW - 2) woff[i] = lane < 16 ? (unsigned)lane * 16u : kOOB;
   }
   const rsrc_t rsc = XF == 1 ? buf_rsrc(xin.sc, (unsigned)C * 4u) : rz;
   const rsrc_t rsh = XF == 1 ? buf_rsrc(xin.sh, (unsigned)C * 4u) : rz;
@@ -1756,7 +1770,7 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
     rsrc_t r = cc < NC ? rx : rz;
     unsigned inc = 128u;
     if constexpr (XF == 1 && I >= PPW - 2) {
-      if (wv == 7) {
+      if (wv == NW - 1) {
         r = cc < NC ? (I == PPW - 2 ? rsc : rsh) : rz;
         inc = 256u;
       }
@@ -1779,7 +1793,7 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
   // A fragment of lane (li, lg): pixel li of the fragment's 16, 16-B chunk lg
   // of the half-step's 32 channels (tap and half: compile-time offsets)
   const int aoff = li * WG::PS + lg * 16;
-  const int wpx = wm * 64;   // the wave's first pixel in the tile
+  const int wpx = wm * (BM / WGM);   // the wave's first pixel in the tile
   const char* const bbase = ring + li * 64 + (pp_chunk(li, lg) << 4) + wn * WTN * 64;
 
   // XF 1: element k of a window for this thread = 16-B chunk c16 = tid & 7 of
@@ -1934,7 +1948,17 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
   wait_vmcnt<0>();
   __syncthreads();   // ring and windows drained (incl. the null-resource tail fetches) before LDS is reused
   if constexpr (VLP_WIN_EXP == 6) if (sh.dbg != 7) return;
+#if VLP_WIN_STAMP
+  const unsigned long long t_loop = __builtin_amdgcn_s_memtime();
+#endif
   ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep, acc, row0, col0, g, wm, wn, smem);
+#if VLP_WIN_STAMP
+  __syncthreads();
+  if (XF == 0 && threadIdx.x == 0) {
+    unsigned long long* st = reinterpret_cast<unsigned long long*>(xin.out) + (size_t)bid * 4;
+    st[0] = t_start; st[1] = t_loop; st[2] = __builtin_amdgcn_s_memtime(); st[3] = __builtin_amdgcn_s_memrealtime();
+  }
+#endif
 }
 
 // 3x3 / stride 1 / pad 1 with C and the GEMM N both multiples of 128, 256-pixel
@@ -1960,9 +1984,10 @@ template <int TW, bool FLIP, int XF, class EP>
 static int launch_win_t(const ConvGeom& g, int cin, int nout, const void* x, const void* w, const EP& ep,
                         hipStream_t st, const WinXIn& xin) {
   constexpr int BN = 128;
-  constexpr int lds = win_lds_bytes<TW, BN>();
+  constexpr int NW = XF == 1 ? 8 : VLP_WIN_NW;
+  constexpr int lds = win_lds_bytes<TW, BN, NW>();
   static KernelDevState kst;
-  const int e = prepare_kernel(kst, (const void*)&conv3x3_win_kernel<TW, BN, FLIP, XF, EP>, lds, 0, nullptr);
+  const int e = prepare_kernel(kst, (const void*)&conv3x3_win_kernel<TW, BN, NW, FLIP, XF, EP>, lds, 0, nullptr);
   if (e) return e;
   GemmShape sh;
   sh.M = g.N * g.H * g.W;
@@ -1975,8 +2000,37 @@ static int launch_win_t(const ConvGeom& g, int cin, int nout, const void* x, con
   sh.dbg = 0;
   sh.nsplit = 1;
   KMat<bf16> lb{(const bf16*)w, sh.K, nout, sh.K};
-  hipLaunchKernelGGL((conv3x3_win_kernel<TW, BN, FLIP, XF, EP>), dim3(sh.tiles_m * sh.tiles_n), dim3(512), lds, st, sh,
+#if VLP_WIN_STAMP
+  // diagnostic build: per-workgroup s_memtime stamps (start, main loop done,
+  // epilogue done), medians printed to stderr after each launch
+  static unsigned long long* dbuf = nullptr;
+  const int nb = sh.tiles_m * sh.tiles_n;
+  if (!dbuf) (void)hipMalloc(&dbuf, (size_t)65536 * 4 * 8);
+  WinXIn xs = xin;
+  if (XF == 0) xs.out = reinterpret_cast<bf16*>(dbuf);
+  hipLaunchKernelGGL((conv3x3_win_kernel<TW, BN, NW, FLIP, XF, EP>), dim3(nb), dim3(NW * 64), lds, st, sh,
+                     g.H, cin, (const bf16*)x, (unsigned)((size_t)g.N * g.H * g.W * cin * 2), lb, ep, xs);
+  if (XF == 0 && nb <= 65536) {
+    (void)hipStreamSynchronize(st);
+    std::vector<unsigned long long> h((size_t)nb * 4);
+    (void)hipMemcpy(h.data(), dbuf, h.size() * 8, hipMemcpyDeviceToHost);
+    std::vector<double> a(nb), b(nb);
+    unsigned long long t0 = ~0ull, t1 = 0;
+    for (int i = 0; i < nb; ++i) {
+      a[i] = (double)(h[i * 4 + 1] - h[i * 4]);
+      b[i] = (double)(h[i * 4 + 2] - h[i * 4 + 1]);
+      t0 = std::min(t0, h[i * 4]);
+      t1 = std::max(t1, h[i * 4 + 2]);
+    }
+    std::sort(a.begin(), a.end());
+    std::sort(b.begin(), b.end());
+    fprintf(stderr, "win TW=%d flip=%d wg=%d: main loop median %.0f cyc (p90 %.0f), epilogue median %.0f cyc (p90 %.0f), span %llu cyc\n",
+            TW, (int)FLIP, nb, a[nb / 2], a[nb * 9 / 10], b[nb / 2], b[nb * 9 / 10], t1 - t0);
+  }
+#else
+  hipLaunchKernelGGL((conv3x3_win_kernel<TW, BN, NW, FLIP, XF, EP>), dim3(sh.tiles_m * sh.tiles_n), dim3(NW * 64), lds, st, sh,
                      g.H, cin, (const bf16*)x, (unsigned)((size_t)g.N * g.H * g.W * cin * 2), lb, ep, xin);
+#endif
   return (int)hipGetLastError();
 }
 #ifndef VLP_WIN
