@@ -957,6 +957,10 @@ struct EpiDgradBN {
   }
   static constexpr bool kRow = true;
   __device__ void pre8(int row, int col, RowPre& p) const { p.u[0] = ldg16(y + (size_t)row * C + col); }
+  // y may come from an LDS image of the tile (the window kernel stages it during the last chunk)
+  static constexpr int kLdsSlot = 0;
+  __device__ const T* lds_operand() const { return y; }
+  __device__ void pre8_rest(int, int, RowPre&) const {}
   // per-channel coefficient arrays (a caller may stage them in LDS: row8 with lds_fp)
   static constexpr int kCoefs = 4;
   __device__ const float* coef(int k) const { return k == 0 ? sc : k == 1 ? sh : k == 2 ? mean : invstd; }
@@ -1101,6 +1105,19 @@ struct EpiDgradRelu {
       p.u[1] = ldg16(relu_out + o);
     }
     p.u[2] = ldg16(y + o);
+  }
+  // y could come from LDS as EpiDgradBN's does (kLdsSlot = 2 + lds_operand()); measured
+  // slower (layer 2 504 -> 528 us, profiles/r5l_lds_operand_ab.txt): the addend and the
+  // mask still make the epilogue wait on global loads, now behind 64 KB more DMA
+  static constexpr int kLdsSlotOff = 2;
+  __device__ void pre8_rest(int row, int col, RowPre& p) const {
+    const size_t o = (size_t)row * C + col;
+    p.u[0] = addend ? ldg16(addend + o) : zero4();
+    if constexpr (BITS) {
+      p.u[1].x = rmask[o >> 3];
+    } else {
+      p.u[1] = ldg16(relu_out + o);
+    }
   }
   static constexpr int kCoefs = 2;
   __device__ const float* coef(int k) const { return k == 0 ? mean : invstd; }
@@ -1687,21 +1704,25 @@ static int launch_rows_c64(const ConvGeom& g, const void* x, const void* w, int 
 #ifndef VLP_WIN_STAMP
 #define VLP_WIN_STAMP 0   // diagnostic build: in-kernel s_memtime stamps (tools/build_variant.sh)
 #endif
-template <int TW, int NW = 8>
+template <int TW, int NW = 8, int MINP = 0>
 struct WinGeom {
   static constexpr int TH = 256 / TW;                  // image rows per tile
   static constexpr int WR = TH + 2, WC = TW + 2;       // window rows / columns
   static constexpr int PS = 160;                       // LDS bytes per window pixel
   static constexpr int BYTES = WR * WC * PS;
-  static constexpr int PPW = ((BYTES + 1023) / 1024 + NW - 1) / NW;   // 1-KiB pieces per wave
+  static constexpr int PPW0 = ((BYTES + 1023) / 1024 + NW - 1) / NW;
+  // 1-KiB pieces per wave (MINP: at least that many pieces per buffer -- 64 when the
+  // epilogue's operand tile [256][128] bf16 is staged in the spare buffer)
+  static constexpr int PPW = PPW0 * NW >= MINP ? PPW0 : (MINP + NW - 1) / NW;
   static constexpr int SLOT = PPW * NW * 1024;         // one window buffer
 };
 struct WinXIn {
   const float* sc; const float* sh;   // XF 1: per-channel BN scale / shift of the input
   bf16* out;                          // XF 1: relu(sc * x + sh) of the tile's pixels
 };
-template <int TW, int BN, int NW = 8>
-constexpr int win_lds_bytes() { return 2 * WinGeom<TW, NW>::SLOT + 4 * BN * 64; }
+template <class EP> constexpr int win_minp() { return LdsSlotTrait<EP>::value >= 0 ? 64 : 0; }
+template <int TW, int BN, int NW = 8, int MINP = 0>
+constexpr int win_lds_bytes() { return 2 * WinGeom<TW, NW, MINP>::SLOT + 4 * BN * 64; }
 
 // NW = 8: 4 x 2 waves of 64 x BN/2, two waves per SIMD; NW = 4: 2 x 2 waves of
 // 128 x BN/2, one wave per SIMD (up to 512 registers: operand sets
@@ -1710,8 +1731,10 @@ template <int TW, int BN, int NW, bool FLIP, int XF, class EP>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 8 ? 2 : 1)))
 conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsigned xbytes, KMat<bf16> lb, EP ep,
                    WinXIn xin) {
-  using WG = WinGeom<TW, NW>;
+  constexpr int LS = LdsSlotTrait<EP>::value;
+  using WG = WinGeom<TW, NW, win_minp<EP>()>;
   constexpr int BM = 256, WGN = 2, WGM = NW / WGN, NT = NW * 64;
+  static_assert(LS < 0 || BN == 128, "the staged epilogue operand is a [256][128] bf16 image");
   constexpr int WTN = BN / WGN;
   constexpr int MB = BM / WGM / 16, NB = WTN / 16;
   constexpr int BSLOT = BN * 64;
@@ -1719,7 +1742,8 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
   using SB = HStager<BN, KMat<bf16>, NT>;
   static_assert(XF == 0 || NW == 8, "the in-window transform schedule assumes 8 waves");
   static_assert(PPW <= 16, "window pieces are issued over the first half-steps of a chunk");
-  static_assert(win_lds_bytes<TW, BN, NW>() <= 160 * 1024 && BM * BN * 2 + 4096 <= win_lds_bytes<TW, BN, NW>(),
+  static_assert(win_lds_bytes<TW, BN, NW, win_minp<EP>()>() <= 160 * 1024 &&
+                    BM * BN * 2 + 4096 <= win_lds_bytes<TW, BN, NW, win_minp<EP>()>(),
                 "LDS budget");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const win = smem;
@@ -1764,9 +1788,22 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
   }
   const rsrc_t rsc = XF == 1 ? buf_rsrc(xin.sc, (unsigned)C * 4u) : rz;
   const rsrc_t rsh = XF == 1 ? buf_rsrc(xin.sh, (unsigned)C * 4u) : rz;
+  // LS >= 0: the pieces of "chunk NC" (issued during the last chunk into its spare
+  // buffer) fetch the epilogue's operand tile instead, [256 rows][256 B] from
+  // rows row0.., columns col0..col0+127 of the [M][sh.N] operand
+  rsrc_t rop = rz;
+  if constexpr (LS >= 0) rop = buf_rsrc(ep.lds_operand(), (unsigned)((size_t)sh.M * sh.N * 2));
   // window piece i of chunk cc into buffer wb (chunk cc >= NC: zeros)
   auto wpiece = [&](auto ic, int cc, char* wb) __attribute__((always_inline)) {
     constexpr int I = decltype(ic)::value;
+    if constexpr (LS >= 0) {
+      if (cc == NC) {
+        const int j = wv * PPW + I, row = j * 4 + (lane >> 4);
+        const unsigned o = row < BM ? (unsigned)(((row0 + row) * sh.N + col0) * 2 + (lane & 15) * 16) : kOOB;
+        dma16(rop, o, wb + j * 1024);
+        return;
+      }
+    }
     rsrc_t r = cc < NC ? rx : rz;
     unsigned inc = 128u;
     if constexpr (XF == 1 && I >= PPW - 2) {
@@ -1951,7 +1988,13 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
 #if VLP_WIN_STAMP
   const unsigned long long t_loop = __builtin_amdgcn_s_memtime();
 #endif
-  ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep, acc, row0, col0, g, wm, wn, smem);
+  if constexpr (LS >= 0) {
+    // NC is even: the last chunk read buffer 1, its spare buffer 0 holds the operand
+    // tile; the staging tile goes to buffer 1 (+ the free ring)
+    ms_epilogue<BM, BN, WGM, WGN, EP, true>(sh, ep, acc, row0, col0, g, wm, wn, smem + WG::SLOT, smem);
+  } else {
+    ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep, acc, row0, col0, g, wm, wn, smem);
+  }
 #if VLP_WIN_STAMP
   __syncthreads();
   if (XF == 0 && threadIdx.x == 0) {
@@ -1985,7 +2028,7 @@ static int launch_win_t(const ConvGeom& g, int cin, int nout, const void* x, con
                         hipStream_t st, const WinXIn& xin) {
   constexpr int BN = 128;
   constexpr int NW = XF == 1 ? 8 : VLP_WIN_NW;
-  constexpr int lds = win_lds_bytes<TW, BN, NW>();
+  constexpr int lds = win_lds_bytes<TW, BN, NW, win_minp<EP>()>();
   static KernelDevState kst;
   const int e = prepare_kernel(kst, (const void*)&conv3x3_win_kernel<TW, BN, NW, FLIP, XF, EP>, lds, 0, nullptr);
   if (e) return e;

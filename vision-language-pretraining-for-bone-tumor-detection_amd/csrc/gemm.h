@@ -228,6 +228,12 @@ template <class E> struct StageBiasTrait<E, std::void_t<decltype(E::kStageBias)>
 };
 template <class E, class = void> struct CoefTrait { static constexpr int value = 0; };
 template <class E> struct CoefTrait<E, std::void_t<decltype(E::kCoefs)>> { static constexpr int value = E::kCoefs; };
+// row epilogues whose operand u[E::kLdsSlot] (a [rows][C] bf16 tensor, E::lds_operand())
+// a kernel may stage into LDS as the tile's [BM][BN] image ahead of the epilogue
+template <class E, class = void> struct LdsSlotTrait { static constexpr int value = -1; };
+template <class E> struct LdsSlotTrait<E, std::void_t<decltype(E::kLdsSlot)>> {
+  static constexpr int value = E::kLdsSlot;
+};
 template <class E, class = void> struct PreDepthTrait { static constexpr int value = 8; };
 template <class E> struct PreDepthTrait<E, std::void_t<decltype(E::kPreDepth)>> {
   static constexpr int value = E::kPreDepth;
@@ -648,11 +654,18 @@ __device__ __forceinline__ double* stat3_of(const EP& ep) {
   else return nullptr;
 }
 
+// timing experiments only (wrong results): 1 = staged epilogues skip their
+// global stores, 2 = staged epilogues skip the statistics reduction + atomics,
+// 3 = row epilogues skip their operand loads (pre8)
+#ifndef VLP_EPI_EXP
+#define VLP_EPI_EXP 0
+#endif
 // Epilogue shared by the multi-stage kernels: lane l = 16g + i owns
 // C[row = rbase + i][col = cbase + 4g .. 4g+3] of each 16x16 block.
-template <int BM, int BN, int WGM, int WGN, class EP, int MB, int NB>
+template <int BM, int BN, int WGM, int WGN, class EP, bool LP = false, int MB, int NB>
 __device__ __forceinline__ void ms_epilogue(const GemmShape& sh, const EP& ep, v4f (&acc)[MB][NB], int row0,
-                                            int col0, int wid, int wm, int wn, char* smem) {
+                                            int col0, int wid, int wm, int wn, char* smem,
+                                            const char* lds_pre = nullptr) {
   constexpr int NT = WGM * WGN * 64;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   const int l = threadIdx.x & 63;
@@ -702,10 +715,18 @@ __device__ __forceinline__ void ms_epilogue(const GemmShape& sh, const EP& ep, v
     constexpr bool S3 = Stat3Trait<EP>::value;
     constexpr int NS = S3 ? 3 : 2;
     PreT pre[D];
+    // lds_pre: operand slot LS of every row is the caller's LDS image [BM rows][BN * 2 B]
+    // (all rows and columns of the tile valid), read at use; the other slots load here
+    constexpr int LS = LP ? LdsSlotTrait<EP>::value : -1;
+    static_assert(!LP || LS >= 0, "LDS operand staging needs E::kLdsSlot");
+    auto pre_load = [&](int row, PreT& p) __attribute__((always_inline)) {
+      if constexpr (LS >= 0) ep.pre8_rest(row, col, p);
+      else ep.pre8(row, col, p);
+    };
 #pragma unroll
     for (int i = 0; i < D; ++i) {
       const int r = r0 + i * RS;
-      if (cok && r < BM && row0 + r < sh.M) ep.pre8(row0 + r, col, pre[i]);
+      if (VLP_EPI_EXP != 3 && cok && r < BM && row0 + r < sh.M) pre_load(row0 + r, pre[i]);
     }
     float cf[NCF > 0 ? NCF : 1][8];
     if constexpr (NCF > 0) {
@@ -729,10 +750,11 @@ __device__ __forceinline__ void ms_epilogue(const GemmShape& sh, const EP& ep, v
     for (int i = 0; i < NIT; ++i) {
       const int r = r0 + i * RS;
       const int row = row0 + r;
-      const PreT cur = pre[i % D];
+      PreT cur = pre[i % D];
+      if constexpr (LS >= 0) cur.u[LS] = *reinterpret_cast<const uint4*>(lds_pre + r * (BN * 2) + c * 16);
       if (i + D < NIT) {
         const int rn = r + D * RS;
-        if (cok && rn < BM && row0 + rn < sh.M) ep.pre8(row0 + rn, col, pre[i % D]);
+        if (VLP_EPI_EXP != 3 && cok && rn < BM && row0 + rn < sh.M) pre_load(row0 + rn, pre[i % D]);
       }
       if (cok && r < BM && row < sh.M) {
         float v[8];
@@ -814,11 +836,11 @@ __device__ __forceinline__ void ms_epilogue(const GemmShape& sh, const EP& ep, v
     for (int q = threadIdx.x; q < BM * CPR; q += NT) {
       const int r = q / CPR, c = q - r * CPR;
       const int row = row0 + r, col = col0 + c * 8;
-      if (row < sh.M && col < sh.N)
+      if (VLP_EPI_EXP != 1 && row < sh.M && col < sh.N)
         ep.store8(row, col, *reinterpret_cast<const uint4*>(stg + r * BN + ((c ^ (r & (CPR - 1))) << 3)));
     }
   }
-  if constexpr (EP::kStats) {
+  if constexpr (EP::kStats && VLP_EPI_EXP != 2) {
     __syncthreads();
     const int rep = ep.stat_rep > 1 ? (wid % ep.stat_rep) : 0;
     for (int cl = threadIdx.x; cl < BN; cl += NT) {
