@@ -108,6 +108,29 @@ def test_conv_fwd(ops, dt, case, xform):
     assert rel(s2.cpu(), (ref * ref).sum((0, 2, 3))) < 1e-4
 
 
+@pytest.mark.parametrize("N,H,W,C,Co", [(32, 64, 64, 128, 128), (128, 16, 16, 512, 512)])
+def test_conv_fwd_persistent_window(ops, N, H, W, C, Co):
+    """The persistent forward of the LDS-window kernel (>= 2 tiles per CU, tile count a
+    multiple of 8: one workgroup per CU walks its XCD's tiles, the next tile's window
+    and filter slices loading over the epilogue) against torch fp32 on the GPU, with
+    the BN sums; every tile's output checked (the tile hand-over is where it breaks)."""
+    torch.manual_seed(21)
+    dev = torch.device("cuda")
+    x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
+    w = (torch.randn(Co, C, 3, 3, device=dev) * (9 * C) ** -0.5).to(torch.bfloat16)
+    wp = torch.empty(Co, 3, 3, C, dtype=torch.bfloat16, device=dev)
+    ops.pack_conv(w.float(), wp, None)
+    s1 = torch.zeros(4 * Co, dtype=torch.float64, device=dev)
+    s2 = torch.zeros_like(s1)
+    y = ops.conv_fwd(x, wp, Co, 3, 3, 1, 1, stat_sum=s1, stat_sumsq=s2, stat_rep=4)
+    ref = F.conv2d(x.permute(0, 3, 1, 2).float(), w.float(), padding=1).permute(0, 2, 3, 1)
+    torch.cuda.synchronize()
+    err = (y.float() - ref).reshape(-1, 256, Co).norm(dim=(1, 2)) / ref.reshape(-1, 256, Co).norm(dim=(1, 2))
+    assert err.max().item() < 1e-2, f"worst tile rel-L2 {err.max().item():.3e} at tile {err.argmax().item()}"
+    assert rel(s1.view(4, Co).sum(0).cpu(), ref.sum((0, 1, 2)).double().cpu()) < 1e-4
+    assert rel(s2.view(4, Co).sum(0).cpu(), (ref.double() ** 2).sum((0, 1, 2)).cpu()) < 1e-4
+
+
 @pytest.mark.parametrize("N,H,W,C", [(3, 5, 128, 64), (2, 128, 128, 64), (300, 4, 128, 64),
                                      (2, 8, 64, 128), (3, 16, 32, 256), (2, 16, 16, 512)])
 def test_conv_fwd_act_matches_pass_then_conv(ops, N, H, W, C):

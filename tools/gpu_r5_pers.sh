@@ -1,0 +1,13 @@
+# persistent window forward: op parity (incl. the persistent shapes), block parity,
+# interleaved timings against the -DVLP_WIN_PERSIST=0 library
+cd $GRAFT_REPO_ROOT
+T=${T:-r5p3}
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_ops.py -k "conv_fwd" > gpurun_out/${T}_ops.log 2>&1 || { echo OPS FAILED; tail -30 gpurun_out/${T}_ops.log; exit 1; }
+tail -1 gpurun_out/${T}_ops.log
+for r in 1 2; do
+timeout -k 10 200 python tools/conv_bench.py --ops fwd --layers l2,l4 --iters 20 > gpurun_out/${T}_cb_pers_$r.log 2>&1 || exit 1
+VLP_HIP_LIB=build_exp/nopers/libvlp_hip.so timeout -k 10 200 python tools/conv_bench.py --ops fwd --layers l2,l4 --iters 20 > gpurun_out/${T}_cb_nopers_$r.log 2>&1 || exit 1
+done
+for f in gpurun_out/${T}_cb_*.log; do echo "== $f"; grep TF/s $f; done
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_blocks.py > gpurun_out/${T}_blocks.log 2>&1 || { echo BLOCKS FAILED; tail -30 gpurun_out/${T}_blocks.log; exit 1; }
+tail -1 gpurun_out/${T}_blocks.log

@@ -1701,6 +1701,9 @@ static int launch_rows_c64(const ConvGeom& g, const void* x, const void* w, int 
 #ifndef VLP_WIN_NW
 #define VLP_WIN_NW 8   // waves per window workgroup (8: two per SIMD; 4: one per SIMD, 128 x 64 per wave)
 #endif
+#ifndef VLP_WIN_PERSIST
+#define VLP_WIN_PERSIST 1   // forward: one workgroup per CU walks its tiles, the next tile's loads over the epilogue
+#endif
 #ifndef VLP_WIN_STAMP
 #define VLP_WIN_STAMP 0   // diagnostic build: in-kernel s_memtime stamps (tools/build_variant.sh)
 #endif
@@ -1720,19 +1723,24 @@ struct WinXIn {
   const float* sc; const float* sh;   // XF 1: per-channel BN scale / shift of the input
   bf16* out;                          // XF 1: relu(sc * x + sh) of the tile's pixels
 };
-template <class EP> constexpr int win_minp() { return LdsSlotTrait<EP>::value >= 0 ? 64 : 0; }
+// persistent form (PS): the forward's staged epilogue, tiles walked by one workgroup per CU
+template <class EP, bool FLIP, int XF, bool PS>
+constexpr bool win_pers() { return PS && !FLIP && XF == 0 && LdsSlotTrait<EP>::value < 0 && StageTrait<EP>::value; }
+template <class EP, bool PERS = false> constexpr int win_minp() { return LdsSlotTrait<EP>::value >= 0 || PERS ? 64 : 0; }
 template <int TW, int BN, int NW = 8, int MINP = 0>
 constexpr int win_lds_bytes() { return 2 * WinGeom<TW, NW, MINP>::SLOT + 4 * BN * 64; }
 
 // NW = 8: 4 x 2 waves of 64 x BN/2, two waves per SIMD; NW = 4: 2 x 2 waves of
 // 128 x BN/2, one wave per SIMD (up to 512 registers: operand sets
 // double-buffered, half the LDS fragment reads per MFMA)
-template <int TW, int BN, int NW, bool FLIP, int XF, class EP>
+template <int TW, int BN, int NW, bool FLIP, int XF, class EP, bool PS = false>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 8 ? 2 : 1)))
 conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsigned xbytes, KMat<bf16> lb, EP ep,
                    WinXIn xin) {
   constexpr int LS = LdsSlotTrait<EP>::value;
-  using WG = WinGeom<TW, NW, win_minp<EP>()>;
+  constexpr bool PERS = win_pers<EP, FLIP, XF, PS>();
+  static_assert(!PS || PERS, "persistent form: forward, staged epilogue");
+  using WG = WinGeom<TW, NW, win_minp<EP, PERS>()>;
   constexpr int BM = 256, WGN = 2, WGM = NW / WGN, NT = NW * 64;
   static_assert(LS < 0 || BN == 128, "the staged epilogue operand is a [256][128] bf16 image");
   constexpr int WTN = BN / WGN;
@@ -1742,9 +1750,10 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
   using SB = HStager<BN, KMat<bf16>, NT>;
   static_assert(XF == 0 || NW == 8, "the in-window transform schedule assumes 8 waves");
   static_assert(PPW <= 16, "window pieces are issued over the first half-steps of a chunk");
-  static_assert(win_lds_bytes<TW, BN, NW, win_minp<EP>()>() <= 160 * 1024 &&
-                    BM * BN * 2 + 4096 <= win_lds_bytes<TW, BN, NW, win_minp<EP>()>(),
+  static_assert(win_lds_bytes<TW, BN, NW, win_minp<EP, PERS>()>() <= 160 * 1024 &&
+                    BM * BN * 2 + 4096 <= win_lds_bytes<TW, BN, NW, win_minp<EP, PERS>()>(),
                 "LDS budget");
+  static_assert(!PERS || (BM * BN * 2 <= WG::SLOT && 2 * BN * 2 * 4 * 4 <= BN * 64), "persistent epilogue scratch");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const win = smem;
   char* const ring = smem + 2 * WG::SLOT;
@@ -1755,13 +1764,27 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
   const int nwg = sh.tiles_m * sh.tiles_n;
   const int bid = blockIdx.x;
   int g = bid;
-  if (nwg >= 16) {   // consecutive tiles (shared halo rows) on one XCD
+  // PERS: grid = a multiple of 8 workgroups, nwg % 8 == 0; XCD x walks tiles
+  // [x * nwg/8, (x+1) * nwg/8), its workgroups interleaved (consecutive tiles share halos)
+  const int pgx = gridDim.x >> 3, pslot = bid >> 3, pper = nwg >> 3;
+  if constexpr (PERS) {
+    g = (bid & 7) * pper + pslot;
+  } else if (nwg >= 16) {   // consecutive tiles (shared halo rows) on one XCD
     const int xcd = bid & 7, idx = bid >> 3, q = nwg >> 3, rr = nwg & 7;
     g = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
   }
-  const int tm = g / sh.tiles_n, tn = g - tm * sh.tiles_n;
-  const int row0 = tm * BM, col0 = tn * BN;
-  const int n = row0 / (H * TW), h0 = (row0 - n * H * TW) / TW;
+  int tm = g / sh.tiles_n, tn = g - tm * sh.tiles_n;
+  int row0 = tm * BM, col0 = tn * BN;
+  int n = row0 / (H * TW), h0 = (row0 - n * H * TW) / TW;
+  auto set_tile = [&](int gg) __attribute__((always_inline)) {
+    g = gg;
+    tm = g / sh.tiles_n;
+    tn = g - tm * sh.tiles_n;
+    row0 = tm * BM;
+    col0 = tn * BN;
+    n = row0 / (H * TW);
+    h0 = (row0 - n * H * TW) / TW;
+  };
   const int NC = C / 64;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1774,18 +1797,22 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
   const rsrc_t rb = lb.rsrc();
   const rsrc_t rz = null_rsrc(zero_page());
   unsigned woff[PPW];
+  unsigned woffn[PERS ? PPW : 1];   // PERS: the next tile's (window 0 is fetched during the last chunk)
+  auto calc_woff = [&](unsigned* wo, int tn_, int th0) __attribute__((always_inline)) {
 #pragma unroll
-  for (int i = 0; i < PPW; ++i) {
-    const int off = (wv * PPW + i) * 1024 + lane * 16;
-    const int p = off / WG::PS, c = (off - p * WG::PS) >> 4;
-    const int wr = p / WG::WC, wc = p - wr * WG::WC;
-    const int hh = h0 - 1 + wr, ww = wc - 1;
-    const bool ok = c < 8 && p < WG::WR * WG::WC && hh >= 0 && hh < H && ww >= 0 && ww < TW;
-    woff[i] = ok ? (unsigned)((((n * H + hh) * TW + ww) * C) * 2 + c * 16) : kOOB;
-    // XF 1: the window's two spare pieces (wave 7's last two) carry the chunk's
-    // 64 BN scales / shifts (lanes 0-15, 16 B each) into the window buffer
-    if (XF == 1 && wv == NW - 1 && i >= PPW - 2) woff[i] = lane < 16 ? (unsigned)lane * 16u : kOOB;
-  }
+    for (int i = 0; i < PPW; ++i) {
+      const int off = (wv * PPW + i) * 1024 + lane * 16;
+      const int p = off / WG::PS, c = (off - p * WG::PS) >> 4;
+      const int wr = p / WG::WC, wc = p - wr * WG::WC;
+      const int hh = th0 - 1 + wr, ww = wc - 1;
+      const bool ok = c < 8 && p < WG::WR * WG::WC && hh >= 0 && hh < H && ww >= 0 && ww < TW;
+      wo[i] = ok ? (unsigned)((((tn_ * H + hh) * TW + ww) * C) * 2 + c * 16) : kOOB;
+      // XF 1: the window's two spare pieces (wave 7's last two) carry the chunk's
+      // 64 BN scales / shifts (lanes 0-15, 16 B each) into the window buffer
+      if (XF == 1 && wv == NW - 1 && i >= PPW - 2) wo[i] = lane < 16 ? (unsigned)lane * 16u : kOOB;
+    }
+  };
+  calc_woff(woff, n, h0);
   const rsrc_t rsc = XF == 1 ? buf_rsrc(xin.sc, (unsigned)C * 4u) : rz;
   const rsrc_t rsh = XF == 1 ? buf_rsrc(xin.sh, (unsigned)C * 4u) : rz;
   // LS >= 0: the pieces of "chunk NC" (issued during the last chunk into its spare
@@ -1794,7 +1821,7 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
   rsrc_t rop = rz;
   if constexpr (LS >= 0) rop = buf_rsrc(ep.lds_operand(), (unsigned)((size_t)sh.M * sh.N * 2));
   // window piece i of chunk cc into buffer wb (chunk cc >= NC: zeros)
-  auto wpiece = [&](auto ic, int cc, char* wb) __attribute__((always_inline)) {
+  auto wpiece = [&](auto ic, int cc, char* wb, const unsigned* wo) __attribute__((always_inline)) {
     constexpr int I = decltype(ic)::value;
     if constexpr (LS >= 0) {
       if (cc == NC) {
@@ -1812,15 +1839,31 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
         inc = 256u;
       }
     }
-    dma16(r, woff[I] + (unsigned)cc * inc, wb + (wv * PPW + I) * 1024);
+    dma16(r, wo[I] + (unsigned)cc * inc, wb + (wv * PPW + I) * 1024);
   };
-  SB sb;
+  SB sb, sbn;
   sb.init(lb, col0, 0, wv);
   // B half-tile hc of tap t, channel chunk cc (cc == NC: past the end, zeros)
   auto bfetch = [&](auto hc, int t, int cc, char* slot) __attribute__((always_inline)) {
     if constexpr (VLP_WIN_EXP == 1 || VLP_WIN_EXP == 3) if (t + cc > 0) return;
     sb.template issue<decltype(hc)::value>(lb, cc < NC ? rb : rz, t * C + cc * 64, slot, wv);
   };
+  int kt = 0;          // PERS: tiles done by this workgroup
+  bool more = false;   // PERS: a next tile follows the current one
+  // PERS: the next tile's window offsets and B loader state, prepared a tile ahead
+  auto prep_next = [&]() __attribute__((always_inline)) {
+    if constexpr (PERS) {
+      more = pslot + (kt + 1) * pgx < pper;
+      if (more) {
+        const int gn = g + pgx;
+        const int tmn = gn / sh.tiles_n, tnn = gn - tmn * sh.tiles_n;
+        const int r0n = tmn * BM, nn = r0n / (H * TW);
+        calc_woff(woffn, nn, (r0n - nn * H * TW) / TW);
+        sbn.init(lb, tnn * BN, 0, wv);
+      }
+    }
+  };
+  prep_next();
 
   v4f acc[MB][NB];
 #pragma unroll
@@ -1909,7 +1952,7 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
   using H0 = std::integral_constant<int, 0>;
   using H1 = std::integral_constant<int, 1>;
   using Z = std::integral_constant<int, 0>;
-  static_for<0, PPW>([&](auto ic) { wpiece(ic, 0, win); });
+  static_for<0, PPW>([&](auto ic) { wpiece(ic, 0, win, woff); });
   bfetch(H0{}, 0, 0, ring);
   bfetch(H1{}, 0, 0, ring + BSLOT);
   bfetch(H0{}, 1, 0, ring + 2 * BSLOT);
@@ -1928,8 +1971,12 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
   // u = cc * 18 + S computes with the fragment set S & 1 read one half-step
   // earlier, reads the next set, and fetches B(u + 3) into ring slot (u + 3) & 3
   // (slot of B(v) = v & 3 = (S + 2 * PC) & 3).
-  auto chunk = [&](auto pc, int cc) __attribute__((always_inline)) {
+  // LAST (PERS): the tile's last chunk prefetches the NEXT tile's window 0 and
+  // B(0..2) where the other chunks fetch their successor's, and skips the
+  // fragment reads for the half-step after it (read after the epilogue)
+  auto chunk = [&](auto pc, auto lastc, int cc) __attribute__((always_inline)) {
     constexpr int PC = decltype(pc)::value;
+    constexpr bool LAST = decltype(lastc)::value;
     char* const wbuf = win + PC * WG::SLOT;
     char* const wnext = win + (1 - PC) * WG::SLOT;
     static_for<0, 18>([&](auto sc_) {
@@ -1939,19 +1986,34 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
       // B(u+1) landed: issued after it are the previous half-step's window piece
       // (half-steps 1..PPW) and B(u+2)
       // (XF 1: and its x_act store, half-steps 2 .. KX+1; vmcnt retires in issue order)
+      // (PERS, the first two half-steps after an epilogue: and its 8 tile stores)
       constexpr int NPRE = (S >= 1 && S <= PPW ? 1 : 0) + (XF == 1 && S >= 2 && S <= KX + 1 ? 1 : 0);
-      wait_vmcnt<SB::P + NPRE>();
+      if constexpr (PERS && PC == 0 && S <= 1) {
+        if (cc == 0 && kt > 0) wait_vmcnt<SB::P + NPRE + 8>();
+        else wait_vmcnt<SB::P + NPRE>();
+      } else {
+        wait_vmcnt<SB::P + NPRE>();
+      }
       if constexpr (XF == 1 && S == 17) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // transformed window cc+1
       if constexpr (VLP_WIN_EXP != 5) raw_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (S < PPW && VLP_WIN_EXP != 2 && VLP_WIN_EXP != 3) wpiece(std::integral_constant<int, S < PPW ? S : 0>{}, cc + 1, wnext);
+      if constexpr (S < PPW && VLP_WIN_EXP != 2 && VLP_WIN_EXP != 3) {
+        if constexpr (LAST) wpiece(std::integral_constant<int, S < PPW ? S : 0>{}, more ? 0 : NC, wnext, woffn);
+        else wpiece(std::integral_constant<int, S < PPW ? S : 0>{}, cc + 1, wnext, woff);
+      }
       // XF 1: the stores of window cc's own pixels, one element per half-step
       // (issued right after the barrier: the next half-step's wait retires them)
       if constexpr (XF == 1 && S >= 1 && S <= KX) xstore(S - 1, cc, wbuf);
       constexpr int S3 = S + 3 < 18 ? S + 3 : S + 3 - 18;   // half-step u + 3 = (chunk, S3)
-      bfetch(std::integral_constant<int, S3 & 1>{}, S3 >> 1, S + 3 < 18 ? cc : cc + 1, ring + ((SL + 3) & 3) * BSLOT);
+      if constexpr (LAST && S + 3 >= 18) {
+        // the next tile's B(0..2) (its chunk 0), or nothing past the last tile
+        if constexpr (VLP_WIN_EXP != 1 && VLP_WIN_EXP != 3)
+          sbn.template issue<S3 & 1>(lb, more ? rb : rz, (S3 >> 1) * C, ring + ((SL + 3) & 3) * BSLOT, wv);
+      } else {
+        bfetch(std::integral_constant<int, S3 & 1>{}, S3 >> 1, S + 3 < 18 ? cc : cc + 1, ring + ((SL + 3) & 3) * BSLOT);
+      }
       if constexpr (S + 1 < 18) rd(std::integral_constant<int, 1 - R>{}, std::integral_constant<int, S + 1>{}, wbuf, (SL + 1) & 3);
-      else rd(std::integral_constant<int, 1 - R>{}, Z{}, wnext, (SL + 1) & 3);
+      else if constexpr (!LAST) rd(std::integral_constant<int, 1 - R>{}, Z{}, wnext, (SL + 1) & 3);
       __builtin_amdgcn_sched_barrier(0);
 #if VLP_PP_PRIO
       __builtin_amdgcn_s_setprio(1);
@@ -1978,9 +2040,42 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
       }
     });
   };
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+  using NL = std::integral_constant<bool, false>;
+  if constexpr (PERS) {
+    for (;;) {
+      for (int cc = 0; cc < NC - 2; cc += 2) {
+        chunk(P0{}, NL{}, cc);
+        chunk(P1{}, NL{}, cc + 1);
+      }
+      chunk(P0{}, NL{}, NC - 2);
+      chunk(P1{}, std::integral_constant<bool, true>{}, NC - 1);
+      // buffer 1 (the last chunk's window) and ring slot 3 are free; the next
+      // tile's window 0 and B(0..2) are landing in buffer 0 and slots 0..2.
+      // The epilogue's stores stay in flight into the next tile (counted by its
+      // first two waits; vmcnt retires in issue order)
+      ms_epilogue<BM, BN, WGM, WGN, EP, false, true>(sh, ep, acc, row0, col0, g, wm, wn, smem + WG::SLOT, nullptr,
+                                                      reinterpret_cast<float*>(ring + 3 * BSLOT));
+      if (!more) break;
+      set_tile(g + pgx);
+#pragma unroll
+      for (int i = 0; i < PPW; ++i) woff[i] = woffn[i];
+      sb = sbn;
+      ++kt;
+      prep_next();
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[a][b] = v4f{0.f, 0.f, 0.f, 0.f};
+      rd(Z{}, Z{}, win, 0);
+    }
+    wait_vmcnt<0>();
+    return;
+  }
   for (int cc = 0; cc < NC; cc += 2) {
-    chunk(std::integral_constant<int, 0>{}, cc);
-    chunk(std::integral_constant<int, 1>{}, cc + 1);
+    chunk(P0{}, NL{}, cc);
+    chunk(P1{}, NL{}, cc + 1);
   }
   wait_vmcnt<0>();
   __syncthreads();   // ring and windows drained (incl. the null-resource tail fetches) before LDS is reused
@@ -2023,14 +2118,20 @@ static bool win_ok(const ConvGeom& g, int cin, int nout) {
          g.H % (256 / g.W) == 0 && cin % 128 == 0 && nout % 128 == 0 &&
          (size_t)g.N * g.H * g.W * cin * 2 < (1ull << 31);
 }
-template <int TW, bool FLIP, int XF, class EP>
+template <int TW, bool FLIP, int XF, class EP, bool PS = false>
 static int launch_win_t(const ConvGeom& g, int cin, int nout, const void* x, const void* w, const EP& ep,
                         hipStream_t st, const WinXIn& xin) {
   constexpr int BN = 128;
   constexpr int NW = XF == 1 ? 8 : VLP_WIN_NW;
-  constexpr int lds = win_lds_bytes<TW, BN, NW, win_minp<EP>()>();
+  constexpr bool PERS = win_pers<EP, FLIP, XF, PS>();
+  if constexpr (!PS && win_pers<EP, FLIP, XF, true>() && VLP_WIN_PERSIST) {
+    // persistent form when every XCD gets the same whole number of tiles
+    const int nwg = (g.N * g.H * g.W / 256) * (nout / BN);
+    if (nwg % 8 == 0 && nwg >= 2 * device_cus()) return launch_win_t<TW, FLIP, XF, EP, true>(g, cin, nout, x, w, ep, st, xin);
+  }
+  constexpr int lds = win_lds_bytes<TW, BN, NW, win_minp<EP, PERS>()>();
   static KernelDevState kst;
-  const int e = prepare_kernel(kst, (const void*)&conv3x3_win_kernel<TW, BN, NW, FLIP, XF, EP>, lds, 0, nullptr);
+  const int e = prepare_kernel(kst, (const void*)&conv3x3_win_kernel<TW, BN, NW, FLIP, XF, EP, PERS>, lds, 0, nullptr);
   if (e) return e;
   GemmShape sh;
   sh.M = g.N * g.H * g.W;
@@ -2051,7 +2152,7 @@ static int launch_win_t(const ConvGeom& g, int cin, int nout, const void* x, con
   if (!dbuf) (void)hipMalloc(&dbuf, (size_t)65536 * 4 * 8);
   WinXIn xs = xin;
   if (XF == 0) xs.out = reinterpret_cast<bf16*>(dbuf);
-  hipLaunchKernelGGL((conv3x3_win_kernel<TW, BN, NW, FLIP, XF, EP>), dim3(nb), dim3(NW * 64), lds, st, sh,
+  hipLaunchKernelGGL((conv3x3_win_kernel<TW, BN, NW, FLIP, XF, EP, PERS>), dim3(nb), dim3(NW * 64), lds, st, sh,
                      g.H, cin, (const bf16*)x, (unsigned)((size_t)g.N * g.H * g.W * cin * 2), lb, ep, xs);
   if (XF == 0 && nb <= 65536) {
     (void)hipStreamSynchronize(st);
@@ -2071,7 +2172,12 @@ static int launch_win_t(const ConvGeom& g, int cin, int nout, const void* x, con
             TW, (int)FLIP, nb, a[nb / 2], a[nb * 9 / 10], b[nb / 2], b[nb * 9 / 10], t1 - t0);
   }
 #else
-  hipLaunchKernelGGL((conv3x3_win_kernel<TW, BN, NW, FLIP, XF, EP>), dim3(sh.tiles_m * sh.tiles_n), dim3(NW * 64), lds, st, sh,
+  int grid = sh.tiles_m * sh.tiles_n;
+  if constexpr (PERS) {
+    const int cus = device_cus() / 8 * 8;
+    if (grid > cus) grid = cus;
+  }
+  hipLaunchKernelGGL((conv3x3_win_kernel<TW, BN, NW, FLIP, XF, EP, PERS>), dim3(grid), dim3(NW * 64), lds, st, sh,
                      g.H, cin, (const bf16*)x, (unsigned)((size_t)g.N * g.H * g.W * cin * 2), lb, ep, xin);
 #endif
   return (int)hipGetLastError();

@@ -662,10 +662,23 @@ __device__ __forceinline__ double* stat3_of(const EP& ep) {
 #endif
 // Epilogue shared by the multi-stage kernels: lane l = 16g + i owns
 // C[row = rbase + i][col = cbase + 4g .. 4g+3] of each 16x16 block.
-template <int BM, int BN, int WGM, int WGN, class EP, bool LP = false, int MB, int NB>
+// LP: the row epilogue's operand slot kLdsSlot comes from the LDS image lds_pre.
+// RAW (staged epilogues): the workgroup syncs are LDS-only (lgkmcnt + s_barrier,
+// no vmcnt drain), so the epilogue's own stores stay in flight past it, and the
+// statistics scratch is red_ovr with the staging tile at smem (persistent kernels
+// keep the next tile's loads in the rest of LDS).
+template <int BM, int BN, int WGM, int WGN, class EP, bool LP = false, bool RAW = false, int MB, int NB>
 __device__ __forceinline__ void ms_epilogue(const GemmShape& sh, const EP& ep, v4f (&acc)[MB][NB], int row0,
                                             int col0, int wid, int wm, int wn, char* smem,
-                                            const char* lds_pre = nullptr) {
+                                            const char* lds_pre = nullptr, float* red_ovr = nullptr) {
+  auto epi_sync = [&]() __attribute__((always_inline)) {
+    if constexpr (RAW) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    } else {
+      __syncthreads();
+    }
+  };
   constexpr int NT = WGM * WGN * 64;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   const int l = threadIdx.x & 63;
@@ -786,13 +799,14 @@ __device__ __forceinline__ void ms_epilogue(const GemmShape& sh, const EP& ep, v
     }
     return;
   }
-  float* red = reinterpret_cast<float*>(smem);
+  float* red = RAW ? red_ovr : reinterpret_cast<float*>(smem);
   // staged epilogues: outputs go through a bf16 LDS tile (16-B chunks XOR-
   // swizzled by row) and leave as full 16-B row segments, 4..8 rows per wave
   // store instead of 32-B pieces of 16 rows
   constexpr bool kStage = StageTrait<EP>::value;
+  static_assert(!RAW || kStage, "raw-sync epilogues are the staged ones");
   constexpr int CPR = BN / 8;
-  bf16* stg = reinterpret_cast<bf16*>(smem + 4096);
+  bf16* stg = reinterpret_cast<bf16*>(smem + (RAW ? 0 : 4096));
   
   static_assert(!EP::kStats || WGM * BN * 2 * 4 <= 4096, "stats scratch");
 #pragma unroll
@@ -831,7 +845,7 @@ __device__ __forceinline__ void ms_epilogue(const GemmShape& sh, const EP& ep, v
     }
   }
   if constexpr (kStage) {
-    __syncthreads();
+    epi_sync();
 #pragma unroll 4
     for (int q = threadIdx.x; q < BM * CPR; q += NT) {
       const int r = q / CPR, c = q - r * CPR;
@@ -841,7 +855,7 @@ __device__ __forceinline__ void ms_epilogue(const GemmShape& sh, const EP& ep, v
     }
   }
   if constexpr (EP::kStats && VLP_EPI_EXP != 2) {
-    __syncthreads();
+    epi_sync();
     const int rep = ep.stat_rep > 1 ? (wid % ep.stat_rep) : 0;
     for (int cl = threadIdx.x; cl < BN; cl += NT) {
       const int col = col0 + cl;
