@@ -2099,6 +2099,205 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
 #endif
 }
 
+// Ping-pong form of the window kernel (VLP_WIN_PP).  The two wave groups (rows
+// 0-127: waves 0-3, rows 128-255: waves 4-7; one wave of each per SIMD) run one
+// barrier interval apart, as in gemm_pp_kernel: every half-step is [wait, barrier,
+// fetch + fragment reads, barrier, MFMAs], so in each interval one group's MFMAs
+// run while the other group issues its LDS-DMA pieces and fragment reads, and the
+// SIMD's MFMA pipe does not drain at every barrier.  Group 0 fetches the windows
+// (chunk c+1's pieces one per half-step over the first PPW half-steps of chunk
+// c), group 1 the B half-tiles (B(u+3) at half-step u, ring slot (u+3) & 3).
+// Barrier k of group 0 pairs with barrier k of group 1: group 1 runs one extra
+// barrier before its first half-step, group 0 one after its last.  Hazards (u =
+// half-step, #k = barrier k; group 0 reads in (#2u+1, #2u+2), group 1 in (#2u+2,
+// #2u+3)): B(u+3) is written after #2u+2, its slot last read before #2u+1; B(v) is
+// waited for by group 1 before #2v and read after #2v+1; window c+1's last piece
+// is waited for by group 0 before #(2 (18c + PPW + 1) + 1) <= #36c+37, the first
+// read of chunk c+1.
+template <int TW, int BN, bool FLIP, class EP>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+conv3x3_winpp_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsigned xbytes, KMat<bf16> lb, EP ep) {
+  // LS >= 0: group 0's last-chunk pieces fetch the row epilogue's operand tile (as
+  // conv3x3_win_kernel) into the spare window buffer
+  constexpr int LS = LdsSlotTrait<EP>::value;
+  using WG = WinGeom<TW, 4, win_minp<EP>()>;   // window pieces over group 0's four waves
+  constexpr int BM = 256, WGN = 2, WGM = 4, NTG = 256;
+  constexpr int WTN = BN / WGN, MB = 4, NB = WTN / 16;
+  constexpr int BSLOT = BN * 64;
+  constexpr int PPW = WG::PPW;
+  using SB = HStager<BN, KMat<bf16>, NTG>;
+  static_assert(PPW <= 16, "group 0's last window piece lands before the next chunk's first read");
+  static_assert(2 * WG::SLOT + 4 * BSLOT <= 160 * 1024 && BM * BN * 2 + 4096 <= 2 * WG::SLOT + 4 * BSLOT, "LDS budget");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const win = smem;
+  char* const ring = smem + 2 * WG::SLOT;
+
+  const int nwg = sh.tiles_m * sh.tiles_n;
+  const int bid = blockIdx.x;
+  int g = bid;
+  if (nwg >= 16) {
+    const int xcd = bid & 7, idx = bid >> 3, q = nwg >> 3, rr = nwg & 7;
+    g = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
+  }
+  const int tm = g / sh.tiles_n, tn = g - tm * sh.tiles_n;
+  const int row0 = tm * BM, col0 = tn * BN;
+  const int n = row0 / (H * TW), h0 = (row0 - n * H * TW) / TW;
+  const int NC = C / 64;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wv / WGN, wn = wv - wm * WGN;
+  const int grp = wv >> 2, wg = wv & 3;
+  const int li = lane & 15, lg = lane >> 4;
+  const rsrc_t rx = buf_rsrc(x, xbytes);
+  const rsrc_t rb = lb.rsrc();
+  const rsrc_t rz = null_rsrc(zero_page());
+  rsrc_t rop = rz;
+  if constexpr (LS >= 0) rop = buf_rsrc(ep.lds_operand(), (unsigned)((size_t)sh.M * sh.N * 2));
+
+  v4f acc[MB][NB];
+#pragma unroll
+  for (int a = 0; a < MB; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[a][b] = v4f{0.f, 0.f, 0.f, 0.f};
+  const int aoff = li * WG::PS + lg * 16;
+  const int wpx = wm * 64;
+  const char* const bbase = ring + li * 64 + (pp_chunk(li, lg) << 4) + wn * WTN * 64;
+  // fragments of half-step (tap t, half hh) of window buffer wb, ring slot sl
+  auto mma = [&](auto sc_, const char* wb, int sl) __attribute__((always_inline)) {
+    constexpr int S = decltype(sc_)::value;
+    constexpr int T = S >> 1, HH = S & 1;
+    constexpr int KH = FLIP ? 2 - T / 3 : T / 3, KW = FLIP ? 2 - T % 3 : T % 3;
+    v8bf fa[MB], fb[NB];
+#pragma unroll
+    for (int a = 0; a < MB; ++a) {
+      const int px = wpx + a * 16;
+      const int wrow = px / TW + KH, wcol = px % TW;
+      fa[a] = *reinterpret_cast<const v8bf*>(wb + aoff + (wrow * WG::WC + wcol + KW) * WG::PS + HH * 64);
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) fb[b] = *reinterpret_cast<const v8bf*>(bbase + sl * BSLOT + b * 16 * 64);
+    __builtin_amdgcn_sched_barrier(0);
+    raw_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#if VLP_PP_PRIO
+    __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+    for (int a = 0; a < MB; ++a)
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[b], fa[a], acc[a][b], 0, 0, 0);
+#if VLP_PP_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  using H0 = std::integral_constant<int, 0>;
+  using H1 = std::integral_constant<int, 1>;
+
+  auto run = [&](auto gc) __attribute__((always_inline)) {
+    constexpr int G = decltype(gc)::value;
+    // group 0: window pieces; group 1: B half-tiles (each holds only its own loader state)
+    unsigned woff[G == 0 ? PPW : 1];
+    SB sb;
+    if constexpr (G == 0) {
+#pragma unroll
+      for (int i = 0; i < PPW; ++i) {
+        const int off = (wg * PPW + i) * 1024 + lane * 16;
+        const int p = off / WG::PS, c = (off - p * WG::PS) >> 4;
+        const int wr = p / WG::WC, wc = p - wr * WG::WC;
+        const int hh = h0 - 1 + wr, ww = wc - 1;
+        const bool ok = c < 8 && p < WG::WR * WG::WC && hh >= 0 && hh < H && ww >= 0 && ww < TW;
+        woff[i] = ok ? (unsigned)((((n * H + hh) * TW + ww) * C) * 2 + c * 16) : kOOB;
+      }
+#pragma unroll
+      for (int i = 0; i < PPW; ++i) dma16(rx, woff[i], win + (wg * PPW + i) * 1024);
+      wait_vmcnt<0>();
+    } else {
+      sb.init(lb, col0, 0, wg);
+      sb.template issue<0>(lb, rb, 0, ring, wg);
+      sb.template issue<1>(lb, rb, 0, ring + BSLOT, wg);
+      sb.template issue<0>(lb, rb, C, ring + 2 * BSLOT, wg);
+      wait_vmcnt<2 * SB::P>();
+    }
+    raw_barrier();
+    if constexpr (G == 1) raw_barrier();   // the stagger
+    __builtin_amdgcn_sched_barrier(0);
+    auto chunk = [&](auto pc, int cc) __attribute__((always_inline)) {
+      constexpr int PC = decltype(pc)::value;
+      const char* const wbuf = win + PC * WG::SLOT;
+      char* const wnext = win + (1 - PC) * WG::SLOT;
+      static_for<0, 18>([&](auto sc_) {
+        constexpr int S = decltype(sc_)::value;
+        constexpr int SL = (S + 2 * PC) & 3;
+        if constexpr (G == 0) {
+          wait_vmcnt<(S >= 1 && S <= PPW) ? 1 : 0>();   // pieces of half-step S-2 landed
+        } else {
+          wait_vmcnt<SB::P>();                           // B(u+1) landed
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        raw_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (G == 0) {
+          if constexpr (S < PPW) {
+            constexpr int I = S < PPW ? S : 0;
+            if (LS >= 0 && cc + 1 == NC) {
+              const int j = wg * PPW + I, row = j * 4 + (lane >> 4);
+              const unsigned o = row < BM ? (unsigned)(((row0 + row) * sh.N + col0) * 2 + (lane & 15) * 16) : kOOB;
+              dma16(rop, o, wnext + j * 1024);
+            } else {
+              dma16(cc + 1 < NC ? rx : rz, woff[I] + (unsigned)(cc + 1) * 128u, wnext + (wg * PPW + I) * 1024);
+            }
+          }
+        } else {
+          constexpr int S3 = S + 3 < 18 ? S + 3 : S + 3 - 18;
+          const int c3 = S + 3 < 18 ? cc : cc + 1;
+          sb.template issue<S3 & 1>(lb, c3 < NC ? rb : rz, (S3 >> 1) * C + c3 * 64, ring + ((SL + 3) & 3) * BSLOT, wg);
+        }
+        mma(sc_, wbuf, SL);
+      });
+    };
+    for (int cc = 0; cc < NC; cc += 2) {
+      chunk(std::integral_constant<int, 0>{}, cc);
+      chunk(std::integral_constant<int, 1>{}, cc + 1);
+    }
+    if constexpr (G == 0) raw_barrier();   // matches group 1's stagger barrier
+  };
+  if (grp == 0) run(std::integral_constant<int, 0>{});
+  else run(std::integral_constant<int, 1>{});
+  wait_vmcnt<0>();
+  __syncthreads();
+  if constexpr (LS >= 0) {
+    ms_epilogue<BM, BN, WGM, WGN, EP, true>(sh, ep, acc, row0, col0, g, wm, wn, smem + WG::SLOT, smem);
+  } else {
+    ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep, acc, row0, col0, g, wm, wn, smem);
+  }
+}
+template <int TW, bool FLIP, class EP>
+static int launch_winpp_t(const ConvGeom& g, int cin, int nout, const void* x, const void* w, const EP& ep,
+                          hipStream_t st) {
+  constexpr int BN = 128;
+  constexpr int lds = 2 * WinGeom<TW, 4, win_minp<EP>()>::SLOT + 4 * BN * 64;
+  static KernelDevState kst;
+  const int e = prepare_kernel(kst, (const void*)&conv3x3_winpp_kernel<TW, BN, FLIP, EP>, lds, 0, nullptr);
+  if (e) return e;
+  GemmShape sh;
+  sh.M = g.N * g.H * g.W;
+  sh.N = nout;
+  sh.K = 9 * cin;
+  sh.kchunk = sh.K;
+  sh.tiles_m = sh.M / 256;
+  sh.tiles_n = nout / BN;
+  sh.xsplit = 0;
+  sh.dbg = 0;
+  sh.nsplit = 1;
+  KMat<bf16> lb{(const bf16*)w, sh.K, nout, sh.K};
+  hipLaunchKernelGGL((conv3x3_winpp_kernel<TW, BN, FLIP, EP>), dim3(sh.tiles_m * sh.tiles_n), dim3(512), lds, st, sh,
+                     g.H, cin, (const bf16*)x, (unsigned)((size_t)g.N * g.H * g.W * cin * 2), lb, ep);
+  return (int)hipGetLastError();
+}
+
 // 3x3 / stride 1 / pad 1 with C and the GEMM N both multiples of 128, 256-pixel
 // tiles of whole rows, widths 16 / 32 / 64 (ResNet34 layers 2-4 at 512 x 512)
 // image widths routed to the window kernel (bit W / 16): r5 A/B at the bench
@@ -2185,9 +2384,17 @@ static int launch_win_t(const ConvGeom& g, int cin, int nout, const void* x, con
 #ifndef VLP_WIN
 #define VLP_WIN 1   // the LDS-window kernel for the 3x3 stride-1 GEMMs of layers 2-4 (0: im2col GEMMs)
 #endif
+#ifndef VLP_WIN_PP
+#define VLP_WIN_PP 1   // the ping-pong form for the plain (XF = 0) window GEMMs
+#endif
 template <bool FLIP, int XF = 0, class EP>
 static int launch_win(const ConvGeom& g, int cin, int nout, const void* x, const void* w, const EP& ep,
                       hipStream_t st, const WinXIn& xin = WinXIn{}) {
+  if constexpr (XF == 0 && VLP_WIN_PP) {
+    if (g.W == 64) return launch_winpp_t<64, FLIP>(g, cin, nout, x, w, ep, st);
+    if (g.W == 32) return launch_winpp_t<32, FLIP>(g, cin, nout, x, w, ep, st);
+    return launch_winpp_t<16, FLIP>(g, cin, nout, x, w, ep, st);
+  }
   if (g.W == 64) return launch_win_t<64, FLIP, XF>(g, cin, nout, x, w, ep, st, xin);
   if (g.W == 32) return launch_win_t<32, FLIP, XF>(g, cin, nout, x, w, ep, st, xin);
   return launch_win_t<16, FLIP, XF>(g, cin, nout, x, w, ep, st, xin);
