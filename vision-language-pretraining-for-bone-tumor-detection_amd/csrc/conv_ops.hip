@@ -1280,11 +1280,31 @@ static int gemm_wgrad(int M, int N, int K, const LA& la, const LB& lb, const EP&
 //   waves: 8, each 32 output pixels x 32 channels (MFMA 16x16x32, B = weights)
 // Requirements: C = Co = 64, 3x3, stride 1, pad 1, W = 128, bf16.
 constexpr int kRcW = 128;                        // image width handled
-constexpr int kRcSlot = (kRcW + 2) * 128;        // one ring row (bytes)
+// Ring row layout.  Planar (VLP_RC_PLANAR, default): 8 planes, one per 16-B
+// channel chunk, each 130 pixels x 16 B padded to 144 16-B units, so a fragment
+// read -- pixels {0-3, 12-15} of chunk c and {4-11} of chunk c+1 in one 16-lane
+// group -- falls on 16 distinct bank slots at ANY pixel offset (every filter tap
+// column); the pixel-major image with an XOR swizzle is conflict-free at tap
+// column 0 only (r5 PMC: 44 % of the data-gradient kernels' LDS cycles were
+// conflicts).  The planar rows are 11 % larger: the filter image is staged in the
+// ring area before the first row instead of beside it, and the epilogue's staging
+// tile, statistics and y row live after the ring.  Measured a wash (interleaved x2,
+// profiles/r5r2_rows_planar_ab.txt: -3 % forward, +2 % BN data gradient, the rest
+// within noise): the conflicts are not what holds these kernels; off by default.
+#ifndef VLP_RC_PLANAR
+#define VLP_RC_PLANAR 0
+#endif
+constexpr bool kRcPlanar = VLP_RC_PLANAR;
+constexpr int kRcPlane = 144 * 16;                 // planar: one chunk plane of a ring row
+constexpr int kRcSlot = kRcPlanar ? 8 * kRcPlane : (kRcW + 2) * 128;   // one ring row (bytes)
 constexpr int kRcWeights = 9 * 64 * 128;         // 73728
 constexpr int kRcRing = 5;
-constexpr int kRcXtab = kRcWeights + kRcRing * kRcSlot + 2048;   // input-transform table: (scale, shift) or (k, b, c)
+constexpr int kRcRingOff = kRcPlanar ? 0 : kRcWeights;
+constexpr int kRcAux = kRcPlanar ? kRcRing * kRcSlot : 0;   // staging 16 KB | statistics 32 KB | y row 16 KB
+constexpr int kRcTail = kRcPlanar ? kRcAux + 65536 : kRcWeights + kRcRing * kRcSlot;   // direct-mode stats / coefficients
+constexpr int kRcXtab = kRcTail + 2048;          // input-transform table: (scale, shift) or (k, b, c)
 constexpr int kRcLds = kRcXtab + 768;
+static_assert(kRcLds <= 160 * 1024 && (!kRcPlanar || kRcWeights <= kRcRing * kRcSlot), "rows kernel LDS map");
 
 #ifndef VLP_ACT_NT
 #define VLP_ACT_NT 0   // non-temporal stores of the transformed input rows
@@ -1316,10 +1336,11 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
   static_assert(XF != 2 || RowTrait<EP>::value, "backward input transform with a row-chunk epilogue only");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* wlds = smem;
-  char* ring = smem + kRcWeights;
-  // stats scratch: 2 KB after the ring (direct mode) or the filter area past
+  char* ring = smem + kRcRingOff;
+  char* aux = smem + kRcAux;   // row-chunk epilogue: staging tile, statistics, y row
+  // stats scratch: 2 KB after the ring (direct mode) or the aux area past
   // the 16 KB staging tile (row-chunk mode, 32 KB, used after the last row)
-  float* red = reinterpret_cast<float*>(RowTrait<EP>::value ? smem + 16384 : smem + kRcWeights + kRcRing * kRcSlot);
+  float* red = reinterpret_cast<float*>(RowTrait<EP>::value ? aux + 16384 : smem + kRcTail);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
   const int pq = wv & 3, ch = wv >> 2;
@@ -1335,23 +1356,45 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
     const int tb = flip ? 8 - b : b;
     dma16(rw, (unsigned)((r * 576 + tb * 64 + c * 8) * 2), wlds + j * 1024);
   }
-  // zero halo columns (ring rows 0 and 129 of every slot)
-  for (int q = tid; q < kRcRing * 2 * 8; q += 512) {
-    const int sl = q >> 4, side = (q >> 3) & 1, c = q & 7;
-    *reinterpret_cast<uint4*>(ring + sl * kRcSlot + (side ? (kRcW + 1) * 128 : 0) + c * 16) = zero4();
-  }
-  // input row i of image n -> ring slot (i + 1) % 5, pixels at ring rows 1..128
+  // zero halo columns (ring pixels 0 and 129 of every slot)
+  auto zero_halo = [&]() {
+    for (int q = tid; q < kRcRing * 2 * 8; q += 512) {
+      const int sl = q >> 4, side = (q >> 3) & 1, c = q & 7;
+      if constexpr (kRcPlanar)
+        *reinterpret_cast<uint4*>(ring + sl * kRcSlot + c * kRcPlane + (side ? (kRcW + 1) * 16 : 0)) = zero4();
+      else
+        *reinterpret_cast<uint4*>(ring + sl * kRcSlot + (side ? (kRcW + 1) * 128 : 0) + c * 16) = zero4();
+    }
+  };
+  if constexpr (!kRcPlanar) zero_halo();   // (planar: the filter image occupies the ring until the fragments are loaded)
+  // the ring (or y-row) position of piece jj of this wave: planar piece j = plane
+  // j & 7, pixels 64 (j >> 3) .. +63; pixel-major piece j = pixels 8j .. 8j + 7
+  auto piece_src = [&](int j, int ln, int& px, int& c) __attribute__((always_inline)) {
+    if constexpr (kRcPlanar) {
+      c = j & 7;
+      px = 64 * (j >> 3) + ln;
+    } else {
+      const int q = j * 64 + ln;
+      px = q >> 3;
+      c = (q & 7) ^ (((px + 1) >> 1) & 7);
+    }
+  };
+  auto piece_lds = [&](char* rowbase, int j) __attribute__((always_inline)) -> char* {
+    if constexpr (kRcPlanar) return rowbase + (j & 7) * kRcPlane + (1 + 64 * (j >> 3)) * 16;
+    else return rowbase + 128 + j * 1024;
+  };
+  // input row i of image n -> ring slot (i + 1) % 5, pixels at ring positions 1..128
   auto fetch = [&](int n, int i) {
-    char* slot = ring + ((i + 1) % kRcRing) * kRcSlot + 128;
+    char* slot = ring + ((i + 1) % kRcRing) * kRcSlot;
     const bool live = (unsigned)i < (unsigned)H;
     const rsrc_t r = live ? rx : rz;
     const unsigned base = live ? (unsigned)(((size_t)n * H + i) * kRcW * 128) : 0u;
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
       const int j = wv * 2 + jj;
-      const int q = j * 64 + lane;
-      const int px = q >> 3, c = (q & 7) ^ (((px + 1) >> 1) & 7);
-      dma16(r, base + (unsigned)(px * 128 + c * 16), slot + j * 1024);
+      int px, c;
+      piece_src(j, lane, px, c);
+      dma16(r, base + (unsigned)(px * 128 + c * 16), piece_lds(slot, j));
     }
   };
   v4f s1[2], s2[2];
@@ -1367,6 +1410,10 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int b = 0; b < 2; ++b) wf[t][s][b] = frag_bf16<true, 128, true>(wlds + t * 8192, ch * 32 + b * 16, s);
+  if constexpr (kRcPlanar) {
+    __syncthreads();   // every wave holds its filter fragments: the ring area is free
+    zero_halo();
+  }
   if constexpr (RowTrait<EP>::value && EP::kStats) {
     __syncthreads();   // every wave holds its filter fragments before the area is reused
     v4f* rp = reinterpret_cast<v4f*>(red + tid * 16);
@@ -1375,7 +1422,7 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
   // the epilogue's per-channel coefficients (64 floats each) staged in LDS: read
   // per row with ds_read instead of held in (or reloaded into) VGPRs
   constexpr int NCF = CoefTrait<EP>::value;
-  float* cfl = reinterpret_cast<float*>(smem + kRcWeights + kRcRing * kRcSlot);
+  float* cfl = reinterpret_cast<float*>(smem + kRcTail);
   if constexpr (NCF > 0) {
     for (int q = tid; q < NCF * 64; q += 512) cfl[q] = ep.coef(q >> 6)[q & 63];
     __syncthreads();
@@ -1393,8 +1440,8 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
   // buffer in the filter area's free part (past the 16 KB epilogue staging tile
   // and the 32 KB statistics scratch) at the same chunk positions as the ring
   // row: each thread reads back exactly the chunks its own DMA wrote
-  char* ybuf = smem + 16384 + 32768;
-  static_assert(16384 + 32768 + kRcW * 128 <= kRcWeights, "y row buffer fits the filter area");
+  char* ybuf = aux + 16384 + 32768;
+  static_assert(kRcPlanar || 16384 + 32768 + kRcW * 128 <= kRcWeights, "y row buffer fits the filter area");
   const rsrc_t ry = XF == 2 ? buf_rsrc(xin.y, (unsigned)((size_t)N * H * kRcW * 64 * 2)) : rz;
   auto yload = [&](int n, int r) __attribute__((always_inline)) {
     const bool live = (unsigned)r < (unsigned)H;   // past the last row: a null fetch keeps the vmcnt pattern
@@ -1407,8 +1454,8 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
       const int j = wv * 2 + jj;
-      const int q = j * 64 + sd;
-      const int px = q >> 3, c = (q & 7) ^ (((px + 1) >> 1) & 7);
+      int px, c;
+      piece_src(j, sd, px, c);
       dma16(rr, base + (unsigned)(px * 128 + c * 16), ybuf + j * 1024);
     }
   };
@@ -1416,14 +1463,15 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
   // each thread transforms the two 16-B chunks its own ring fetch wrote, so
   // its vmcnt wait alone makes them readable (no barrier before the transform)
   auto xrow = [&](int n, int r) __attribute__((always_inline)) {
-    char* slot = ring + ((r + 1) % kRcRing) * kRcSlot + 128;
+    char* slot = ring + ((r + 1) % kRcRing) * kRcSlot;
     int sd = lane;
     if constexpr (XF == 2) asm volatile("" : "+v"(sd));
 #pragma unroll
     for (int jj = 0; jj < 2; ++jj) {
-      const int q = (wv * 2 + jj) * 64 + sd;
-      const int px = q >> 3, cc = (q & 7) ^ (((px + 1) >> 1) & 7);
-      uint4* p = reinterpret_cast<uint4*>(slot + q * 16);
+      const int j = wv * 2 + jj, q = j * 64 + sd;
+      int px, cc;
+      piece_src(j, sd, px, cc);
+      uint4* p = reinterpret_cast<uint4*>(piece_lds(slot, j) + sd * 16);
       float f[8];
       Chunk<bf16>::unpack(*p, f);
       if constexpr (XF == 2) {
@@ -1531,7 +1579,7 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const int r = seed + kw;
-          foff[kw][s] = r * 128 + (((4 * s + lg) ^ ((r >> 1) & 7)) << 4);
+          foff[kw][s] = kRcPlanar ? (4 * s + lg) * kRcPlane + r * 16 : r * 128 + (((4 * s + lg) ^ ((r >> 1) & 7)) << 4);
         }
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
@@ -1543,7 +1591,9 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
           for (int s = 0; s < 2; ++s)
 #pragma unroll
             for (int a = 0; a < 2; ++a) {
-              if constexpr (kRowEpi) fa[s][a] = *reinterpret_cast<const v8bf*>(sl + foff[kw][s] + a * 2048);
+              if constexpr (kRowEpi) fa[s][a] = *reinterpret_cast<const v8bf*>(sl + foff[kw][s] + a * (kRcPlanar ? 256 : 2048));
+              else if constexpr (kRcPlanar)
+                fa[s][a] = *reinterpret_cast<const v8bf*>(sl + (4 * s + lg) * kRcPlane + (pq * 32 + a * 16 + kw + li) * 16);
               else fa[s][a] = frag_bf16<true, 128, true>(sl, pq * 32 + a * 16 + kw, s);
             }
 #pragma unroll
@@ -1560,7 +1610,7 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
         // output row is staged as bf16, then thread t handles pixels t/8 and
         // t/8 + 64 at the FIXED 8-channel group t%8, so its operand loads and
         // stores are row-contiguous 16-B chunks
-        bf16* stg = reinterpret_cast<bf16*>(wlds);
+        bf16* stg = reinterpret_cast<bf16*>(kRcPlanar ? aux : wlds);
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
