@@ -1107,8 +1107,9 @@ struct EpiDgradRelu {
     p.u[2] = ldg16(y + o);
   }
   // y could come from LDS as EpiDgradBN's does (kLdsSlot = 2 + lds_operand()); measured
-  // slower (layer 2 504 -> 528 us, profiles/r5l_lds_operand_ab.txt): the addend and the
-  // mask still make the epilogue wait on global loads, now behind 64 KB more DMA
+  // slower (lock-step: layer 2 504 -> 528 us, profiles/r5l_lds_operand_ab.txt; ping-pong:
+  // 494 -> 507, profiles/r5u_relu_lds_ab.txt): the addend and the mask still make the
+  // epilogue wait on global loads, now behind 64 KB more DMA
   static constexpr int kLdsSlotOff = 2;
   __device__ void pre8_rest(int row, int col, RowPre& p) const {
     const size_t o = (size_t)row * C + col;
