@@ -1752,6 +1752,9 @@ static int launch_rows_c64(const ConvGeom& g, const void* x, const void* w, int 
 #ifndef VLP_WIN_NW
 #define VLP_WIN_NW 8   // waves per window workgroup (8: two per SIMD; 4: one per SIMD, 128 x 64 per wave)
 #endif
+#ifndef VLP_WIN_DESYNC
+#define VLP_WIN_DESYNC 0   // half the CUs start half a tile late (conv3x3_winpp_kernel); r5 A/B: no gain, off
+#endif
 #ifndef VLP_WIN_PERSIST
 #define VLP_WIN_PERSIST 1   // forward: one workgroup per CU walks its tiles, the next tile's loads over the epilogue
 #endif
@@ -2167,7 +2170,8 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
 // read of chunk c+1.
 template <int TW, int BN, bool FLIP, class EP>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
-conv3x3_winpp_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsigned xbytes, KMat<bf16> lb, EP ep) {
+conv3x3_winpp_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsigned xbytes, KMat<bf16> lb, EP ep,
+                     int first_round, int desync) {
   // LS >= 0: group 0's last-chunk pieces fetch the row epilogue's operand tile (as
   // conv3x3_win_kernel) into the spare window buffer
   constexpr int LS = LdsSlotTrait<EP>::value;
@@ -2204,6 +2208,13 @@ conv3x3_winpp_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, uns
   const rsrc_t rz = null_rsrc(zero_page());
   rsrc_t rop = rz;
   if constexpr (LS >= 0) rop = buf_rsrc(ep.lds_operand(), (unsigned)((size_t)sh.M * sh.N * 2));
+  // desync > 0: every other CU of each XCD starts its first tile ~desync cycles late,
+  // so the CUs' epilogues (HBM operand loads and stores, MFMAs idle) fall in two
+  // phases instead of one chip-wide burst per round; the offset persists as each
+  // CU takes its next tile when it frees up
+  if (desync > 0 && bid < first_round && ((bid >> 3) & 1)) {
+    for (int t = 0; t < desync; t += 8128) __builtin_amdgcn_s_sleep(127);
+  }
 
   v4f acc[MB][NB];
 #pragma unroll
@@ -2344,8 +2355,14 @@ static int launch_winpp_t(const ConvGeom& g, int cin, int nout, const void* x, c
   sh.dbg = 0;
   sh.nsplit = 1;
   KMat<bf16> lb{(const bf16*)w, sh.K, nout, sh.K};
-  hipLaunchKernelGGL((conv3x3_winpp_kernel<TW, BN, FLIP, EP>), dim3(sh.tiles_m * sh.tiles_n), dim3(512), lds, st, sh,
-                     g.H, cin, (const bf16*)x, (unsigned)((size_t)g.N * g.H * g.W * cin * 2), lb, ep);
+  // desync: half a tile's time (~14k cycles per 64-channel chunk for the row epilogues,
+  // ~10k for the forward) when every CU runs >= 8 tiles (the delayed CUs' idle start
+  // is then <= 1/16 of their work)
+  const int tiles = sh.tiles_m * sh.tiles_n, cus = device_cus();
+  int desync = 0;
+  if (VLP_WIN_DESYNC && tiles >= 8 * cus) desync = (RowTrait<EP>::value ? 14000 : 10000) * (cin / 64) / 2;
+  hipLaunchKernelGGL((conv3x3_winpp_kernel<TW, BN, FLIP, EP>), dim3(tiles), dim3(512), lds, st, sh,
+                     g.H, cin, (const bf16*)x, (unsigned)((size_t)g.N * g.H * g.W * cin * 2), lb, ep, cus, desync);
   return (int)hipGetLastError();
 }
 
