@@ -109,11 +109,12 @@ def test_conv_fwd(ops, dt, case, xform):
 
 
 @pytest.mark.parametrize("N,H,W,C,Co", [(32, 64, 64, 128, 128), (128, 16, 16, 512, 512)])
-def test_conv_fwd_persistent_window(ops, N, H, W, C, Co):
-    """The persistent forward of the LDS-window kernel (>= 2 tiles per CU, tile count a
-    multiple of 8: one workgroup per CU walks its XCD's tiles, the next tile's window
-    and filter slices loading over the epilogue) against torch fp32 on the GPU, with
-    the BN sums; every tile's output checked (the tile hand-over is where it breaks)."""
+def test_conv_fwd_window_many_tiles(ops, N, H, W, C, Co):
+    """The LDS-window forward at >= 2 tiles per CU, tile count a multiple of 8 (the
+    shapes where a build with VLP_WIN_PP=0 takes the persistent form: one workgroup per
+    CU walks its XCD's tiles, the next tile's window and filter slices loading over the
+    epilogue) against torch fp32 on the GPU, with the BN sums; every tile's output
+    checked."""
     torch.manual_seed(21)
     dev = torch.device("cuda")
     x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)

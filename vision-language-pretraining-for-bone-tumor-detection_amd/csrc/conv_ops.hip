@@ -2458,14 +2458,17 @@ static int launch_win_t(const ConvGeom& g, int cin, int nout, const void* x, con
 template <bool FLIP, int XF = 0, class EP>
 static int launch_win(const ConvGeom& g, int cin, int nout, const void* x, const void* w, const EP& ep,
                       hipStream_t st, const WinXIn& xin = WinXIn{}) {
+  // (the lock-step form, conv3x3_win_kernel, is instantiated only for the measured
+  // alternatives: VLP_WIN_PP=0, or the in-window transform with VLP_WIN_ACT=1)
   if constexpr (XF == 0 && VLP_WIN_PP) {
     if (g.W == 64) return launch_winpp_t<64, FLIP>(g, cin, nout, x, w, ep, st);
     if (g.W == 32) return launch_winpp_t<32, FLIP>(g, cin, nout, x, w, ep, st);
     return launch_winpp_t<16, FLIP>(g, cin, nout, x, w, ep, st);
+  } else {
+    if (g.W == 64) return launch_win_t<64, FLIP, XF>(g, cin, nout, x, w, ep, st, xin);
+    if (g.W == 32) return launch_win_t<32, FLIP, XF>(g, cin, nout, x, w, ep, st, xin);
+    return launch_win_t<16, FLIP, XF>(g, cin, nout, x, w, ep, st, xin);
   }
-  if (g.W == 64) return launch_win_t<64, FLIP, XF>(g, cin, nout, x, w, ep, st, xin);
-  if (g.W == 32) return launch_win_t<32, FLIP, XF>(g, cin, nout, x, w, ep, st, xin);
-  return launch_win_t<16, FLIP, XF>(g, cin, nout, x, w, ep, st, xin);
 }
 
 #ifndef VLP_FWD_BN_PP
@@ -2848,10 +2851,12 @@ VLP_EXPORT int vlp_conv_fwd_act(int dtype, const void* x, const void* wp, void* 
   g.M = g.N * g.Ho * g.Wo;
   g.K = g.KH * g.KW * g.C;
   EpiConvFwd<bf16> ep{stat_sum, stat_sumsq, stat_rep, (bf16*)y, g.Co};
+#if VLP_WIN_ACT
   if (!rows_c64_ok(g)) {   // layers 2-4: the window kernel transforms each window chunk once
     WinXIn wx{in_scale, in_shift, (bf16*)x_act};
     return launch_win<false, 1>(g, g.C, g.Co, x, wp, ep, (hipStream_t)stream, wx);
   }
+#endif
   RowsXIn xin{};
   xin.t0 = in_scale;
   xin.t1 = in_shift;
