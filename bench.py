@@ -76,6 +76,10 @@ def parse():
                     help="steps of the isolated (serial-schedule) pass that times the roofline kernel")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo for CPU rehearsal)")
+    ap.add_argument("--dp-rehearsal", type=int, default=1, choices=[0, 1],
+                    help="N=1: also time the K steps with the data-parallel schedule on a world-1 RCCL group "
+                         "(every collective issued, per-stage gradient buckets launched from the weight-gradient "
+                         "stream) and report it beside `value` as `dp_schedule_1gpu`")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU work: exercise the launcher, the rendezvous and the max-over-ranks timing "
                          "and print the JSON line (CPU test of the N-rank path)")
@@ -396,6 +400,29 @@ def pcie_inclusive(args, model, opt, world, dev):
     return out
 
 
+def dp_rehearsal(args, prefetched_steps, timed, dev):
+    """The world > 1 step schedule measured on one GPU: a world-1 RCCL process
+    group with vlp_amd.dist.REHEARSE set, so ClipStepFn issues every collective
+    of a data-parallel step (embedding all-gathers, loss all-reduce, gradient
+    reduce-scatters, the head / text arenas and the four per-stage image-arena
+    buckets, each launched from the stream that produced it) and the image
+    tower fires its per-stage callbacks.  Same prefetched steps as `value`."""
+    from vlp_amd import dist as vdist
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=dev)
+    vdist.REHEARSE = True
+    try:
+        prefetched_steps(2)
+        el, _ = timed(lambda: prefetched_steps(args.steps))
+    finally:
+        vdist.REHEARSE = False
+        torch.cuda.synchronize()
+        dist.destroy_process_group()
+    return {"value": round(args.batch * args.steps / el, 2), "ms_per_step": round(el / args.steps * 1e3, 3),
+            "note": "world-1 RCCL group, every data-parallel collective issued, image-arena buckets per stage "
+                    "from the weight-gradient stream (the N > 1 schedule on one GPU)"}
+
+
 def _traffic(family):
     """HBM bytes per launch of the roofline kernel from the committed PMC passes
     (profiles/roofline_traffic.json, written by tools/pmc_traffic.py from
@@ -509,6 +536,12 @@ def main():
 
     prefetched_steps(2)   # warm the copy stream and the pinned buffers
     el, loss = timed(lambda: prefetched_steps(args.steps))
+    rehearsal = None
+    if world == 1 and args.dp_rehearsal:
+        rehearsal = dp_rehearsal(args, prefetched_steps, timed, dev)
+        # the plain schedule again right after it: the box's drift between the two
+        el2, _ = timed(lambda: prefetched_steps(args.steps))
+        rehearsal["value_plain_rerun"] = round(args.batch * args.steps / el2, 2)
     # isolated roofline pass: serial schedule, the dominant family timed with HIP
     # events on its launch stream; bracketed by marker dispatches so a rocprofv3
     # kernel trace of this command averages exactly these launches
@@ -588,6 +621,9 @@ def main():
                                           "main stream (no CU sharing); `value` uses the side-stream schedule"}
         if shared is not None and shared[0] > 0:
             res["roofline"]["achieved_under_default_schedule"] = round((shared[2] / (shared[0] / 1e3)) / 1e12, 2)
+        if rehearsal is not None:
+            rehearsal["vs_value"] = round(rehearsal["value"] / value, 4)
+            res["dp_schedule_1gpu"] = rehearsal
         if ldelta is not None:
             res["loss_delta_vs_fp32"] = ldelta
         if pcie is not None:

@@ -146,6 +146,10 @@ def test_constructor_contract():
     for bad in (30, 512):
         with pytest.raises(ValueError, match="embedding_dim"):
             _module(embedding_dim=bad)
+    # bf16: the projection matmuls need E % 8 == 0 (16-B bf16 rows); fp32 keeps E % 4
+    assert _module(embedding_dim=36, compute_dtype="fp32")._head.embedding_dim == 36
+    with pytest.raises(ValueError, match="embedding_dim"):
+        _module(embedding_dim=36, compute_dtype="bf16")
 
 
 def test_validation_dataloader_index_contract(module):

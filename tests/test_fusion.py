@@ -241,3 +241,56 @@ def test_fusion_all_reduce_gradients_single_rank():
             assert torch.equal(p.grad, before[n]), n
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_fusion_dp2_trainer_all_reduce(tmp_path):
+    """BASELINE configs[4]'s data-parallel path at world size 2:
+    two ranks (torch.distributed.run, gloo, both on the one GPU; tests/_fusion_dp_worker.py)
+    each run one step of src/utils/trainer.py's Trainer.fit on their 6-row shard of a
+    12-row batch, fp32 parity mode.  The trainer's DDP hook (FusionModule.all_reduce_gradients:
+    one SUM all-reduce over the tower's flat arena, one over the head, x 1/world) must leave
+    both ranks with bit-identical gradients equal to the mean of the per-shard oracle
+    gradients (per-rank BatchNorm statistics, as DDP): every tensor rel-L2 <= 1e-3 (the
+    single-rank 64 px gate of test_fusion_step_vs_oracle_fp32)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import subprocess
+    import sys
+    from tests.conftest import ROOT
+    B, H = 6, 64
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+           "--nnodes=1", "--nproc-per-node", "2", os.path.join(ROOT, "tests", "_fusion_dp_worker.py"),
+           str(tmp_path), str(B), str(H)]
+    r = subprocess.run(cmd, env=dict(os.environ, OMP_NUM_THREADS="4"), timeout=300, capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = [torch.load(tmp_path / f"r{k}.pt", weights_only=True) for k in range(2)]
+    g0, g1 = res[0]["grads"], res[1]["grads"]
+    assert g0.keys() == g1.keys() and len(g0) > 100
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), f"ranks disagree after the all-reduce: {k}"
+    full = _fusion_batch(2 * B, H)
+    ref, losses = {}, []
+    for rk in range(2):
+        o = _oracle()
+        o.train()
+        sl = slice(rk * B, (rk + 1) * B)
+        lo, fo = o(full["x-ray"][sl], full["age_encoded"][sl], full["sex_encoded"][sl],
+                   full["anatomy_site_encoded"][sl])
+        L = o.compute_loss(fo, lo, full["tumor"][sl], full["dataset"][sl])[0]
+        L.backward()
+        losses.append(L.item())
+        for k, p in o.named_parameters():
+            if p.grad is not None:
+                kk = k.replace("image_network.trunk.", "image_network.")
+                ref[kk] = ref.get(kk, 0) + p.grad.double() / 2
+    for rk in range(2):
+        assert abs(res[rk]["loss"] - losses[rk]) < 1e-4, (rk, res[rk]["loss"], losses[rk])
+    checked = 0
+    for k, g in g0.items():
+        if k not in ref or ref[k].norm() < 1e-6:    # biases feeding BatchNorm1d: analytically 0
+            continue
+        e = _rel(g, ref[k])
+        assert e <= 1e-3, (k, e)
+        checked += 1
+    assert checked > 100

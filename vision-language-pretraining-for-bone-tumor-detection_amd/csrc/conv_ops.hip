@@ -2165,9 +2165,12 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
 // barrier before its first half-step, group 0 one after its last.  Hazards (u =
 // half-step, #k = barrier k; group 0 reads in (#2u+1, #2u+2), group 1 in (#2u+2,
 // #2u+3)): B(u+3) is written after #2u+2, its slot last read before #2u+1; B(v) is
-// waited for by group 1 before #2v and read after #2v+1; window c+1's last piece
-// is waited for by group 0 before #(2 (18c + PPW + 1) + 1) <= #36c+37, the first
-// read of chunk c+1.
+// waited for by group 1 before #2v and read after #2v+1; window c+1's pieces go
+// out at half-steps 18c+1 .. 18c+PPW (PPW <= 16), the last waited for by group 0
+// before #36c+37, the first read of chunk c+1.  Window buffer reuse: chunk c+1's
+// first piece is written after #36c+3; the last reads of that buffer (chunk c-1)
+// are group 1's at half-step 18c-1, issued before #36c+1 and retired by its
+// lgkmcnt(0) before it reaches #36c+2 (one barrier of margin, as the B ring).
 template <int TW, int BN, bool FLIP, class EP>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
 conv3x3_winpp_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsigned xbytes, KMat<bf16> lb, EP ep,
@@ -2294,7 +2297,7 @@ conv3x3_winpp_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, uns
         constexpr int S = decltype(sc_)::value;
         constexpr int SL = (S + 2 * PC) & 3;
         if constexpr (G == 0) {
-          wait_vmcnt<(S >= 1 && S <= PPW) ? 1 : 0>();   // pieces of half-step S-2 landed
+          wait_vmcnt<(S >= 2 && S <= PPW + 1) ? 1 : 0>();   // pieces of half-step S-2 landed
         } else {
           wait_vmcnt<SB::P>();                           // B(u+1) landed
         }
@@ -2302,8 +2305,11 @@ conv3x3_winpp_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, uns
         raw_barrier();
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (G == 0) {
-          if constexpr (S < PPW) {
-            constexpr int I = S < PPW ? S : 0;
+          // piece I = S-1 at half-steps 1..PPW: the first write into wnext follows
+          // barrier #36c+3, after group 1's lgkmcnt(0) on its last reads of that
+          // buffer (chunk c-1, half-step 17, completed before its barrier #36c+2)
+          if constexpr (S >= 1 && S <= PPW) {
+            constexpr int I = S >= 1 && S <= PPW ? S - 1 : 0;
             if (LS >= 0 && cc + 1 == NC) {
               const int j = wg * PPW + I, row = j * 4 + (lane >> 4);
               const unsigned o = row < BM ? (unsigned)(((row0 + row) * sh.N + col0) * 2 + (lane & 15) * 16) : kOOB;
@@ -2383,7 +2389,8 @@ static bool win_ok(const ConvGeom& g, int cin, int nout) {
   return g.KH == 3 && g.KW == 3 && g.S == 1 && g.P == 1 && (g.W == 16 || g.W == 32 || g.W == 64) &&
          ((VLP_WIN_WIDTHS >> (g.W / 16)) & 1) &&
          g.H % (256 / g.W) == 0 && cin % 128 == 0 && nout % 128 == 0 &&
-         (size_t)g.N * g.H * g.W * cin * 2 < (1ull << 31);
+         // 32-bit offsets into the input AND the [M][nout] epilogue operands / outputs
+         (size_t)g.N * g.H * g.W * (cin > nout ? cin : nout) * 2 < (1ull << 31);
 }
 template <int TW, bool FLIP, int XF, class EP, bool PS = false>
 static int launch_win_t(const ConvGeom& g, int cin, int nout, const void* x, const void* w, const EP& ep,

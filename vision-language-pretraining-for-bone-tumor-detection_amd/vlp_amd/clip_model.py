@@ -40,6 +40,11 @@ class ClipHead(ArenaModule):
         if embedding_dim % 4 or not 4 <= embedding_dim <= MAX_EMBEDDING_DIM:
             raise ValueError(f"embedding_dim={embedding_dim}: the HIP contrastive head supports multiples of 4 "
                              f"up to {MAX_EMBEDDING_DIM} (vlp_clip_loss_fused)")
+        if compute_dtype == "bf16" and embedding_dim % 8:
+            # the bf16 projection matmuls (vlp_matmul) take E as a contiguous extent,
+            # which must be a multiple of 8 bf16 elements (16-B rows)
+            raise ValueError(f"embedding_dim={embedding_dim}: compute_dtype='bf16' needs a multiple of 8 "
+                             "(16-byte rows in the bf16 projection matmuls)")
         self.image_dim, self.text_dim, self.embedding_dim = image_dim, text_dim, embedding_dim
         self.compute_dtype = compute_dtype
         self._init_arena([("image_projection", (image_dim, embedding_dim)),
@@ -217,7 +222,7 @@ class ClipStepFn(torch.autograd.Function):
         # referenced until the join below.
         reducer = vdist.GradReducer()
         on_stage = None
-        if vdist.world()[1] > 1:
+        if vdist.active():
             def on_stage(off, n):
                 reducer.reduce_span(img_t.arena, off, n)
         s_txt = _text_stream(dcls.device)

@@ -22,10 +22,25 @@ import torch
 import torch.distributed as dist
 
 
+# One-GPU rehearsal of the data-parallel schedule (bench.py --dp-rehearsal):
+# with a world-1 process group initialised, every collective below is still
+# issued (RCCL on one rank), and ClipStepFn wires the per-stage bucket
+# callbacks exactly as at world > 1, so the multi-GPU stream schedule runs and
+# is timed on one GPU.
+REHEARSE = False
+
+
 def world():
     if dist.is_available() and dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
     return 0, 1
+
+
+def active() -> bool:
+    """True when the step exchanges data: world > 1, or a world-1 group in rehearsal."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return dist.get_world_size() > 1 or REHEARSE
 
 
 def _staged(t: torch.Tensor) -> bool:
@@ -42,7 +57,7 @@ class _Done:
 
 def all_gather_rows(x: torch.Tensor) -> torch.Tensor:
     r, w = world()
-    if w == 1:
+    if not active():
         return x
     if _staged(x):
         parts = [torch.empty_like(x, device="cpu") for _ in range(w)]
@@ -55,7 +70,7 @@ def all_gather_rows(x: torch.Tensor) -> torch.Tensor:
 
 def reduce_scatter_rows(x_all: torch.Tensor) -> torch.Tensor:
     r, w = world()
-    if w == 1:
+    if not active():
         return x_all
     rows = x_all.shape[0] // w
     if _staged(x_all):
@@ -68,8 +83,7 @@ def reduce_scatter_rows(x_all: torch.Tensor) -> torch.Tensor:
 
 
 def all_reduce_sum_(t: torch.Tensor, async_op: bool = False):
-    r, w = world()
-    if w == 1:
+    if not active():
         return None
     if _staged(t) and t.is_cuda:
         h = t.detach().cpu()
