@@ -3,14 +3,15 @@ by pytest): one rank of a world-size-2 late-fusion finetune step (BASELINE
 configs[4]) through the trainer's data-parallel gradient averaging.
 
 Launched by torch.distributed.run with the gloo backend, both ranks on the box's
-one GPU.  Each rank builds the same FusionModule (fp32 parity mode, the oracle's
-weights), takes its B-row shard of a 2B-row batch and runs ONE step of
+one GPU.  Each rank builds the same FusionModule (fp32 parity mode, the module's
+own seeded initialisation, saved by rank 0 for the oracle), takes its B-row shard of a 2B-row batch and runs ONE step of
 src/utils/trainer.py's `Trainer.fit`: training_step + backward, then
 `Trainer.average_gradients` -> FusionModule.all_reduce_gradients (one SUM
 all-reduce over the tower's flat gradient arena, one over the head, x 1/world),
 then the optimizer step at lr = 0 (weights unchanged, so p.grad after fit is the
-averaged gradient).  Writes every parameter gradient and the local loss to
-<outdir>/r<rank>.pt.
+averaged gradient; fit zeroes the gradients first).  Before fit the rank's own
+gradient (training_step + backward, no collective) is taken on the same shard.
+Writes both gradient sets and the local loss to <outdir>/r<rank>.pt.
 """
 import functools
 import os
@@ -32,20 +33,28 @@ def main():
     torch.cuda.set_device(0)
     from src.models.baseline.FusionModule import FusionModule
     from src.utils.trainer import Trainer
-    from tests.test_fusion import _fusion_batch, _oracle
+    from tests.test_fusion import _fusion_batch
 
-    o = _oracle()
+    # the module's own initialisation (timm init, zero-init last BN: what a finetune
+    # from scratch starts from), identical on both ranks; rank 0 hands it to the test
+    torch.manual_seed(0)
     m = FusionModule("resnet34", functools.partial(torch.optim.AdamW, lr=0.0, weight_decay=0.0),
                      label_weights=(0.7, 2.0), coral_lambda=0.5, compute_dtype="fp32")
-    m.load_state_dict(o.state_dict_hip_layout(), strict=True)
+    if rank == 0:
+        torch.save({k: v.detach().cpu() for k, v in m.state_dict().items()}, os.path.join(outdir, "init.pt"))
     full = _fusion_batch(world * B, H)
     sl = slice(rank * B, (rank + 1) * B)
     shard = {k: (v[sl] if torch.is_tensor(v) else v[sl]) for k, v in full.items() if k != "x-ray-u8"}
+    # this rank's own gradient first (no collective): the averaged one must be the mean of these
+    m.train()
+    m.training_step({k: (v.cuda() if torch.is_tensor(v) else v) for k, v in shard.items()}).backward()
+    torch.cuda.synchronize()
+    local = {k: p.grad.detach().cpu().clone() for k, p in m.named_parameters() if p.grad is not None}
     tr = Trainer(max_epochs=1, enable_checkpointing=False)
     tr.fit(m, train_dataloaders=[shard])
     torch.cuda.synchronize()
     grads = {k: p.grad.detach().cpu().clone() for k, p in m.named_parameters() if p.grad is not None}
-    torch.save({"grads": grads, "loss": float(m.logged["train/loss"].detach())},
+    torch.save({"grads": grads, "local": local, "loss": float(m.logged["train/loss"].detach())},
                os.path.join(outdir, f"r{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
