@@ -110,11 +110,8 @@ def test_conv_fwd(ops, dt, case, xform):
 
 @pytest.mark.parametrize("N,H,W,C,Co", [(32, 64, 64, 128, 128), (128, 16, 16, 512, 512)])
 def test_conv_fwd_window_many_tiles(ops, N, H, W, C, Co):
-    """The LDS-window forward at >= 2 tiles per CU, tile count a multiple of 8 (the
-    shapes where a build with VLP_WIN_PP=0 takes the persistent form: one workgroup per
-    CU walks its XCD's tiles, the next tile's window and filter slices loading over the
-    epilogue) against torch fp32 on the GPU, with the BN sums; every tile's output
-    checked."""
+    """The LDS-window forward at >= 2 tiles per CU against torch fp32 on the GPU, with
+    the BN sums; every tile's output checked."""
     torch.manual_seed(21)
     dev = torch.device("cuda")
     x = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
@@ -132,14 +129,13 @@ def test_conv_fwd_window_many_tiles(ops, N, H, W, C, Co):
     assert rel(s2.view(4, Co).sum(0).cpu(), (ref.double() ** 2).sum((0, 1, 2)).cpu()) < 1e-4
 
 
-@pytest.mark.parametrize("N,H,W,C", [(3, 5, 128, 64), (2, 128, 128, 64), (300, 4, 128, 64),
-                                     (2, 8, 64, 128), (3, 16, 32, 256), (2, 16, 16, 512)])
+@pytest.mark.parametrize("N,H,W,C", [(3, 5, 128, 64), (2, 128, 128, 64), (300, 4, 128, 64)])
 def test_conv_fwd_act_matches_pass_then_conv(ops, N, H, W, C):
-    """vlp_conv_fwd_act (bn1 + ReLU applied once per input element: in the layer-1
-    rows kernel's ring, W = 128; in the window of the LDS-window kernel, layers
-    2-4) against the separate bn_add_relu pass + conv_fwd: a1 and y bit-identical,
-    BN sums equal up to fp64 atomic order; N = 300 > CUs puts two images on some
-    workgroups; C = 256 / 512 has several N tiles (one writes a1)."""
+    """vlp_conv_fwd_act (bn1 + ReLU applied once per input row in the layer-1 rows
+    kernel's ring, W = 128) against the separate bn_add_relu pass + conv_fwd: a1 and
+    y bit-identical, BN sums equal up to fp64 atomic order; N = 300 > CUs puts two
+    images on some workgroups.  Layers 2-4 are refused (the r6 in-window transform
+    measured slower than the pass and was removed)."""
     torch.manual_seed(11)
     dev = torch.device("cuda")
     y1 = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
@@ -148,9 +144,9 @@ def test_conv_fwd_act_matches_pass_then_conv(ops, N, H, W, C):
     w = (torch.randn(C, C, 3, 3) * (9 * C) ** -0.5).to(torch.bfloat16).float()
     wp = torch.empty(C, 3, 3, C, dtype=torch.bfloat16, device=dev)
     ops.pack_conv(w.cuda(), wp, None)
-    if W != 128 and not ops.conv_fwd_act_ok(y1, C, 3, 3, 1, 1):
-        pytest.skip("in-window BN + ReLU not dispatched (VLP_WIN_ACT=0, DESIGN.md §4)")
     assert ops.conv_fwd_act_ok(y1, C, 3, 3, 1, 1)
+    for (w2, c2) in ((64, 128), (32, 256), (16, 512)):
+        assert not ops.conv_fwd_act_ok(torch.empty(2, 16, w2, c2, dtype=torch.bfloat16, device=dev), c2, 3, 3, 1, 1)
     a_ref = torch.empty_like(y1)
     ops.bn_add_relu(y1, sc, sh, None, None, None, a_ref)
     r1, r2 = (torch.zeros(4 * C, dtype=torch.float64, device=dev) for _ in range(2))

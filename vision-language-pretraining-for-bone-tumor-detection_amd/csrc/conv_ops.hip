@@ -1281,31 +1281,19 @@ static int gemm_wgrad(int M, int N, int K, const LA& la, const LB& lb, const EP&
 //   waves: 8, each 32 output pixels x 32 channels (MFMA 16x16x32, B = weights)
 // Requirements: C = Co = 64, 3x3, stride 1, pad 1, W = 128, bf16.
 constexpr int kRcW = 128;                        // image width handled
-// Ring row layout.  Planar (VLP_RC_PLANAR, default): 8 planes, one per 16-B
-// channel chunk, each 130 pixels x 16 B padded to 144 16-B units, so a fragment
-// read -- pixels {0-3, 12-15} of chunk c and {4-11} of chunk c+1 in one 16-lane
-// group -- falls on 16 distinct bank slots at ANY pixel offset (every filter tap
-// column); the pixel-major image with an XOR swizzle is conflict-free at tap
-// column 0 only (r5 PMC: 44 % of the data-gradient kernels' LDS cycles were
-// conflicts).  The planar rows are 11 % larger: the filter image is staged in the
-// ring area before the first row instead of beside it, and the epilogue's staging
-// tile, statistics and y row live after the ring.  Measured a wash (interleaved x2,
-// profiles/r5r2_rows_planar_ab.txt: -3 % forward, +2 % BN data gradient, the rest
-// within noise): the conflicts are not what holds these kernels; off by default.
-#ifndef VLP_RC_PLANAR
-#define VLP_RC_PLANAR 0
-#endif
-constexpr bool kRcPlanar = VLP_RC_PLANAR;
-constexpr int kRcPlane = 144 * 16;                 // planar: one chunk plane of a ring row
-constexpr int kRcSlot = kRcPlanar ? 8 * kRcPlane : (kRcW + 2) * 128;   // one ring row (bytes)
+// Ring row layout: pixel-major, 16-B chunk c of pixel p at c ^ ((p >> 1) & 7)
+// (conflict-free at tap column 0 only; r5 PMC: 44 % of the data-gradient kernels'
+// LDS cycles are conflicts, but a conflict-free planar layout measured a wash --
+// profiles/r5r2_rows_planar_ab.txt -- and was removed).
+constexpr int kRcSlot = (kRcW + 2) * 128;        // one ring row (bytes)
 constexpr int kRcWeights = 9 * 64 * 128;         // 73728
 constexpr int kRcRing = 5;
-constexpr int kRcRingOff = kRcPlanar ? 0 : kRcWeights;
-constexpr int kRcAux = kRcPlanar ? kRcRing * kRcSlot : 0;   // staging 16 KB | statistics 32 KB | y row 16 KB
-constexpr int kRcTail = kRcPlanar ? kRcAux + 65536 : kRcWeights + kRcRing * kRcSlot;   // direct-mode stats / coefficients
+constexpr int kRcRingOff = kRcWeights;
+constexpr int kRcAux = 0;                        // staging 16 KB | statistics 32 KB | y row 16 KB (filter area)
+constexpr int kRcTail = kRcWeights + kRcRing * kRcSlot;   // direct-mode stats / coefficients
 constexpr int kRcXtab = kRcTail + 2048;          // input-transform table: (scale, shift) or (k, b, c)
 constexpr int kRcLds = kRcXtab + 768;
-static_assert(kRcLds <= 160 * 1024 && (!kRcPlanar || kRcWeights <= kRcRing * kRcSlot), "rows kernel LDS map");
+static_assert(kRcLds <= 160 * 1024, "rows kernel LDS map");
 
 #ifndef VLP_ACT_NT
 #define VLP_ACT_NT 0   // non-temporal stores of the transformed input rows
@@ -1361,28 +1349,18 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
   auto zero_halo = [&]() {
     for (int q = tid; q < kRcRing * 2 * 8; q += 512) {
       const int sl = q >> 4, side = (q >> 3) & 1, c = q & 7;
-      if constexpr (kRcPlanar)
-        *reinterpret_cast<uint4*>(ring + sl * kRcSlot + c * kRcPlane + (side ? (kRcW + 1) * 16 : 0)) = zero4();
-      else
-        *reinterpret_cast<uint4*>(ring + sl * kRcSlot + (side ? (kRcW + 1) * 128 : 0) + c * 16) = zero4();
+      *reinterpret_cast<uint4*>(ring + sl * kRcSlot + (side ? (kRcW + 1) * 128 : 0) + c * 16) = zero4();
     }
   };
-  if constexpr (!kRcPlanar) zero_halo();   // (planar: the filter image occupies the ring until the fragments are loaded)
-  // the ring (or y-row) position of piece jj of this wave: planar piece j = plane
-  // j & 7, pixels 64 (j >> 3) .. +63; pixel-major piece j = pixels 8j .. 8j + 7
+  zero_halo();
+  // the ring (or y-row) position of piece jj of this wave: pixels 8j .. 8j + 7
   auto piece_src = [&](int j, int ln, int& px, int& c) __attribute__((always_inline)) {
-    if constexpr (kRcPlanar) {
-      c = j & 7;
-      px = 64 * (j >> 3) + ln;
-    } else {
-      const int q = j * 64 + ln;
-      px = q >> 3;
-      c = (q & 7) ^ (((px + 1) >> 1) & 7);
-    }
+    const int q = j * 64 + ln;
+    px = q >> 3;
+    c = (q & 7) ^ (((px + 1) >> 1) & 7);
   };
   auto piece_lds = [&](char* rowbase, int j) __attribute__((always_inline)) -> char* {
-    if constexpr (kRcPlanar) return rowbase + (j & 7) * kRcPlane + (1 + 64 * (j >> 3)) * 16;
-    else return rowbase + 128 + j * 1024;
+    return rowbase + 128 + j * 1024;
   };
   // input row i of image n -> ring slot (i + 1) % 5, pixels at ring positions 1..128
   auto fetch = [&](int n, int i) {
@@ -1411,10 +1389,6 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int b = 0; b < 2; ++b) wf[t][s][b] = frag_bf16<true, 128, true>(wlds + t * 8192, ch * 32 + b * 16, s);
-  if constexpr (kRcPlanar) {
-    __syncthreads();   // every wave holds its filter fragments: the ring area is free
-    zero_halo();
-  }
   if constexpr (RowTrait<EP>::value && EP::kStats) {
     __syncthreads();   // every wave holds its filter fragments before the area is reused
     v4f* rp = reinterpret_cast<v4f*>(red + tid * 16);
@@ -1442,7 +1416,7 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
   // and the 32 KB statistics scratch) at the same chunk positions as the ring
   // row: each thread reads back exactly the chunks its own DMA wrote
   char* ybuf = aux + 16384 + 32768;
-  static_assert(kRcPlanar || 16384 + 32768 + kRcW * 128 <= kRcWeights, "y row buffer fits the filter area");
+  static_assert(16384 + 32768 + kRcW * 128 <= kRcWeights, "y row buffer fits the filter area");
   const rsrc_t ry = XF == 2 ? buf_rsrc(xin.y, (unsigned)((size_t)N * H * kRcW * 64 * 2)) : rz;
   auto yload = [&](int n, int r) __attribute__((always_inline)) {
     const bool live = (unsigned)r < (unsigned)H;   // past the last row: a null fetch keeps the vmcnt pattern
@@ -1580,7 +1554,7 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           const int r = seed + kw;
-          foff[kw][s] = kRcPlanar ? (4 * s + lg) * kRcPlane + r * 16 : r * 128 + (((4 * s + lg) ^ ((r >> 1) & 7)) << 4);
+          foff[kw][s] = r * 128 + (((4 * s + lg) ^ ((r >> 1) & 7)) << 4);
         }
 #pragma unroll
       for (int kh = 0; kh < 3; ++kh) {
@@ -1592,9 +1566,7 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
           for (int s = 0; s < 2; ++s)
 #pragma unroll
             for (int a = 0; a < 2; ++a) {
-              if constexpr (kRowEpi) fa[s][a] = *reinterpret_cast<const v8bf*>(sl + foff[kw][s] + a * (kRcPlanar ? 256 : 2048));
-              else if constexpr (kRcPlanar)
-                fa[s][a] = *reinterpret_cast<const v8bf*>(sl + (4 * s + lg) * kRcPlane + (pq * 32 + a * 16 + kw + li) * 16);
+              if constexpr (kRowEpi) fa[s][a] = *reinterpret_cast<const v8bf*>(sl + foff[kw][s] + a * 2048);
               else fa[s][a] = frag_bf16<true, 128, true>(sl, pq * 32 + a * 16 + kw, s);
             }
 #pragma unroll
@@ -1611,7 +1583,7 @@ conv3x3_c64_rows_kernel(int N, int H, const bf16* __restrict__ x, const bf16* __
         // output row is staged as bf16, then thread t handles pixels t/8 and
         // t/8 + 64 at the FIXED 8-channel group t%8, so its operand loads and
         // stores are row-contiguous 16-B chunks
-        bf16* stg = reinterpret_cast<bf16*>(kRcPlanar ? aux : wlds);
+        bf16* stg = reinterpret_cast<bf16*>(wlds);
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
@@ -1734,33 +1706,14 @@ static int launch_rows_c64(const ConvGeom& g, const void* x, const void* w, int 
 // conflict-free for all 3 column offsets).  The LDS-DMA pieces (1 KiB per wave
 // instruction, lane -> 16 B) fill the padding from past the buffer resource
 // (zeros), as they do pixels outside the image.  Two window buffers: chunk
-// c+1's pieces are issued one per half-step over the first PPW half-steps of
-// chunk c, so the in-order vmcnt wait for each B half-tile never waits on a
-// whole window.
-// XF = 1 (forward): the window holds the raw output of the previous conv; at the
-// chunk's first half-step every thread turns its own pieces into
-// relu(sc * x + sh) (interior pixels only -- the zero padding stays zero) and
-// stores the tile's own pixels to xin.out, the activation the weight gradient
-// reads (BN-apply + ReLU without a separate pass, as the layer-1 rows kernel).
-// 8 waves: 4 (M) x 2 (N), 64 x BN/2 per wave (MFMA 16x16x32), the epilogue is the
-// multi-stage kernels' ms_epilogue<256, BN, 4, 2>.
-// timing experiments only (wrong results): 1 = no B fetches in the loop, 2 = no
-// window fetches, 3 = neither, 4 = no MFMAs, 5 = no barriers, 6 = no epilogue
-#ifndef VLP_WIN_EXP
-#define VLP_WIN_EXP 0
-#endif
-#ifndef VLP_WIN_NW
-#define VLP_WIN_NW 8   // waves per window workgroup (8: two per SIMD; 4: one per SIMD, 128 x 64 per wave)
-#endif
-#ifndef VLP_WIN_DESYNC
-#define VLP_WIN_DESYNC 0   // half the CUs start half a tile late (conv3x3_winpp_kernel); r5 A/B: no gain, off
-#endif
-#ifndef VLP_WIN_PERSIST
-#define VLP_WIN_PERSIST 1   // forward: one workgroup per CU walks its tiles, the next tile's loads over the epilogue
-#endif
-#ifndef VLP_WIN_STAMP
-#define VLP_WIN_STAMP 0   // diagnostic build: in-kernel s_memtime stamps (tools/build_variant.sh)
-#endif
+// c+1's pieces are issued over the first half-steps of chunk c, so the in-order
+// vmcnt wait for each B half-tile never waits on a whole window.  Workgroup
+// geometry: 8 waves, 4 (M) x 2 (N), 64 x BN/2 per wave (MFMA 16x16x32), in two
+// ping-pong groups (below); the epilogue is the multi-stage kernels'
+// ms_epilogue<256, BN, 4, 2>.  (r5: a lock-step 8-wave form, a persistent forward
+// and timing-experiment builds were measured against this one and removed; their
+// records are profiles/r5q3_window_pingpong_ab.txt, r5p3_window_persistent_ab.txt,
+// r5x_window_experiments.txt, r5ds_window_desync_ab.json.)
 template <int TW, int NW = 8, int MINP = 0>
 struct WinGeom {
   static constexpr int TH = 256 / TW;                  // image rows per tile
@@ -1773,387 +1726,10 @@ struct WinGeom {
   static constexpr int PPW = PPW0 * NW >= MINP ? PPW0 : (MINP + NW - 1) / NW;
   static constexpr int SLOT = PPW * NW * 1024;         // one window buffer
 };
-struct WinXIn {
-  const float* sc; const float* sh;   // XF 1: per-channel BN scale / shift of the input
-  bf16* out;                          // XF 1: relu(sc * x + sh) of the tile's pixels
-};
-// persistent form (PS): the forward's staged epilogue, tiles walked by one workgroup per CU
-template <class EP, bool FLIP, int XF, bool PS>
-constexpr bool win_pers() { return PS && !FLIP && XF == 0 && LdsSlotTrait<EP>::value < 0 && StageTrait<EP>::value; }
-template <class EP, bool PERS = false> constexpr int win_minp() { return LdsSlotTrait<EP>::value >= 0 || PERS ? 64 : 0; }
-template <int TW, int BN, int NW = 8, int MINP = 0>
-constexpr int win_lds_bytes() { return 2 * WinGeom<TW, NW, MINP>::SLOT + 4 * BN * 64; }
+// 64 pieces per buffer when the row epilogue's operand tile [256][128] bf16 is staged in the spare buffer
+template <class EP> constexpr int win_minp() { return LdsSlotTrait<EP>::value >= 0 ? 64 : 0; }
 
-// NW = 8: 4 x 2 waves of 64 x BN/2, two waves per SIMD; NW = 4: 2 x 2 waves of
-// 128 x BN/2, one wave per SIMD (up to 512 registers: operand sets
-// double-buffered, half the LDS fragment reads per MFMA)
-template <int TW, int BN, int NW, bool FLIP, int XF, class EP, bool PS = false>
-__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 8 ? 2 : 1)))
-conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsigned xbytes, KMat<bf16> lb, EP ep,
-                   WinXIn xin) {
-  constexpr int LS = LdsSlotTrait<EP>::value;
-  constexpr bool PERS = win_pers<EP, FLIP, XF, PS>();
-  static_assert(!PS || PERS, "persistent form: forward, staged epilogue");
-  using WG = WinGeom<TW, NW, win_minp<EP, PERS>()>;
-  constexpr int BM = 256, WGN = 2, WGM = NW / WGN, NT = NW * 64;
-  static_assert(LS < 0 || BN == 128, "the staged epilogue operand is a [256][128] bf16 image");
-  constexpr int WTN = BN / WGN;
-  constexpr int MB = BM / WGM / 16, NB = WTN / 16;
-  constexpr int BSLOT = BN * 64;
-  constexpr int PPW = WG::PPW;
-  using SB = HStager<BN, KMat<bf16>, NT>;
-  static_assert(XF == 0 || NW == 8, "the in-window transform schedule assumes 8 waves");
-  static_assert(PPW <= 16, "window pieces are issued over the first half-steps of a chunk");
-  static_assert(win_lds_bytes<TW, BN, NW, win_minp<EP, PERS>()>() <= 160 * 1024 &&
-                    BM * BN * 2 + 4096 <= win_lds_bytes<TW, BN, NW, win_minp<EP, PERS>()>(),
-                "LDS budget");
-  static_assert(!PERS || (BM * BN * 2 <= WG::SLOT && 2 * BN * 2 * 4 * 4 <= BN * 64), "persistent epilogue scratch");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* const win = smem;
-  char* const ring = smem + 2 * WG::SLOT;
-
-#if VLP_WIN_STAMP
-  const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-#endif
-  const int nwg = sh.tiles_m * sh.tiles_n;
-  const int bid = blockIdx.x;
-  int g = bid;
-  // PERS: grid = a multiple of 8 workgroups, nwg % 8 == 0; XCD x walks tiles
-  // [x * nwg/8, (x+1) * nwg/8), its workgroups interleaved (consecutive tiles share halos)
-  const int pgx = gridDim.x >> 3, pslot = bid >> 3, pper = nwg >> 3;
-  if constexpr (PERS) {
-    g = (bid & 7) * pper + pslot;
-  } else if (nwg >= 16) {   // consecutive tiles (shared halo rows) on one XCD
-    const int xcd = bid & 7, idx = bid >> 3, q = nwg >> 3, rr = nwg & 7;
-    g = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + idx;
-  }
-  int tm = g / sh.tiles_n, tn = g - tm * sh.tiles_n;
-  int row0 = tm * BM, col0 = tn * BN;
-  int n = row0 / (H * TW), h0 = (row0 - n * H * TW) / TW;
-  auto set_tile = [&](int gg) __attribute__((always_inline)) {
-    g = gg;
-    tm = g / sh.tiles_n;
-    tn = g - tm * sh.tiles_n;
-    row0 = tm * BM;
-    col0 = tn * BN;
-    n = row0 / (H * TW);
-    h0 = (row0 - n * H * TW) / TW;
-  };
-  const int NC = C / 64;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wv / WGN, wn = wv - wm * WGN;
-  const int li = lane & 15, lg = lane >> 4;
-
-  // this thread's window pieces: LDS byte -> (pixel, 16-B chunk) -> source
-  // offset in channel chunk 0 (kOOB for padding and outside the image)
-  const rsrc_t rx = buf_rsrc(x, xbytes);
-  const rsrc_t rb = lb.rsrc();
-  const rsrc_t rz = null_rsrc(zero_page());
-  unsigned woff[PPW];
-  unsigned woffn[PERS ? PPW : 1];   // PERS: the next tile's (window 0 is fetched during the last chunk)
-  auto calc_woff = [&](unsigned* wo, int tn_, int th0) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-      const int off = (wv * PPW + i) * 1024 + lane * 16;
-      const int p = off / WG::PS, c = (off - p * WG::PS) >> 4;
-      const int wr = p / WG::WC, wc = p - wr * WG::WC;
-      const int hh = th0 - 1 + wr, ww = wc - 1;
-      const bool ok = c < 8 && p < WG::WR * WG::WC && hh >= 0 && hh < H && ww >= 0 && ww < TW;
-      wo[i] = ok ? (unsigned)((((tn_ * H + hh) * TW + ww) * C) * 2 + c * 16) : kOOB;
-      // XF 1: the window's two spare pieces (wave 7's last two) carry the chunk's
-      // 64 BN scales / shifts (lanes 0-15, 16 B each) into the window buffer
-      if (XF == 1 && wv == NW - 1 && i >= PPW - 2) wo[i] = lane < 16 ? (unsigned)lane * 16u : kOOB;
-    }
-  };
-  calc_woff(woff, n, h0);
-  const rsrc_t rsc = XF == 1 ? buf_rsrc(xin.sc, (unsigned)C * 4u) : rz;
-  const rsrc_t rsh = XF == 1 ? buf_rsrc(xin.sh, (unsigned)C * 4u) : rz;
-  // LS >= 0: the pieces of "chunk NC" (issued during the last chunk into its spare
-  // buffer) fetch the epilogue's operand tile instead, [256 rows][256 B] from
-  // rows row0.., columns col0..col0+127 of the [M][sh.N] operand
-  rsrc_t rop = rz;
-  if constexpr (LS >= 0) rop = buf_rsrc(ep.lds_operand(), (unsigned)((size_t)sh.M * sh.N * 2));
-  // window piece i of chunk cc into buffer wb (chunk cc >= NC: zeros)
-  auto wpiece = [&](auto ic, int cc, char* wb, const unsigned* wo) __attribute__((always_inline)) {
-    constexpr int I = decltype(ic)::value;
-    if constexpr (LS >= 0) {
-      if (cc == NC) {
-        const int j = wv * PPW + I, row = j * 4 + (lane >> 4);
-        const unsigned o = row < BM ? (unsigned)(((row0 + row) * sh.N + col0) * 2 + (lane & 15) * 16) : kOOB;
-        dma16(rop, o, wb + j * 1024);
-        return;
-      }
-    }
-    rsrc_t r = cc < NC ? rx : rz;
-    unsigned inc = 128u;
-    if constexpr (XF == 1 && I >= PPW - 2) {
-      if (wv == NW - 1) {
-        r = cc < NC ? (I == PPW - 2 ? rsc : rsh) : rz;
-        inc = 256u;
-      }
-    }
-    dma16(r, wo[I] + (unsigned)cc * inc, wb + (wv * PPW + I) * 1024);
-  };
-  SB sb, sbn;
-  sb.init(lb, col0, 0, wv);
-  // B half-tile hc of tap t, channel chunk cc (cc == NC: past the end, zeros)
-  auto bfetch = [&](auto hc, int t, int cc, char* slot) __attribute__((always_inline)) {
-    if constexpr (VLP_WIN_EXP == 1 || VLP_WIN_EXP == 3) if (t + cc > 0) return;
-    sb.template issue<decltype(hc)::value>(lb, cc < NC ? rb : rz, t * C + cc * 64, slot, wv);
-  };
-  int kt = 0;          // PERS: tiles done by this workgroup
-  bool more = false;   // PERS: a next tile follows the current one
-  // PERS: the next tile's window offsets and B loader state, prepared a tile ahead
-  auto prep_next = [&]() __attribute__((always_inline)) {
-    if constexpr (PERS) {
-      more = pslot + (kt + 1) * pgx < pper;
-      if (more) {
-        const int gn = g + pgx;
-        const int tmn = gn / sh.tiles_n, tnn = gn - tmn * sh.tiles_n;
-        const int r0n = tmn * BM, nn = r0n / (H * TW);
-        calc_woff(woffn, nn, (r0n - nn * H * TW) / TW);
-        sbn.init(lb, tnn * BN, 0, wv);
-      }
-    }
-  };
-  prep_next();
-
-  v4f acc[MB][NB];
-#pragma unroll
-  for (int a = 0; a < MB; ++a)
-#pragma unroll
-    for (int b = 0; b < NB; ++b) acc[a][b] = v4f{0.f, 0.f, 0.f, 0.f};
-  // A fragment of lane (li, lg): pixel li of the fragment's 16, 16-B chunk lg
-  // of the half-step's 32 channels (tap and half: compile-time offsets)
-  const int aoff = li * WG::PS + lg * 16;
-  const int wpx = wm * (BM / WGM);   // the wave's first pixel in the tile
-  const char* const bbase = ring + li * 64 + (pp_chunk(li, lg) << 4) + wn * WTN * 64;
-
-  // XF 1: element k of a window for this thread = 16-B chunk c16 = tid & 7 of
-  // window pixel (tid >> 3) + 64 k; interior pixels become relu(sc * x + sh) in
-  // place (the zero padding stays zero), k = 0 .. KX-1.  The transform of window
-  // cc+1 runs one element per half-step over half-steps X0 .. X0+KX-1 of chunk cc
-  // (all pieces landed and visible from half-step PPW + 1), the stores of the
-  // tile's own pixels to xin.out over half-steps 1 .. KX of chunk cc+1 (read back
-  // from the window; one N tile stores).
-  constexpr int KX = (WG::WR * WG::WC + 63) / 64;
-  constexpr int X0 = PPW + 1;
-  static_assert(XF == 0 || (X0 + KX <= 17 && KX <= 16 && (WG::BYTES + 1023) / 1024 <= 8 * PPW - 2), "XF schedule");
-  const int c16 = tid & 7;
-  v4f xs0, xs1, xh0, xh1;
-  auto xcoef = [&](const char* wb) __attribute__((always_inline)) {
-    const float* t = reinterpret_cast<const float*>(wb + (8 * PPW - 2) * 1024) + c16 * 8;
-    xs0 = *reinterpret_cast<const v4f*>(t);
-    xs1 = *reinterpret_cast<const v4f*>(t + 4);
-    xh0 = *reinterpret_cast<const v4f*>(t + 256);
-    xh1 = *reinterpret_cast<const v4f*>(t + 260);
-  };
-  // window pixel of element k -> (inside the image, inside the tile's rows)
-  auto xpix = [&](int k, bool& img, bool& own) __attribute__((always_inline)) {
-    int t = tid;
-    asm volatile("" : "+v"(t));   // recomputed where used: not hoisted into registers across the chunk loop
-    const int p = (t >> 3) + 64 * k;
-    const int wr = p / WG::WC, wc = p - wr * WG::WC;
-    const int hh = h0 - 1 + wr;
-    img = p < WG::WR * WG::WC && hh >= 0 && hh < H && wc >= 1 && wc <= TW;
-    own = img && wr >= 1 && wr <= WG::TH;
-    return p;
-  };
-  auto xelem = [&](int k, char* wb) __attribute__((always_inline)) {
-    bool img, own;
-    const int p = xpix(k, img, own);
-    if (img) {
-      uint4* q = reinterpret_cast<uint4*>(wb + p * WG::PS + c16 * 16);
-      float f[8];
-      Chunk<bf16>::unpack(*q, f);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        f[j] = fmaxf(fmaf(f[j], xs0[j], xh0[j]), 0.f);
-        f[4 + j] = fmaxf(fmaf(f[4 + j], xs1[j], xh1[j]), 0.f);
-      }
-      *q = Chunk<bf16>::pack(f);
-    }
-  };
-  // one buffer store per thread and half-step whatever the lane's pixel (others
-  // past the resource: dropped), so every wave's vmcnt bookkeeping is the same
-  const rsrc_t rxo = XF == 1 ? buf_rsrc(xin.out, xbytes) : rz;
-  auto xstore = [&](int k, int cc, const char* wb) __attribute__((always_inline)) {
-    bool img, own;
-    const int p = xpix(k, img, own);
-    const int wr = p / WG::WC, wc = p - wr * WG::WC;
-    const unsigned e = (unsigned)((((n * H + h0 - 1 + wr) * TW + (wc - 1)) * C + cc * 64 + c16 * 8) * 2);
-    typedef unsigned v4u_ __attribute__((__vector_size__(16)));
-    const v4u_ v = *reinterpret_cast<const v4u_*>(wb + p * WG::PS + c16 * 16);
-    __builtin_amdgcn_raw_buffer_store_b128(v, rxo, own && tn == 0 ? e : kOOB, 0, 0);
-  };
-  // fragments of half-step (tap t, half hh) from window buffer wb, ring slot sl
-  v8bf fa[2][MB], fb[2][NB];
-  auto rd = [&](auto setc, auto sc_, char* wb, int sl) __attribute__((always_inline)) {
-    constexpr int R = decltype(setc)::value, S = decltype(sc_)::value;
-    constexpr int T = S >> 1, HH = S & 1;
-    constexpr int KH = FLIP ? 2 - T / 3 : T / 3, KW = FLIP ? 2 - T % 3 : T % 3;
-#pragma unroll
-    for (int a = 0; a < MB; ++a) {
-      const int px = wpx + a * 16;   // wave-uniform
-      const int wrow = px / TW + KH, wcol = px % TW;
-      fa[R][a] = *reinterpret_cast<const v8bf*>(wb + aoff + (wrow * WG::WC + wcol + KW) * WG::PS + HH * 64);
-    }
-#pragma unroll
-    for (int b = 0; b < NB; ++b) fb[R][b] = *reinterpret_cast<const v8bf*>(bbase + sl * BSLOT + b * 16 * 64);
-  };
-
-  using H0 = std::integral_constant<int, 0>;
-  using H1 = std::integral_constant<int, 1>;
-  using Z = std::integral_constant<int, 0>;
-  static_for<0, PPW>([&](auto ic) { wpiece(ic, 0, win, woff); });
-  bfetch(H0{}, 0, 0, ring);
-  bfetch(H1{}, 0, 0, ring + BSLOT);
-  bfetch(H0{}, 1, 0, ring + 2 * BSLOT);
-  wait_vmcnt<2 * SB::P>();   // window 0 and B(0)
-  raw_barrier();
-  if constexpr (XF == 1) {
-    xcoef(win);
-#pragma unroll
-    for (int k = 0; k < KX; ++k) xelem(k, win);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    raw_barrier();
-  }
-  rd(Z{}, Z{}, win, 0);
-
-  // one 64-channel chunk; PC (= cc & 1) selects the window buffer.  Half-step
-  // u = cc * 18 + S computes with the fragment set S & 1 read one half-step
-  // earlier, reads the next set, and fetches B(u + 3) into ring slot (u + 3) & 3
-  // (slot of B(v) = v & 3 = (S + 2 * PC) & 3).
-  // LAST (PERS): the tile's last chunk prefetches the NEXT tile's window 0 and
-  // B(0..2) where the other chunks fetch their successor's, and skips the
-  // fragment reads for the half-step after it (read after the epilogue)
-  auto chunk = [&](auto pc, auto lastc, int cc) __attribute__((always_inline)) {
-    constexpr int PC = decltype(pc)::value;
-    constexpr bool LAST = decltype(lastc)::value;
-    char* const wbuf = win + PC * WG::SLOT;
-    char* const wnext = win + (1 - PC) * WG::SLOT;
-    static_for<0, 18>([&](auto sc_) {
-      constexpr int S = decltype(sc_)::value;
-      constexpr int R = S & 1;
-      constexpr int SL = (S + 2 * PC) & 3;
-      // B(u+1) landed: issued after it are the previous half-step's window piece
-      // (half-steps 1..PPW) and B(u+2)
-      // (XF 1: and its x_act store, half-steps 2 .. KX+1; vmcnt retires in issue order)
-      // (PERS, the first two half-steps after an epilogue: and its 8 tile stores)
-      constexpr int NPRE = (S >= 1 && S <= PPW ? 1 : 0) + (XF == 1 && S >= 2 && S <= KX + 1 ? 1 : 0);
-      if constexpr (PERS && PC == 0 && S <= 1) {
-        if (cc == 0 && kt > 0) wait_vmcnt<SB::P + NPRE + 8>();
-        else wait_vmcnt<SB::P + NPRE>();
-      } else {
-        wait_vmcnt<SB::P + NPRE>();
-      }
-      if constexpr (XF == 1 && S == 17) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // transformed window cc+1
-      if constexpr (VLP_WIN_EXP != 5) raw_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (S < PPW && VLP_WIN_EXP != 2 && VLP_WIN_EXP != 3) {
-        if constexpr (LAST) wpiece(std::integral_constant<int, S < PPW ? S : 0>{}, more ? 0 : NC, wnext, woffn);
-        else wpiece(std::integral_constant<int, S < PPW ? S : 0>{}, cc + 1, wnext, woff);
-      }
-      // XF 1: the stores of window cc's own pixels, one element per half-step
-      // (issued right after the barrier: the next half-step's wait retires them)
-      if constexpr (XF == 1 && S >= 1 && S <= KX) xstore(S - 1, cc, wbuf);
-      constexpr int S3 = S + 3 < 18 ? S + 3 : S + 3 - 18;   // half-step u + 3 = (chunk, S3)
-      if constexpr (LAST && S + 3 >= 18) {
-        // the next tile's B(0..2) (its chunk 0), or nothing past the last tile
-        if constexpr (VLP_WIN_EXP != 1 && VLP_WIN_EXP != 3)
-          sbn.template issue<S3 & 1>(lb, more ? rb : rz, (S3 >> 1) * C, ring + ((SL + 3) & 3) * BSLOT, wv);
-      } else {
-        bfetch(std::integral_constant<int, S3 & 1>{}, S3 >> 1, S + 3 < 18 ? cc : cc + 1, ring + ((SL + 3) & 3) * BSLOT);
-      }
-      if constexpr (S + 1 < 18) rd(std::integral_constant<int, 1 - R>{}, std::integral_constant<int, S + 1>{}, wbuf, (SL + 1) & 3);
-      else if constexpr (!LAST) rd(std::integral_constant<int, 1 - R>{}, Z{}, wnext, (SL + 1) & 3);
-      __builtin_amdgcn_sched_barrier(0);
-#if VLP_PP_PRIO
-      __builtin_amdgcn_s_setprio(1);
-#endif
-      if constexpr (VLP_WIN_EXP == 4) {
-#pragma unroll
-        for (int a = 0; a < MB; ++a) acc[a][0][0] += (float)fa[R][a][0] + (float)fb[R][a][0];
-      } else {
-#pragma unroll
-      for (int a = 0; a < MB; ++a)
-#pragma unroll
-        for (int b = 0; b < NB; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[R][b], fa[R][a], acc[a][b], 0, 0, 0);
-      }
-#if VLP_PP_PRIO
-      __builtin_amdgcn_s_setprio(0);
-#endif
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (XF == 1 && S >= X0 && S < X0 + KX) {
-        if (cc + 1 < NC) {
-          if constexpr (S == X0) xcoef(wnext);
-          xelem(S - X0, wnext);
-        }
-      }
-    });
-  };
-  using P0 = std::integral_constant<int, 0>;
-  using P1 = std::integral_constant<int, 1>;
-  using NL = std::integral_constant<bool, false>;
-  if constexpr (PERS) {
-    for (;;) {
-      for (int cc = 0; cc < NC - 2; cc += 2) {
-        chunk(P0{}, NL{}, cc);
-        chunk(P1{}, NL{}, cc + 1);
-      }
-      chunk(P0{}, NL{}, NC - 2);
-      chunk(P1{}, std::integral_constant<bool, true>{}, NC - 1);
-      // buffer 1 (the last chunk's window) and ring slot 3 are free; the next
-      // tile's window 0 and B(0..2) are landing in buffer 0 and slots 0..2.
-      // The epilogue's stores stay in flight into the next tile (counted by its
-      // first two waits; vmcnt retires in issue order)
-      ms_epilogue<BM, BN, WGM, WGN, EP, false, true>(sh, ep, acc, row0, col0, g, wm, wn, smem + WG::SLOT, nullptr,
-                                                      reinterpret_cast<float*>(ring + 3 * BSLOT));
-      if (!more) break;
-      set_tile(g + pgx);
-#pragma unroll
-      for (int i = 0; i < PPW; ++i) woff[i] = woffn[i];
-      sb = sbn;
-      ++kt;
-      prep_next();
-#pragma unroll
-      for (int a = 0; a < MB; ++a)
-#pragma unroll
-        for (int b = 0; b < NB; ++b) acc[a][b] = v4f{0.f, 0.f, 0.f, 0.f};
-      rd(Z{}, Z{}, win, 0);
-    }
-    wait_vmcnt<0>();
-    return;
-  }
-  for (int cc = 0; cc < NC; cc += 2) {
-    chunk(P0{}, NL{}, cc);
-    chunk(P1{}, NL{}, cc + 1);
-  }
-  wait_vmcnt<0>();
-  __syncthreads();   // ring and windows drained (incl. the null-resource tail fetches) before LDS is reused
-  if constexpr (VLP_WIN_EXP == 6) if (sh.dbg != 7) return;
-#if VLP_WIN_STAMP
-  const unsigned long long t_loop = __builtin_amdgcn_s_memtime();
-#endif
-  if constexpr (LS >= 0) {
-    // NC is even: the last chunk read buffer 1, its spare buffer 0 holds the operand
-    // tile; the staging tile goes to buffer 1 (+ the free ring)
-    ms_epilogue<BM, BN, WGM, WGN, EP, true>(sh, ep, acc, row0, col0, g, wm, wn, smem + WG::SLOT, smem);
-  } else {
-    ms_epilogue<BM, BN, WGM, WGN, EP>(sh, ep, acc, row0, col0, g, wm, wn, smem);
-  }
-#if VLP_WIN_STAMP
-  __syncthreads();
-  if (XF == 0 && threadIdx.x == 0) {
-    unsigned long long* st = reinterpret_cast<unsigned long long*>(xin.out) + (size_t)bid * 4;
-    st[0] = t_start; st[1] = t_loop; st[2] = __builtin_amdgcn_s_memtime(); st[3] = __builtin_amdgcn_s_memrealtime();
-  }
-#endif
-}
-
-// Ping-pong form of the window kernel (VLP_WIN_PP).  The two wave groups (rows
+// Ping-pong window kernel (conv3x3_winpp_kernel).  The two wave groups (rows
 // 0-127: waves 0-3, rows 128-255: waves 4-7; one wave of each per SIMD) run one
 // barrier interval apart, as in gemm_pp_kernel: every half-step is [wait, barrier,
 // fetch + fragment reads, barrier, MFMAs], so in each interval one group's MFMAs
@@ -2171,10 +1747,13 @@ conv3x3_win_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsig
 // first piece is written after #36c+3; the last reads of that buffer (chunk c-1)
 // are group 1's at half-step 18c-1, issued before #36c+1 and retired by its
 // lgkmcnt(0) before it reaches #36c+2 (one barrier of margin, as the B ring).
+//
+// (r6: BN-apply + ReLU of the input applied in the window, XF = 1, was built here
+// -- bit-identical to the pass + conv -- and measured slower than the separate
+// pass at every width: profiles/r6_window_act_ab.txt; removed.)
 template <int TW, int BN, bool FLIP, class EP>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
-conv3x3_winpp_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsigned xbytes, KMat<bf16> lb, EP ep,
-                     int first_round, int desync) {
+conv3x3_winpp_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, unsigned xbytes, KMat<bf16> lb, EP ep) {
   // LS >= 0: group 0's last-chunk pieces fetch the row epilogue's operand tile (as
   // conv3x3_win_kernel) into the spare window buffer
   constexpr int LS = LdsSlotTrait<EP>::value;
@@ -2211,13 +1790,6 @@ conv3x3_winpp_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, uns
   const rsrc_t rz = null_rsrc(zero_page());
   rsrc_t rop = rz;
   if constexpr (LS >= 0) rop = buf_rsrc(ep.lds_operand(), (unsigned)((size_t)sh.M * sh.N * 2));
-  // desync > 0: every other CU of each XCD starts its first tile ~desync cycles late,
-  // so the CUs' epilogues (HBM operand loads and stores, MFMAs idle) fall in two
-  // phases instead of one chip-wide burst per round; the offset persists as each
-  // CU takes its next tile when it frees up
-  if (desync > 0 && bid < first_round && ((bid >> 3) & 1)) {
-    for (int t = 0; t < desync; t += 8128) __builtin_amdgcn_s_sleep(127);
-  }
 
   v4f acc[MB][NB];
 #pragma unroll
@@ -2305,10 +1877,10 @@ conv3x3_winpp_kernel(GemmShape sh, int H, int C, const bf16* __restrict__ x, uns
         raw_barrier();
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (G == 0) {
-          // piece I = S-1 at half-steps 1..PPW: the first write into wnext follows
-          // barrier #36c+3, after group 1's lgkmcnt(0) on its last reads of that
-          // buffer (chunk c-1, half-step 17, completed before its barrier #36c+2)
           if constexpr (S >= 1 && S <= PPW) {
+            // piece I = S-1 at half-steps 1..PPW: the first write into wnext follows
+            // barrier #36c+3, after group 1's lgkmcnt(0) on its last reads of that
+            // buffer (chunk c-1, half-step 17, completed before its barrier #36c+2)
             constexpr int I = S >= 1 && S <= PPW ? S - 1 : 0;
             if (LS >= 0 && cc + 1 == NC) {
               const int j = wg * PPW + I, row = j * 4 + (lane >> 4);
@@ -2361,14 +1933,8 @@ static int launch_winpp_t(const ConvGeom& g, int cin, int nout, const void* x, c
   sh.dbg = 0;
   sh.nsplit = 1;
   KMat<bf16> lb{(const bf16*)w, sh.K, nout, sh.K};
-  // desync: half a tile's time (~14k cycles per 64-channel chunk for the row epilogues,
-  // ~10k for the forward) when every CU runs >= 8 tiles (the delayed CUs' idle start
-  // is then <= 1/16 of their work)
-  const int tiles = sh.tiles_m * sh.tiles_n, cus = device_cus();
-  int desync = 0;
-  if (VLP_WIN_DESYNC && tiles >= 8 * cus) desync = (RowTrait<EP>::value ? 14000 : 10000) * (cin / 64) / 2;
-  hipLaunchKernelGGL((conv3x3_winpp_kernel<TW, BN, FLIP, EP>), dim3(tiles), dim3(512), lds, st, sh,
-                     g.H, cin, (const bf16*)x, (unsigned)((size_t)g.N * g.H * g.W * cin * 2), lb, ep, cus, desync);
+  hipLaunchKernelGGL((conv3x3_winpp_kernel<TW, BN, FLIP, EP>), dim3(sh.tiles_m * sh.tiles_n), dim3(512), lds, st,
+                     sh, g.H, cin, (const bf16*)x, (unsigned)((size_t)g.N * g.H * g.W * cin * 2), lb, ep);
   return (int)hipGetLastError();
 }
 
@@ -2380,102 +1946,22 @@ static int launch_winpp_t(const ConvGeom& g, int cin, int nout, const void* x, c
 #ifndef VLP_WIN_WIDTHS
 #define VLP_WIN_WIDTHS ((1 << 1) | (1 << 4))
 #endif
-// BN-apply + ReLU of the input in the window (vlp_conv_fwd_act for layers 2-4):
-// off -- r5 A/B: the in-window transform costs more than the separate pass
-#ifndef VLP_WIN_ACT
-#define VLP_WIN_ACT 0
-#endif
-static bool win_ok(const ConvGeom& g, int cin, int nout) {
+static bool win_ok(const ConvGeom& g, int cin, int nout, int widths = VLP_WIN_WIDTHS) {
   return g.KH == 3 && g.KW == 3 && g.S == 1 && g.P == 1 && (g.W == 16 || g.W == 32 || g.W == 64) &&
-         ((VLP_WIN_WIDTHS >> (g.W / 16)) & 1) &&
+         ((widths >> (g.W / 16)) & 1) &&
          g.H % (256 / g.W) == 0 && cin % 128 == 0 && nout % 128 == 0 &&
          // 32-bit offsets into the input AND the [M][nout] epilogue operands / outputs
          (size_t)g.N * g.H * g.W * (cin > nout ? cin : nout) * 2 < (1ull << 31);
 }
-template <int TW, bool FLIP, int XF, class EP, bool PS = false>
-static int launch_win_t(const ConvGeom& g, int cin, int nout, const void* x, const void* w, const EP& ep,
-                        hipStream_t st, const WinXIn& xin) {
-  constexpr int BN = 128;
-  constexpr int NW = XF == 1 ? 8 : VLP_WIN_NW;
-  constexpr bool PERS = win_pers<EP, FLIP, XF, PS>();
-  if constexpr (!PS && win_pers<EP, FLIP, XF, true>() && VLP_WIN_PERSIST) {
-    // persistent form when every XCD gets the same whole number of tiles
-    const int nwg = (g.N * g.H * g.W / 256) * (nout / BN);
-    if (nwg % 8 == 0 && nwg >= 2 * device_cus()) return launch_win_t<TW, FLIP, XF, EP, true>(g, cin, nout, x, w, ep, st, xin);
-  }
-  constexpr int lds = win_lds_bytes<TW, BN, NW, win_minp<EP, PERS>()>();
-  static KernelDevState kst;
-  const int e = prepare_kernel(kst, (const void*)&conv3x3_win_kernel<TW, BN, NW, FLIP, XF, EP, PERS>, lds, 0, nullptr);
-  if (e) return e;
-  GemmShape sh;
-  sh.M = g.N * g.H * g.W;
-  sh.N = nout;
-  sh.K = 9 * cin;
-  sh.kchunk = sh.K;
-  sh.tiles_m = sh.M / 256;
-  sh.tiles_n = nout / BN;
-  sh.xsplit = 0;
-  sh.dbg = 0;
-  sh.nsplit = 1;
-  KMat<bf16> lb{(const bf16*)w, sh.K, nout, sh.K};
-#if VLP_WIN_STAMP
-  // diagnostic build: per-workgroup s_memtime stamps (start, main loop done,
-  // epilogue done), medians printed to stderr after each launch
-  static unsigned long long* dbuf = nullptr;
-  const int nb = sh.tiles_m * sh.tiles_n;
-  if (!dbuf) (void)hipMalloc(&dbuf, (size_t)65536 * 4 * 8);
-  WinXIn xs = xin;
-  if (XF == 0) xs.out = reinterpret_cast<bf16*>(dbuf);
-  hipLaunchKernelGGL((conv3x3_win_kernel<TW, BN, NW, FLIP, XF, EP, PERS>), dim3(nb), dim3(NW * 64), lds, st, sh,
-                     g.H, cin, (const bf16*)x, (unsigned)((size_t)g.N * g.H * g.W * cin * 2), lb, ep, xs);
-  if (XF == 0 && nb <= 65536) {
-    (void)hipStreamSynchronize(st);
-    std::vector<unsigned long long> h((size_t)nb * 4);
-    (void)hipMemcpy(h.data(), dbuf, h.size() * 8, hipMemcpyDeviceToHost);
-    std::vector<double> a(nb), b(nb);
-    unsigned long long t0 = ~0ull, t1 = 0;
-    for (int i = 0; i < nb; ++i) {
-      a[i] = (double)(h[i * 4 + 1] - h[i * 4]);
-      b[i] = (double)(h[i * 4 + 2] - h[i * 4 + 1]);
-      t0 = std::min(t0, h[i * 4]);
-      t1 = std::max(t1, h[i * 4 + 2]);
-    }
-    std::sort(a.begin(), a.end());
-    std::sort(b.begin(), b.end());
-    fprintf(stderr, "win TW=%d flip=%d wg=%d: main loop median %.0f cyc (p90 %.0f), epilogue median %.0f cyc (p90 %.0f), span %llu cyc\n",
-            TW, (int)FLIP, nb, a[nb / 2], a[nb * 9 / 10], b[nb / 2], b[nb * 9 / 10], t1 - t0);
-  }
-#else
-  int grid = sh.tiles_m * sh.tiles_n;
-  if constexpr (PERS) {
-    const int cus = device_cus() / 8 * 8;
-    if (grid > cus) grid = cus;
-  }
-  hipLaunchKernelGGL((conv3x3_win_kernel<TW, BN, NW, FLIP, XF, EP, PERS>), dim3(grid), dim3(NW * 64), lds, st, sh,
-                     g.H, cin, (const bf16*)x, (unsigned)((size_t)g.N * g.H * g.W * cin * 2), lb, ep, xin);
-#endif
-  return (int)hipGetLastError();
-}
 #ifndef VLP_WIN
 #define VLP_WIN 1   // the LDS-window kernel for the 3x3 stride-1 GEMMs of layers 2-4 (0: im2col GEMMs)
 #endif
-#ifndef VLP_WIN_PP
-#define VLP_WIN_PP 1   // the ping-pong form for the plain (XF = 0) window GEMMs
-#endif
-template <bool FLIP, int XF = 0, class EP>
+template <bool FLIP, class EP>
 static int launch_win(const ConvGeom& g, int cin, int nout, const void* x, const void* w, const EP& ep,
-                      hipStream_t st, const WinXIn& xin = WinXIn{}) {
-  // (the lock-step form, conv3x3_win_kernel, is instantiated only for the measured
-  // alternatives: VLP_WIN_PP=0, or the in-window transform with VLP_WIN_ACT=1)
-  if constexpr (XF == 0 && VLP_WIN_PP) {
-    if (g.W == 64) return launch_winpp_t<64, FLIP>(g, cin, nout, x, w, ep, st);
-    if (g.W == 32) return launch_winpp_t<32, FLIP>(g, cin, nout, x, w, ep, st);
-    return launch_winpp_t<16, FLIP>(g, cin, nout, x, w, ep, st);
-  } else {
-    if (g.W == 64) return launch_win_t<64, FLIP, XF>(g, cin, nout, x, w, ep, st, xin);
-    if (g.W == 32) return launch_win_t<32, FLIP, XF>(g, cin, nout, x, w, ep, st, xin);
-    return launch_win_t<16, FLIP, XF>(g, cin, nout, x, w, ep, st, xin);
-  }
+                      hipStream_t st) {
+  if (g.W == 64) return launch_winpp_t<64, FLIP>(g, cin, nout, x, w, ep, st);
+  if (g.W == 32) return launch_winpp_t<32, FLIP>(g, cin, nout, x, w, ep, st);
+  return launch_winpp_t<16, FLIP>(g, cin, nout, x, w, ep, st);
 }
 
 #ifndef VLP_FWD_BN_PP
@@ -2844,7 +2330,7 @@ VLP_EXPORT int vlp_conv_fwd_act_ok(int dtype, int N, int H, int W, int C, int Co
                                   int P) {
   if (dtype != VLP_BF16 || N < 1) return 0;
   const ConvGeom g = make_geom(N, H, W, C, Co, KH, KW, S, P);
-  return rows_c64_ok(g) || (VLP_WIN && VLP_WIN_ACT && win_ok(g, C, Co)) ? 1 : 0;
+  return rows_c64_ok(g) ? 1 : 0;
 }
 
 VLP_EXPORT int vlp_conv_fwd_act(int dtype, const void* x, const void* wp, void* y, void* x_act, int N,
@@ -2858,12 +2344,6 @@ VLP_EXPORT int vlp_conv_fwd_act(int dtype, const void* x, const void* wp, void* 
   g.M = g.N * g.Ho * g.Wo;
   g.K = g.KH * g.KW * g.C;
   EpiConvFwd<bf16> ep{stat_sum, stat_sumsq, stat_rep, (bf16*)y, g.Co};
-#if VLP_WIN_ACT
-  if (!rows_c64_ok(g)) {   // layers 2-4: the window kernel transforms each window chunk once
-    WinXIn wx{in_scale, in_shift, (bf16*)x_act};
-    return launch_win<false, 1>(g, g.C, g.Co, x, wp, ep, (hipStream_t)stream, wx);
-  }
-#endif
   RowsXIn xin{};
   xin.t0 = in_scale;
   xin.t1 = in_shift;

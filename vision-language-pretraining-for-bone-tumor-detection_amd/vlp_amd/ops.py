@@ -65,11 +65,11 @@ def conv_fwd_act_ok(x, Co, KH, KW, S, P):
 
 def conv_fwd_act(x, wp, Co, KH, KW, S, P, in_scale, in_shift, x_act, stat_sum, stat_sumsq, stat_rep=1, out=None):
     """conv(relu(in_scale*x + in_shift)) with that activation also written to x_act
-    (vlp_conv_fwd_act: BN-apply + ReLU fused into the layer-1 rows kernel)."""
+    (vlp_conv_fwd_act: BN-apply + ReLU fused into the layer-1 rows kernel's ring)."""
     N, H, W, C = x.shape
     Ho, Wo = conv_out_hw(H, W, KH, KW, S, P)
     y = out if out is not None else torch.empty((N, Ho, Wo, Co), dtype=x.dtype, device=x.device)
-    tk = ktimer.begin("conv_fwd[act]/narrow", 2.0 * N * Ho * Wo * Co * C * KH * KW)
+    tk = ktimer.begin("conv_fwd[act]/" + ("narrow" if C == 64 else "wide"), 2.0 * N * Ho * Wo * Co * C * KH * KW)
     lib().vlp_conv_fwd_act(dcode(x), ptr(x), ptr(wp), ptr(y), ptr(x_act), N, H, W, C, Co, KH, KW, S, P,
                            ptr(in_scale), ptr(in_shift), ptr(stat_sum), ptr(stat_sumsq), int(stat_rep), _s())
     ktimer.end(tk)
