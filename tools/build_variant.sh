@@ -19,7 +19,7 @@ for f in $ALL; do
   [ $f = nest_ops ] && EXTRA="-mllvm -amdgpu-mfma-vgpr-form=1"
   [ $f = prep_ops ] && EXTRA="-ffp-contract=off"
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -fvisibility=hidden \
-    -Wno-unused-result $EXTRA $FLAGS -c $CSRC/$f.hip -o $OUT/obj/$f.o &
+    -Wno-unused-result -Wno-c++20-extensions $EXTRA $FLAGS -c $CSRC/$f.hip -o $OUT/obj/$f.o &
   PIDS="$PIDS $!"
 done
 for p in $PIDS; do wait $p || { echo "variant $NAME: compile failed"; exit 1; }; done

@@ -127,20 +127,15 @@ int main() {
   run("copy grid=2048", 2.0, [&] { hipLaunchKernelGGL((copy_kernel<false>), dim3(2048), dim3(256), 0, 0, n, y, o); });
   run("copy grid=16384", 2.0, [&] { hipLaunchKernelGGL((copy_kernel<false>), dim3(16384), dim3(256), 0, 0, n, y, o); });
   GS(1, false, true, 4096);    // the product's default shape (bn_add_relu_kernel<bf16, true, 1, NT>)
-  GS(1, false, false, 4096);
-  GS(2, false, true, 4096);
-  GS(4, false, true, 2048);
   GS(1, true, true, 4096);
-  GS(2, true, true, 4096);
-  GS(1, false, true, 2048);
-  GS(1, false, true, 8192);
-  GS(1, false, true, 16384);
-  BK(2, false, true, 2048);
   BK(4, false, true, 2048);
-  BK(4, false, true, 1024);
-  BK(8, false, true, 1024);
+  BK(2, true, true, 2048);
+  BK(4, true, true, 1024);
   BK(4, true, true, 2048);
-  BK(2, false, false, 2048);
-  BK(4, false, true, 4096);
+  BK(4, true, true, 4096);
+  BK(8, true, true, 1024);
+  BK(8, true, true, 2048);
+  BK(16, true, true, 1024);
+  BK(4, true, false, 2048);
   return 0;
 }

@@ -243,6 +243,71 @@ bn_add_relu_kernel(unsigned nchunks, int cpr, const T* __restrict__ y, const flo
   }
 }
 
+// ---- blocked streaming layout (r6) ----
+// A workgroup owns contiguous segments of 256 * U 16-B chunks (thread t: chunks
+// seg + t + 256 k, k < U), segments grid-strided, every load of a segment issued
+// before its first store, non-temporal stores (and loads, NTL).  At the bs = 256 layer-1
+// size (537 MB per tensor) a 2-read / 1-write pass runs 5.9 TB/s this way against
+// 4.4 TB/s for the thread-strided single-chunk loop (tools/probes/ew_probe.hip,
+// profiles/r6_ew_probe.txt): each workgroup's requests sweep whole DRAM pages.
+// 256 % cpr == 0 keeps every chunk a thread touches in its own channel group.
+__device__ __forceinline__ uint4 ntl16(const void* p) {
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  const v4u w = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+  return make_uint4(w.x, w.y, w.z, w.w);
+}
+constexpr int kBlkU = 4;   // chunks per thread per segment
+static inline int blk_grid(size_t nchunks) {
+  size_t b = (nchunks + 256 * kBlkU - 1) / (256 * kBlkU);
+  return (int)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
+}
+template <bool HAS_IDT, bool NTL>
+__global__ void __launch_bounds__(256)
+bn_add_relu_blk_kernel(unsigned nchunks, int cpr, const bf16* __restrict__ y, const float* __restrict__ sc,
+                       const float* __restrict__ sh, const bf16* __restrict__ idt,
+                       const float* __restrict__ scd, const float* __restrict__ shd, bf16* __restrict__ out,
+                       uint8_t* __restrict__ rmask) {
+  constexpr int U = kBlkU;
+  const int c0 = (int)(threadIdx.x % (unsigned)cpr) * 8;
+  float a[8], b[8], c[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {   // as bn_add_relu_kernel
+    a[j] = sc[c0 + j]; b[j] = sh[c0 + j];
+    c[j] = scd ? scd[c0 + j] : 1.f;
+    b[j] += scd ? shd[c0 + j] : 0.f;
+  }
+  for (unsigned s0 = blockIdx.x * (256u * U); s0 < nchunks; s0 += gridDim.x * (256u * U)) {
+    const unsigned i0 = s0 + threadIdx.x;
+    uint4 yv[U], iv[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const unsigned i = i0 + 256u * k;
+      if (i < nchunks) {
+        yv[k] = NTL ? ntl16(y + (size_t)i * 8) : ldg16(y + (size_t)i * 8);
+        if constexpr (HAS_IDT) iv[k] = NTL ? ntl16(idt + (size_t)i * 8) : ldg16(idt + (size_t)i * 8);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const unsigned i = i0 + 256u * k;
+      if (i >= nchunks) continue;
+      float u[8], v[8];
+      Chunk<bf16>::unpack(yv[k], u);
+      if constexpr (HAS_IDT) {
+        Chunk<bf16>::unpack(iv[k], v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) u[j] = fmaxf(fmaf(u[j], a[j], fmaf(v[j], c[j], b[j])), 0.f);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) u[j] = fmaxf(fmaf(u[j], a[j], b[j]), 0.f);
+      }
+      const uint4 pk = Chunk<bf16>::pack(u);
+      ew_st16<1, true>(out + (size_t)i * 8, pk);
+      if (rmask) rmask[i] = relu_bits8(pk);
+    }
+  }
+}
+
 // ---- backward reduction: g = dout * (out > 0); sums of g, g*xhat_a, g*xhat_b ----
 // dout may instead be a broadcast [N][C] gradient divided by HW (global avg pool).
 template <typename T>
@@ -393,6 +458,54 @@ bn_bwd_apply_kernel(unsigned nchunks, int cpr, double count, const T* __restrict
 #pragma unroll
       for (int j = 0; j < E; ++j) d[j] = bn_bwd_dy(kb[j], bb[j], cb[j], g[j], y[j]);
       stg16((T*)B.dy + (size_t)i * E, Chunk<T>::pack(d));
+    }
+  }
+}
+
+// blocked form of the plain bn_bwd_apply (no broadcast gradient, no mask, no
+// g_out): dy_a = k_a g + b_a y_a + c_a [, dy_b likewise]; same arithmetic
+template <bool HAS_B, bool NTL>
+__global__ void __launch_bounds__(256)
+bn_bwd_apply_blk_kernel(unsigned nchunks, int cpr, double count, const bf16* __restrict__ dout, BnBwdSide A,
+                        BnBwdSide B) {
+  constexpr int U = kBlkU;
+  const int c0 = (int)(threadIdx.x % (unsigned)cpr) * 8;
+  const float inv_count = (float)(1.0 / count);
+  float ka[8], ba[8], ca[8], kb[8], bb[8], cb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = c0 + j;
+    bn_bwd_coef(A.gamma[c], A.istd[c], A.mean[c], A.sum_g[c], A.sum_gx[c], inv_count, ka[j], ba[j], ca[j]);
+    if (HAS_B) bn_bwd_coef(B.gamma[c], B.istd[c], B.mean[c], B.sum_g[c], B.sum_gx[c], inv_count, kb[j], bb[j], cb[j]);
+  }
+  for (unsigned s0 = blockIdx.x * (256u * U); s0 < nchunks; s0 += gridDim.x * (256u * U)) {
+    const unsigned i0 = s0 + threadIdx.x;
+    uint4 gv[U], yv[U], zv[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const unsigned i = i0 + 256u * k;
+      if (i < nchunks) {
+        gv[k] = NTL ? ntl16(dout + (size_t)i * 8) : ldg16(dout + (size_t)i * 8);
+        yv[k] = NTL ? ntl16((const bf16*)A.y + (size_t)i * 8) : ldg16((const bf16*)A.y + (size_t)i * 8);
+        if constexpr (HAS_B) zv[k] = NTL ? ntl16((const bf16*)B.y + (size_t)i * 8) : ldg16((const bf16*)B.y + (size_t)i * 8);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const unsigned i = i0 + 256u * k;
+      if (i >= nchunks) continue;
+      float g[8], y[8], d[8];
+      Chunk<bf16>::unpack(gv[k], g);
+      Chunk<bf16>::unpack(yv[k], y);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = bn_bwd_dy(ka[j], ba[j], ca[j], g[j], y[j]);
+      ew_st16<1, true>((bf16*)A.dy + (size_t)i * 8, Chunk<bf16>::pack(d));
+      if constexpr (HAS_B) {
+        Chunk<bf16>::unpack(zv[k], y);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = bn_bwd_dy(kb[j], bb[j], cb[j], g[j], y[j]);
+        ew_st16<1, true>((bf16*)B.dy + (size_t)i * 8, Chunk<bf16>::pack(d));
+      }
     }
   }
 }
@@ -849,6 +962,30 @@ static inline int ew_grid(size_t nchunks) { return ew_blocks(nchunks, 256, 4096)
 // (tools/ew_bench.py, bs = 256): unrolling loses at every size; non-temporal
 // stores take bn_add_relu from 4.8-4.9 to 5.2-6.3 TB/s at layers 1-2 and do
 // not help bn_bwd_apply, so the defaults are 4 and 0.
+// r6: the blocked streaming layout (bn_add_relu_blk_kernel, bn_bwd_apply_blk_kernel)
+// for the bf16 passes, chosen per pass and per-tensor size from tools/ew_bench.py
+// at the bs = 256 ResNet34 sizes (three libraries interleaved x2 on one box,
+// profiles/r6_ew_blocked_ab.txt; us per launch, old / blocked / blocked + NT loads):
+//   bn_add_relu, no residual: 128^2x64 208 / 206 / 198, 64^2x128 85 / 89 / 104,
+//                             32^2x256 47 / 49 / 57, 16^2x512 37 / 29 / 34
+//   bn_add_relu + residual + mask bits: 362 / 287 / 278, 159 / 152 / 147, 70 / 75 / 82, 40 / 42 / 48
+//   bn_bwd_apply: 318 / 292 / 273, 153 / 145 / 138, 78 / 60 / 72, 33 / 32 / 39
+// Non-temporal loads pay only for tensors past the 256 MB MALL (at smaller sizes
+// the producer's output may still be there).  0: the thread-strided kernels below,
+// 1: blocked, 2: blocked + non-temporal loads.  VLP_EW_BLK=0 forces 0.
+#ifndef VLP_EW_BLK
+#define VLP_EW_BLK 1
+#endif
+static inline int ew_form_add_relu(size_t tensor_bytes, bool residual) {
+  if (!VLP_EW_BLK) return 0;
+  const size_t MB = 1u << 20;
+  if (residual) return tensor_bytes >= 256 * MB ? 2 : 0;
+  return tensor_bytes >= 512 * MB ? 2 : (tensor_bytes <= 100 * MB ? 1 : 0);
+}
+static inline int ew_form_bwd_apply(size_t tensor_bytes) {
+  if (!VLP_EW_BLK) return 0;
+  return tensor_bytes >= (256u << 20) ? 2 : 1;
+}
 static inline int ew_variant() {
   return 4;
 }
@@ -914,7 +1051,18 @@ VLP_EXPORT int vlp_bn_add_relu(int dtype, long long M, int C, const void* y, con
   int cpr = C / epc;
   if (256 % cpr) return (int)hipErrorInvalidValue;
   dim3 g(ew_grid(n));
-  if (dtype == VLP_BF16) {
+  const int form = dtype == VLP_BF16 ? ew_form_add_relu((size_t)n * 16, idt != nullptr) : 0;
+  if (form > 0) {
+#define VLP_ADD_RELU_BLK(NTL)                                                                                     \
+    if (idt)                                                                                                      \
+      hipLaunchKernelGGL((bn_add_relu_blk_kernel<true, NTL>), dim3(blk_grid(n)), dim3(256), 0, st, n, cpr,        \
+                         (const bf16*)y, sc, sh, (const bf16*)idt, scd, shd, (bf16*)out, relu_mask);               \
+    else                                                                                                          \
+      hipLaunchKernelGGL((bn_add_relu_blk_kernel<false, NTL>), dim3(blk_grid(n)), dim3(256), 0, st, n, cpr,       \
+                         (const bf16*)y, sc, sh, (const bf16*)idt, scd, shd, (bf16*)out, relu_mask);
+    if (form == 2) { VLP_ADD_RELU_BLK(true) } else { VLP_ADD_RELU_BLK(false) }
+#undef VLP_ADD_RELU_BLK
+  } else if (dtype == VLP_BF16) {
     switch (ew_variant()) {
 #define VLP_ADD_RELU(U, NT)                                                                                    \
   if (idt)                                                                                                     \
@@ -980,7 +1128,18 @@ VLP_EXPORT int vlp_bn_bwd_apply(int dtype, long long M, int C, const void* dout,
   unsigned n = (unsigned)((size_t)M * C / epc);
   dim3 g(ew_grid(n));
   bool hb = dy_b != nullptr;
-  if (dtype == VLP_BF16) {
+  const int form = dtype == VLP_BF16 && !dbc && !mask && !g_out ? ew_form_bwd_apply((size_t)n * 16) : 0;
+  if (form > 0) {
+#define VLP_BWD_APPLY_BLK(NTL)                                                                                     \
+    if (hb)                                                                                                        \
+      hipLaunchKernelGGL((bn_bwd_apply_blk_kernel<true, NTL>), dim3(blk_grid(n)), dim3(256), 0, st, n, cpr,        \
+                         (double)M, (const bf16*)dout, A, B);                                                      \
+    else                                                                                                           \
+      hipLaunchKernelGGL((bn_bwd_apply_blk_kernel<false, NTL>), dim3(blk_grid(n)), dim3(256), 0, st, n, cpr,       \
+                         (double)M, (const bf16*)dout, A, B);
+    if (form == 2) { VLP_BWD_APPLY_BLK(true) } else { VLP_BWD_APPLY_BLK(false) }
+#undef VLP_BWD_APPLY_BLK
+  } else if (dtype == VLP_BF16) {
     if (hb)
       hipLaunchKernelGGL((bn_bwd_apply_kernel<bf16, true>), g, dim3(256), 0, st, n, cpr, (double)M,
                          (const bf16*)dout, dbc, HW, (const bf16*)mask, A, B, (bf16*)g_out);
