@@ -108,6 +108,10 @@ def _project_backward(head, wT, feat, ld, dim, proj_name, E, emb, norm, g_emb, g
 
 _TEXT_STREAMS = {}
 _USE_TEXT_STREAM = os.environ.get("VLP_TEXT_STREAM", "1") != "0"
+# (r6, measured and not adopted, profiles/r6_text_stream_ab.txt: the text forward
+# on the main stream ahead of the image tower, and a high-priority text stream;
+# the rocprofv3 timeline shows the main stream waiting ≈1 ms at the join before
+# the head, but both alternatives cost more than that wait)
 
 
 def _text_stream(dev):
