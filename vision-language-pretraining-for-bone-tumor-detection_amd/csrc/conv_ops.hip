@@ -2143,6 +2143,39 @@ __global__ void wgrad_fold_kernel(int Co, int C, int T, int ks, size_t slab, con
   g[((size_t)co * C + c) * T + t] = (a0 + a1) + (a2 + a3);
 }
 
+// r6: one workgroup per output channel row (T * C floats): every split slab read
+// as 16-B vectors (the per-element kernel above issued 4-B loads), the same
+// per-element summation order (s mod 4 partials, (a0 + a1) + (a2 + a3)), and the
+// [t][c] -> [c][t] transpose staged in LDS so the gradient row is written
+// contiguously.  Rows up to kFoldRowMax floats (layer 4: 9 * 512).
+constexpr int kFoldRowMax = 9 * 512;
+__global__ void __launch_bounds__(256) wgrad_fold_row_kernel(int C, int T, int ks, size_t slab,
+                                                              const float* __restrict__ ws, float* __restrict__ g) {
+  __shared__ float row[kFoldRowMax];
+  const int L = C * T;
+  const size_t base = (size_t)blockIdx.x * L;
+  for (int e = threadIdx.x * 4; e < L; e += 1024) {
+    const float* p = ws + base + e;
+    v4f a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
+    int s = 0;
+    for (; s + 4 <= ks; s += 4) {
+      a0 += *reinterpret_cast<const v4f*>(p + (size_t)s * slab);
+      a1 += *reinterpret_cast<const v4f*>(p + (size_t)(s + 1) * slab);
+      a2 += *reinterpret_cast<const v4f*>(p + (size_t)(s + 2) * slab);
+      a3 += *reinterpret_cast<const v4f*>(p + (size_t)(s + 3) * slab);
+    }
+    for (; s < ks; ++s) a0 += *reinterpret_cast<const v4f*>(p + (size_t)s * slab);
+    const v4f v = (a0 + a1) + (a2 + a3);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) row[e + j] = v[j];   // slab order: e = t * C + c
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < L; o += 256) {       // gradient order: o = c * T + t
+    const int c = o / T, t = o - c * T;
+    g[base + o] = row[t * C + c];
+  }
+}
+
 #ifndef VLP_WGRAD_SLOT_DIV
 #define VLP_WGRAD_SLOT_DIV 1   // weight-gradient split count sized for 1/DIV of the chip's slots
 #endif
@@ -2512,6 +2545,11 @@ VLP_EXPORT int vlp_conv_wgrad_fold(int Co, int C, int KH, int KW, int nsplit, co
                                    void* stream) {
   if (nsplit < 1) return (int)hipErrorInvalidValue;
   const size_t n = (size_t)Co * KH * KW * C;
+  if (C % 4 == 0 && KH * KW * C <= kFoldRowMax && ((uintptr_t)split_ws & 15) == 0) {
+    hipLaunchKernelGGL(wgrad_fold_row_kernel, dim3((unsigned)Co), dim3(256), 0, (hipStream_t)stream, C, KH * KW,
+                       nsplit, n, split_ws, grad);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(wgrad_fold_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, Co,
                      C, KH * KW, nsplit, n, split_ws, grad);
   return (int)hipGetLastError();
