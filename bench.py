@@ -423,10 +423,14 @@ def dp_rehearsal(args, prefetched_steps, timed, dev):
                     "from the weight-gradient stream (the N > 1 schedule on one GPU)"}
 
 
-def _traffic(family):
+def _traffic(family, dtype="bf16", image_model="resnet34"):
     """HBM bytes per launch of the roofline kernel from the committed PMC passes
     (profiles/roofline_traffic.json, written by tools/pmc_traffic.py from
-    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this same command)."""
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this same command).  The
+    table holds the default bf16 runs (ResNet34 and NesT families); any other
+    dtype reports null rather than another kernel's bytes."""
+    if dtype != "bf16":
+        return None
     path = os.path.join(ROOT, "profiles", "roofline_traffic.json")
     try:
         with open(path) as f:
@@ -606,7 +610,7 @@ def main():
                          "flop_per_launch": round(flop_k / max(nl, 1)), "peak_measured": peak_meas,
                          "frac_of_measured": round(achieved / peak_meas, 4) if peak_meas else None,
                          "traffic_unit": "HBM bytes/launch",
-                         "traffic": _traffic(tk),
+                         "traffic": _traffic(tk, args.dtype, args.image_model),
                          "timed_in": f"isolated pass of {args.roofline_steps} steps, serial schedule "
                                      "(bracketed by vlp_trace_marker dispatches)"},
             "loss": round(loss.item(), 5),
@@ -623,6 +627,8 @@ def main():
             res["roofline"]["achieved_under_default_schedule"] = round((shared[2] / (shared[0] / 1e3)) / 1e12, 2)
         if rehearsal is not None:
             rehearsal["vs_value"] = round(rehearsal["value"] / value, 4)
+            # against the two plain runs bracketing it in time (the box drifts between runs)
+            rehearsal["vs_plain_mean"] = round(rehearsal["value"] / ((value + rehearsal["value_plain_rerun"]) / 2), 4)
             res["dp_schedule_1gpu"] = rehearsal
         if ldelta is not None:
             res["loss_delta_vs_fp32"] = ldelta
