@@ -135,7 +135,7 @@ def test_conv_fwd_act_matches_pass_then_conv(ops, N, H, W, C):
     kernel's ring, W = 128) against the separate bn_add_relu pass + conv_fwd: a1 and
     y bit-identical, BN sums equal up to fp64 atomic order; N = 300 > CUs puts two
     images on some workgroups.  Layers 2-4 are refused (the r6 in-window transform
-    measured slower than the pass and was removed, DESIGN §10)."""
+    measured slower than the pass and was removed, DESIGN §11)."""
     torch.manual_seed(11)
     dev = torch.device("cuda")
     y1 = torch.randn(N, H, W, C, device=dev).to(torch.bfloat16)
