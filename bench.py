@@ -478,12 +478,18 @@ def main():
     # The roofline kernel is timed in a separate pass with the serial schedule,
     # where its launches do not share the CUs with the data-gradient chain.
     from vlp_amd import resnet34 as _r34
+    from vlp_amd import clip_model as _cm
     from vlp_amd._lib import lib as _vlib
     resnet = args.image_model == "resnet34"
+    text_stream0 = _cm._USE_TEXT_STREAM
 
     def set_wgrad_stream(on):
+        # off = the fully serial schedule of the kernel report and the roofline pass:
+        # the weight gradients AND the text tower on the main stream, so no family's
+        # HIP-event time includes sharing the CUs with another stream
         if resnet:
             _r34._USE_WG_STREAM = bool(on) and args.wgrad_stream
+        _cm._USE_TEXT_STREAM = text_stream0 if on else False
     set_wgrad_stream(True)
 
     for _ in range(args.warmup):
@@ -621,8 +627,8 @@ def main():
         res["serial_schedule"] = {"value": round(ps / el_serial, 2),
                                   "ms_per_step": round(el_serial / args.roofline_steps * 1e3, 3),
                                   "steps": args.roofline_steps,
-                                  "note": "the roofline pass: same prefetched steps with the weight gradients on the "
-                                          "main stream (no CU sharing); `value` uses the side-stream schedule"}
+                                  "note": "the roofline pass: same prefetched steps with the weight gradients and the "
+                                          "text tower on the main stream (no CU sharing); `value` uses the side streams"}
         if shared is not None and shared[0] > 0:
             res["roofline"]["achieved_under_default_schedule"] = round((shared[2] / (shared[0] / 1e3)) / 1e12, 2)
         if rehearsal is not None:

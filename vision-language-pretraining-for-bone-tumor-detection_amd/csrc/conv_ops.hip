@@ -2149,6 +2149,9 @@ __global__ void wgrad_fold_kernel(int Co, int C, int T, int ks, size_t slab, con
 // [t][c] -> [c][t] transpose staged in LDS so the gradient row is written
 // contiguously.  Rows up to kFoldRowMax floats (layer 4: 9 * 512).
 constexpr int kFoldRowMax = 9 * 512;
+#ifndef VLP_FOLD_ROW
+#define VLP_FOLD_ROW 1   // 0: the per-element fold (wgrad_fold_kernel) for every conv
+#endif
 __global__ void __launch_bounds__(256) wgrad_fold_row_kernel(int C, int T, int ks, size_t slab,
                                                               const float* __restrict__ ws, float* __restrict__ g) {
   __shared__ float row[kFoldRowMax];
@@ -2158,6 +2161,20 @@ __global__ void __launch_bounds__(256) wgrad_fold_row_kernel(int C, int T, int k
     const float* p = ws + base + e;
     v4f a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, a2 = a0, a3 = a0;
     int s = 0;
+    // 16 slabs' loads in flight per thread (the layer-1 folds reduce ~85 slabs with
+    // 64 workgroups: latency-bound), added in the same per-element order
+    for (; s + 16 <= ks; s += 16) {
+      v4f t[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) t[j] = *reinterpret_cast<const v4f*>(p + (size_t)(s + j) * slab);
+#pragma unroll
+      for (int j = 0; j < 16; j += 4) {
+        a0 += t[j];
+        a1 += t[j + 1];
+        a2 += t[j + 2];
+        a3 += t[j + 3];
+      }
+    }
     for (; s + 4 <= ks; s += 4) {
       a0 += *reinterpret_cast<const v4f*>(p + (size_t)s * slab);
       a1 += *reinterpret_cast<const v4f*>(p + (size_t)(s + 1) * slab);
@@ -2545,7 +2562,7 @@ VLP_EXPORT int vlp_conv_wgrad_fold(int Co, int C, int KH, int KW, int nsplit, co
                                    void* stream) {
   if (nsplit < 1) return (int)hipErrorInvalidValue;
   const size_t n = (size_t)Co * KH * KW * C;
-  if (C % 4 == 0 && KH * KW * C <= kFoldRowMax && ((uintptr_t)split_ws & 15) == 0) {
+  if (VLP_FOLD_ROW && C % 4 == 0 && KH * KW * C <= kFoldRowMax && ((uintptr_t)split_ws & 15) == 0) {
     hipLaunchKernelGGL(wgrad_fold_row_kernel, dim3((unsigned)Co), dim3(256), 0, (hipStream_t)stream, C, KH * KW,
                        nsplit, n, split_ws, grad);
     return (int)hipGetLastError();
