@@ -439,6 +439,44 @@ def test_conv_wgrad_split_slabs(ops, case, ws_floats):
     assert rel(g.cpu(), w.grad) < 2e-3
 
 
+@pytest.mark.parametrize("N,H,slabs", [(3, 5, None), (2, 1, None), (5, 9, 2), (4, 32, None), (1, 128, None)])
+def test_conv_wgrad_rows_layer1(ops, N, H, slabs):
+    """Layer-1 weight gradient (3x3, 64 -> 64, W = 128) on the row-streaming
+    kernel: one fp32 slab per workgroup (a workgroup loops over several images
+    when the workspace holds fewer slabs than images), folded into the parameter
+    layout.  Against torch's fp32 weight gradient of the same bf16 operands, and
+    bit-identical from run to run (fixed slab order)."""
+    import ctypes
+    from vlp_amd._lib import lib
+    W, C = 128, 64
+    dt = torch.bfloat16
+    torch.manual_seed(11)
+    x = torch.randn(N, C, H, W).to(dt).float().requires_grad_()
+    w = (torch.randn(C, C, 3, 3) * (9 * C) ** -0.5).requires_grad_()
+    y = F.conv2d(x, w, padding=1)
+    dy = torch.randn_like(y).to(dt).float()
+    y.backward(dy)
+    slab = C * C * 9
+    nws = (slabs or 64) * slab
+    ws = torch.full((nws + 64,), float("nan"), device="cuda")
+    dyd, xd = nhwc(dy).to(dt).cuda(), nhwc(x.detach()).to(dt).cuda()
+    st = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for _ in range(2):
+        g = torch.full((C, C, 3, 3), float("nan"), device="cuda")
+        ns = ctypes.c_int(0)
+        assert lib().vlp_conv_wgrad_ws(1, dyd.data_ptr(), xd.data_ptr(), ws.data_ptr(), nws, ctypes.addressof(ns),
+                                       N, H, W, C, C, 3, 3, 1, 1, st) == 0
+        assert ns.value == min(N, slabs or N), ns.value   # one slab per workgroup
+        lib().vlp_conv_wgrad_fold(C, C, 3, 3, ns.value, ws.data_ptr(), g.data_ptr(), st)
+        outs.append(g)
+    torch.cuda.synchronize()
+    assert torch.isnan(ws[nws:]).all().item(), "slab writes past the workspace"
+    assert torch.equal(outs[0], outs[1])
+    err = (outs[0].cpu() - w.grad).abs().max().item() / w.grad.abs().max().item()
+    assert err < 1e-5, err   # fp32 sums of exact bf16 products: only the summation order differs
+
+
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("N,H,W,C", [(2, 10, 10, 64), (2, 4, 128, 64), (4, 7, 7, 512), (2, 14, 14, 256),
                                      (2, 8, 64, 128), (2, 16, 16, 512)])

@@ -1685,6 +1685,192 @@ static int launch_rows_c64(const ConvGeom& g, const void* x, const void* w, int 
   return (int)hipGetLastError();
 }
 
+// ---------------- row-streaming 3x3 weight gradient, 64 -> 64 channels (layer1) ----------------
+//   dW[co][(kh,kw,ci)] = sum_(n,i,j) dy[n][i][j][co] * x[n][i+kh-1][j+kw-1][ci]
+// The im2col weight-gradient GEMM (64 x 192 tiles) pulled every input pixel
+// through the LDS-DMA path once per filter tap (9x the input and 3x dy per
+// launch) and ran at 40 % of HBM and 33 % of the MFMA rate.  Here a workgroup
+// owns whole images and streams them row by row: dy row i and input rows
+// i-1..i+1 sit in two LDS rings, pixel-major as they arrive, and both MFMA
+// operands are ds_read_b64_tr_b16 transposing reads -- the reduction index of
+// both is the pixel, so a tap's column shift is only the first ring position
+// a lane addresses.  Each byte of dy and x is fetched from HBM once.  The
+// workgroup's 64 x 576 fp32 partial stays in registers across its images and
+// is written once, as split slab blockIdx.x; vlp_conv_wgrad_fold sums the
+// slabs in a fixed order (deterministic).
+//   waves: 8; wave w owns output channels 32(w&1) .. +31 x columns 144(w>>1) .. +143
+//   (2 x 9 blocks of 16 x 16: 72 fp32 accumulators per lane)
+//   rings: input rows in 5 slots (rows i-1 .. i+3), dy rows in 3 (i .. i+2), so
+//   two rows of each are in flight while row i is reduced
+#ifndef VLP_WGRAD_ROWS
+#define VLP_WGRAD_ROWS 1   // 0: layer-1 weight gradients on the im2col GEMM (gemm_short)
+#endif
+constexpr int kRwXSlot = (kRcW + 2) * 128;   // 130 ring positions: zero halo at 0 and 129
+constexpr int kRwDSlot = kRcW * 128;
+constexpr int kRwXSlots = 5, kRwDSlots = 3;
+constexpr int kRwDOff = kRwXSlots * kRwXSlot;
+constexpr int kRwLds = kRwDOff + kRwDSlots * kRwDSlot;
+static_assert(kRwLds <= 160 * 1024, "weight-gradient rows kernel LDS map");
+static_assert(kRwXSlot % 256 == 0 && kRwDOff % 256 == 0, "ring slots start on bank 0");
+// 16-B chunk c of ring position `pos` is stored at chunk c ^ mn8_h(pos).  A
+// transposing read's 32-lane half touches positions r0 + {0..3} and r0 + {8..11}
+// (8 B each of one 32-B channel block); XOR-ing bits 1 and 3 of the position
+// into the chunk puts them on 64 distinct banks for every r0 mod 8 (a Python
+// bank model over the r0 the reads use: 0..2 and 4..6 mod 8, all conflict-free).
+
+// two transposing reads (k-rows +0..3 from `lo`, +4..7 from `hi`) at immediate OFF
+template <int OFF>
+__device__ __forceinline__ v8bf tr_pair(unsigned lo_addr, unsigned hi_addr) {
+  v4bf lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(lo_addr), "n"(OFF));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(hi_addr), "n"(OFF));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+conv3x3_c64_wgrad_rows_kernel(int N, int H, const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                              float* __restrict__ ws) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
+  const int ch = wv & 1, cq = wv >> 1;
+  const unsigned bytes = (unsigned)((size_t)N * H * kRcW * 128);
+  const rsrc_t rx = buf_rsrc(x, bytes), rd = buf_rsrc(dy, bytes);
+
+  // zero halo positions (never DMA targets): all 8 chunks of positions 0 and 129
+  for (int q = tid; q < kRwXSlots * 16; q += 512) {
+    const int sl = q >> 4, side = (q >> 3) & 1, c = q & 7;
+    *reinterpret_cast<uint4*>(smem + sl * kRwXSlot + (side ? (kRcW + 1) * 128 : 0) + c * 16) = zero4();
+  }
+  // DMA pieces: piece j = 2 wv + jj of a row fills LDS chunks j*64 + lane (pixel
+  // (j*64 + lane) >> 3, stored chunk lane & 7) from the logical chunk the swizzle
+  // puts there; input rows sit one position right of their pixel (the halo)
+  unsigned xo[2], dof[2];
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int u = (wv * 2 + jj) * 64 + lane, px = u >> 3, cs = u & 7;
+    dof[jj] = (unsigned)(px * 128 + ((cs ^ mn8_h(px)) << 4));
+    xo[jj] = (unsigned)(px * 128 + ((cs ^ mn8_h(px + 1)) << 4));
+  }
+  auto fetch_x = [&](int n, int r) __attribute__((always_inline)) {
+    char* sl = smem + ((r + 1) % kRwXSlots) * kRwXSlot + 128;
+    const unsigned base = (unsigned)r < (unsigned)H ? (unsigned)(((size_t)n * H + r) * (kRcW * 128)) : kOOB;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) dma16(rx, base + xo[jj], sl + (wv * 2 + jj) * 1024);
+  };
+  auto fetch_d = [&](int n, int r) __attribute__((always_inline)) {
+    char* sl = smem + kRwDOff + (r % kRwDSlots) * kRwDSlot;
+    const unsigned base = r < H ? (unsigned)(((size_t)n * H + r) * (kRcW * 128)) : kOOB;
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) dma16(rd, base + dof[jj], sl + (wv * 2 + jj) * 1024);
+  };
+
+  // lane read addresses (slot 0, k-step 0): lane 16g + 4q + p reads k-rows
+  // (pixels) 8g + q (+4 for the upper half) at channels 4p .. 4p+3 of its block
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const unsigned l0 = lds_addr(smem);
+  unsigned abase[2][2], bbase[9][2];
+  int bkh[9];   // input-row offset (kh) of column block jb: wave-uniform
+#pragma unroll
+  for (int hl = 0; hl < 2; ++hl) {
+    const int pos = 8 * g + q + 4 * hl;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int c = 2 * (2 * ch + a) + (p >> 1);
+      abase[a][hl] = l0 + kRwDOff + pos * 128 + ((c ^ mn8_h(pos)) << 4) + 8 * (p & 1);
+    }
+#pragma unroll
+    for (int jb = 0; jb < 9; ++jb) {
+      const int b = 9 * cq + jb, t = b >> 2, kw = t % 3, c = 2 * (b & 3) + (p >> 1);
+      bkh[jb] = t / 3;
+      const int ps = pos + kw;
+      bbase[jb][hl] = l0 + ps * 128 + ((c ^ mn8_h(ps)) << 4) + 8 * (p & 1);
+    }
+  }
+
+  v4f acc[2][9];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int jb = 0; jb < 9; ++jb) acc[a][jb] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  struct Frags { v8bf a[2]; v8bf b[9]; };
+  // k-step S (pixels 32S .. 32S+31) of the row whose dy slot is at byte dso and
+  // whose column blocks' input rows are at xso[jb]
+  auto issue = [&](auto S, unsigned dso, const unsigned (&xso)[9], Frags& f) __attribute__((always_inline)) {
+    constexpr int OFF = decltype(S)::value * 32 * 128;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) f.a[a] = tr_pair<OFF>(abase[a][0] + dso, abase[a][1] + dso);
+#pragma unroll
+    for (int jb = 0; jb < 9; ++jb) f.b[jb] = tr_pair<OFF>(bbase[jb][0] + xso[jb], bbase[jb][1] + xso[jb]);
+  };
+  // the asm reads are invisible to the compiler's LDS tracking: wait by hand and
+  // tie the wait to the fragment registers so no MFMA is scheduled above it
+  auto land = [&](Frags& f) __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int a = 0; a < 2; ++a) asm volatile("" : "+v"(f.a[a]));
+#pragma unroll
+    for (int jb = 0; jb < 9; ++jb) asm volatile("" : "+v"(f.b[jb]));
+  };
+
+  for (int n = blockIdx.x; n < N; n += gridDim.x) {
+    wait_vmcnt<0>();
+    __syncthreads();   // the previous image's ring reads are done (and the halo is zero)
+    fetch_x(n, -1); fetch_x(n, 0); fetch_x(n, 1); fetch_d(n, 0);
+    fetch_x(n, 2); fetch_d(n, 1);
+    for (int i = 0; i < H; ++i) {
+      wait_vmcnt<4>();   // input row i+1 and dy row i landed (input i+2 and dy i+1 in flight)
+      raw_barrier();     // ... for every wave; row i-1's reads are done everywhere
+      fetch_x(n, i + 3);   // into row i-2's slot
+      fetch_d(n, i + 2);   // into row i-1's slot
+      const unsigned dso = (unsigned)((i % kRwDSlots) * kRwDSlot);
+      unsigned xso[9];
+#pragma unroll
+      for (int jb = 0; jb < 9; ++jb) xso[jb] = (unsigned)(((i + bkh[jb]) % kRwXSlots) * kRwXSlot);
+      Frags f[2];
+      issue(std::integral_constant<int, 0>{}, dso, xso, f[0]);
+      static_for<0, 4>([&](auto S) {
+        constexpr int s = decltype(S)::value;
+        land(f[s & 1]);
+        if constexpr (s < 3) issue(std::integral_constant<int, s + 1>{}, dso, xso, f[(s + 1) & 1]);
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int jb = 0; jb < 9; ++jb)
+            acc[a][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[s & 1].b[jb], f[s & 1].a[a], acc[a][jb], 0, 0, 0);
+      });
+    }
+  }
+  // lane (g, i) holds columns 16 b + 4g .. +3 of output channel 16 (2ch + a) + i
+  float* out = ws + (size_t)blockIdx.x * (64 * 576);
+  const int i16 = lane & 15;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int jb = 0; jb < 9; ++jb)
+      *reinterpret_cast<v4f*>(out + (size_t)(16 * (2 * ch + a) + i16) * 576 + 16 * (9 * cq + jb) + 4 * g) = acc[a][jb];
+}
+
+static bool wgrad_rows_ok(const ConvGeom& g) {
+  return VLP_WGRAD_ROWS && g.C == 64 && g.Co == 64 && g.KH == 3 && g.KW == 3 && g.S == 1 && g.P == 1 &&
+         g.W == kRcW && g.H >= 1 && (size_t)g.N * g.H * kRcW * 128 < (1ull << 31);
+}
+// one slab per workgroup: grid <= the slabs the workspace holds
+static int launch_wgrad_rows(const ConvGeom& g, const void* dy, const void* x, float* ws, int max_ks, int* ks_out,
+                             hipStream_t st) {
+  const hipError_t ae = hipFuncSetAttribute((const void*)&conv3x3_c64_wgrad_rows_kernel,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, kRwLds);
+  if (ae != hipSuccess) return (int)ae;
+  int grid = device_cus();
+  if (grid > g.N) grid = g.N;
+  if (grid > max_ks) grid = max_ks;
+  hipLaunchKernelGGL(conv3x3_c64_wgrad_rows_kernel, dim3(grid), dim3(512), kRwLds, st, g.N, g.H,
+                     (const bf16*)dy, (const bf16*)x, ws);
+  *ks_out = grid;
+  return (int)hipGetLastError();
+}
+
 // ---------------- LDS-window implicit GEMM: 3x3, stride 1, 64-channel chunks ----------------
 // The im2col GEMMs fetch every input pixel once per filter tap: 9 copies of the
 // A operand per 64-channel chunk pass through the LDS-DMA path, whose intake
@@ -2208,6 +2394,8 @@ static int conv_wgrad_ws_t(const void* dy, const void* x, float* ws, long long w
   int ks = 1;
   bool split_store = false;
   if constexpr (std::is_same<T, bf16>::value) {
+    // layer 1: the row-streaming kernel, one slab per workgroup
+    if (wgrad_rows_ok(g)) return launch_wgrad_rows(g, dy, x, ws, max_ks, ks_out, st);
     // tile engines whose epilogue honours per-split output slabs
     if (gemm_variant() >= 5 && g.K % 4 == 0) {
       constexpr int mink5 = 2048;
