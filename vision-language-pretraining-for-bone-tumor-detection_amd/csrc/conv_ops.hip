@@ -1702,6 +1702,10 @@ static int launch_rows_c64(const ConvGeom& g, const void* x, const void* w, int 
 //   (2 x 9 blocks of 16 x 16: 72 fp32 accumulators per lane)
 //   rings: input rows in 5 slots (rows i-1 .. i+3), dy rows in 3 (i .. i+2), so
 //   two rows of each are in flight while row i is reduced
+// Measured at bs 256 (profiles/r6_wgrad_rows_ab.txt): 337 us per launch, 3.2 TB/s
+// and 0.92 PF; timing builds without the MFMAs ~215 us (5 TB/s) and without the
+// ring fetches ~200 us, at an effective clock of ~1.6 GHz (GRBM_GUI_ACTIVE / 8 /
+// wall): the two halves overlap only partly under the chip's power limit.
 #ifndef VLP_WGRAD_ROWS
 #define VLP_WGRAD_ROWS 1   // 0: layer-1 weight gradients on the im2col GEMM (gemm_short)
 #endif
@@ -1794,54 +1798,101 @@ conv3x3_c64_wgrad_rows_kernel(int N, int H, const bf16* __restrict__ dy, const b
 #pragma unroll
     for (int jb = 0; jb < 9; ++jb) acc[a][jb] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  struct Frags { v8bf a[2]; v8bf b[9]; };
-  // k-step S (pixels 32S .. 32S+31) of the row whose dy slot is at byte dso and
-  // whose column blocks' input rows are at xso[jb]
-  auto issue = [&](auto S, unsigned dso, const unsigned (&xso)[9], Frags& f) __attribute__((always_inline)) {
-    constexpr int OFF = decltype(S)::value * 32 * 128;
+  // Read units: k-step s = u / 3 (pixels 32s .. 32s+31) and column blocks
+  // 3 (u % 3) .. +2, plus the k-step's two dy fragments in its first unit.  Unit
+  // u+1's reads are issued in front of unit u's 6 MFMAs (about 100 cycles per
+  // wave, two waves per SIMD, cover their latency) with 40 fragment VGPRs live;
+  // whole k-steps double-buffered (88) spilled once the pipeline crossed rows.
+  v8bf fa[2][2], fb[2][3];
+  auto issue_unit = [&](auto U, unsigned dso, const unsigned (&xso)[9]) __attribute__((always_inline)) {
+    constexpr int u = decltype(U)::value, s = u / 3, gq = u % 3, OFF = s * 32 * 128;
+    if constexpr (gq == 0) {
 #pragma unroll
-    for (int a = 0; a < 2; ++a) f.a[a] = tr_pair<OFF>(abase[a][0] + dso, abase[a][1] + dso);
+      for (int a = 0; a < 2; ++a) fa[s & 1][a] = tr_pair<OFF>(abase[a][0] + dso, abase[a][1] + dso);
+    }
 #pragma unroll
-    for (int jb = 0; jb < 9; ++jb) f.b[jb] = tr_pair<OFF>(bbase[jb][0] + xso[jb], bbase[jb][1] + xso[jb]);
+    for (int jj = 0; jj < 3; ++jj) {
+      const int jb = 3 * gq + jj;
+      fb[u & 1][jj] = tr_pair<OFF>(bbase[jb][0] + xso[jb], bbase[jb][1] + xso[jb]);
+    }
   };
   // the asm reads are invisible to the compiler's LDS tracking: wait by hand and
   // tie the wait to the fragment registers so no MFMA is scheduled above it
-  auto land = [&](Frags& f) __attribute__((always_inline)) {
+  auto land_unit = [&](auto U) __attribute__((always_inline)) {
+    constexpr int u = decltype(U)::value, s = u / 3, gq = u % 3;
+    v8bf(&ta)[2] = fa[s & 1];
+    v8bf(&tb)[3] = fb[u & 1];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (gq == 0) {
 #pragma unroll
-    for (int a = 0; a < 2; ++a) asm volatile("" : "+v"(f.a[a]));
+      for (int a = 0; a < 2; ++a) asm volatile("" : "+v"(ta[a]));
+    }
 #pragma unroll
-    for (int jb = 0; jb < 9; ++jb) asm volatile("" : "+v"(f.b[jb]));
+    for (int jj = 0; jj < 3; ++jj) asm volatile("" : "+v"(tb[jj]));
+  };
+  auto mfma_unit = [&](auto U) __attribute__((always_inline)) {
+    constexpr int u = decltype(U)::value, s = u / 3, gq = u % 3;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int jj = 0; jj < 3; ++jj)
+        acc[a][3 * gq + jj] =
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[u & 1][jj], fa[s & 1][a], acc[a][3 * gq + jj], 0, 0, 0);
+  };
+  auto slots = [&](int i, unsigned& dso, unsigned (&xso)[9]) __attribute__((always_inline)) {
+    dso = (unsigned)((i % kRwDSlots) * kRwDSlot);
+#pragma unroll
+    for (int jb = 0; jb < 9; ++jb) xso[jb] = (unsigned)(((i + bkh[jb]) % kRwXSlots) * kRwXSlot);
   };
 
+  // Per row i: read units 0..10, then the row's one barrier, then unit 11.  The
+  // barrier sits in front of the LAST unit so that the next row's first reads
+  // (and the ring fetches of input row i+4 / dy row i+3) are issued before it and
+  // overlap its MFMAs: no wave idles on an LDS round trip at a row start.  Fetch
+  // group of row i (issued at its barrier): input row i+4 into the slot of row
+  // i-1 and dy row i+3 into the slot of dy row i -- every wave has LANDED all of
+  // row i's fragment reads before the barrier (lgkmcnt(0)), so both slots are
+  // free.  vmcnt (in-order retirement): at row i's barrier the groups of rows i-1
+  // (input i+3, dy i+2) and i-2 are outstanding; waiting down to 4 lands the
+  // older one, i.e. input row i+2 and dy row i+1, the last rows row i+1 needs.
   for (int n = blockIdx.x; n < N; n += gridDim.x) {
     wait_vmcnt<0>();
     __syncthreads();   // the previous image's ring reads are done (and the halo is zero)
     fetch_x(n, -1); fetch_x(n, 0); fetch_x(n, 1); fetch_d(n, 0);
     fetch_x(n, 2); fetch_d(n, 1);
+    wait_vmcnt<4>();     // input rows -1..1 and dy row 0 (input 2 and dy 1 in flight)
+    raw_barrier();
+    fetch_x(n, 3); fetch_d(n, 2);   // the "row -1" group
+    unsigned dso, xso[9];
+    slots(0, dso, xso);
+    issue_unit(std::integral_constant<int, 0>{}, dso, xso);
     for (int i = 0; i < H; ++i) {
-      wait_vmcnt<4>();   // input row i+1 and dy row i landed (input i+2 and dy i+1 in flight)
-      raw_barrier();     // ... for every wave; row i-1's reads are done everywhere
-      fetch_x(n, i + 3);   // into row i-2's slot
-      fetch_d(n, i + 2);   // into row i-1's slot
-      const unsigned dso = (unsigned)((i % kRwDSlots) * kRwDSlot);
-      unsigned xso[9];
-#pragma unroll
-      for (int jb = 0; jb < 9; ++jb) xso[jb] = (unsigned)(((i + bkh[jb]) % kRwXSlots) * kRwXSlot);
-      Frags f[2];
-      issue(std::integral_constant<int, 0>{}, dso, xso, f[0]);
-      static_for<0, 4>([&](auto S) {
-        constexpr int s = decltype(S)::value;
-        land(f[s & 1]);
-        if constexpr (s < 3) issue(std::integral_constant<int, s + 1>{}, dso, xso, f[(s + 1) & 1]);
-#pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-          for (int jb = 0; jb < 9; ++jb)
-            acc[a][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[s & 1].b[jb], f[s & 1].a[a], acc[a][jb], 0, 0, 0);
+      // sched_barrier: the scheduler otherwise sinks each unit's reads below the
+      // MFMAs of the unit before (fewer live VGPRs), so every unit waited out a
+      // full LDS round trip in front of its MFMAs
+      static_for<0, 11>([&](auto U) {
+        land_unit(U);
+        issue_unit(std::integral_constant<int, decltype(U)::value + 1>{}, dso, xso);
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_unit(U);
+        __builtin_amdgcn_sched_barrier(0);
       });
+      land_unit(std::integral_constant<int, 11>{});   // this wave reads nothing more of row i
+      wait_vmcnt<4>();     // input row i+2 and dy row i+1 landed
+      raw_barrier();
+      fetch_x(n, i + 4);
+      fetch_d(n, i + 3);
+      // unconditional (a branch here made the compiler copy the in-flight
+      // fragment registers at the merge); past the last row it reads stale slots
+      slots(i + 1, dso, xso);
+      issue_unit(std::integral_constant<int, 0>{}, dso, xso);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_unit(std::integral_constant<int, 11>{});
+      __builtin_amdgcn_sched_barrier(0);
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // no read in flight past the image
   }
+  wait_vmcnt<0>();
   // lane (g, i) holds columns 16 b + 4g .. +3 of output channel 16 (2ch + a) + i
   float* out = ws + (size_t)blockIdx.x * (64 * 576);
   const int i16 = lane & 15;
