@@ -14,7 +14,7 @@ namespace vlp {
 
 // NesT short-K / short-side token GEMMs on gemm_big_kernel (tools/build_variant.sh A/B knobs)
 #ifndef VLP_LIN_SHORTK
-#define VLP_LIN_SHORTK 0
+#define VLP_LIN_SHORTK 1
 #endif
 #ifndef VLP_LINW_BIG
 #define VLP_LINW_BIG 1
@@ -195,8 +195,12 @@ static int gemm_lin(int M, int N, int K, int ksplit, const LA& la, const LB& lb,
     // short-K token GEMMs (NesT levels 0 / 1: K = 96 / 192 over 0.5-2 M token rows)
     // are HBM-bound: the LDS-DMA kernel with two K-tiles in flight instead of the
     // one-tile ring (the loaders zero-fill the K tail)
+    // (r6, tools/nest_gemm_bench.py, profiles/r6_lin_shortk_ab.txt: wins at K >= 192 --
+    // level 1 fc1 674 -> 550 us, fc2 410 -> 349, qkv 345 -> 318, level-0 fc2 618 -> 548 --
+    // and for N <= 128; loses on the K = 96, N >= 288 level-0 qkv / fc1: 674 -> 780,
+    // 1123 -> 1324, which keep the one-tile ring)
     if constexpr (LA::kKContig && LB::kKContig) {
-      if (VLP_LIN_SHORTK && gemm_variant() >= 5 && M >= 65536 && N >= 96)
+      if (VLP_LIN_SHORTK && gemm_variant() >= 5 && M >= 65536 && N >= 96 && (K >= 192 || N <= 128))
         return gemm_big_auto(M, N, K, ksplit, la, lb, ep, st);
     }
   }
