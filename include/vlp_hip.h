@@ -140,6 +140,13 @@ int vlp_conv_wgrad_ws(int dtype, const void* dy, const void* x, float* split_ws,
                       void* stream);
 int vlp_conv_wgrad_fold(int Co, int C, int KH, int KW, int nsplit, const float* split_ws, float* grad,
                         void* stream);
+/* vlp_conv_wgrad_ws takes the layer-1 row-streaming kernel (bf16, C = Co = 64,
+ * 3x3/1 pad 1, W = 128; one workgroup per image, one slab each) when the batch
+ * holds at least this many images, else the im2col GEMM.  n < 0 restores the
+ * default (3/4 of the device's CUs: below it the per-image workgroups leave the
+ * chip idle).  *prev (may be null) receives the previous setting (-1 = default).
+ * Returns 0.  Host-only, no GPU work. */
+int vlp_set_wgrad_rows_min_images(int n, int* prev);
 /* dw_ws[Co][KH][KW][C] += sum over pixels dy x_patch (fp32 atomics; zero first).
  * Optional BN+ReLU-on-load of x as in vlp_conv_fwd. */
 int vlp_conv_wgrad(int dtype, const void* dy, const void* x, float* dw_ws, int N, int H, int W,

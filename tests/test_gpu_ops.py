@@ -462,14 +462,21 @@ def test_conv_wgrad_rows_layer1(ops, N, H, slabs):
     dyd, xd = nhwc(dy).to(dt).cuda(), nhwc(x.detach()).to(dt).cuda()
     st = torch.cuda.current_stream().cuda_stream
     outs = []
-    for _ in range(2):
-        g = torch.full((C, C, 3, 3), float("nan"), device="cuda")
-        ns = ctypes.c_int(0)
-        assert lib().vlp_conv_wgrad_ws(1, dyd.data_ptr(), xd.data_ptr(), ws.data_ptr(), nws, ctypes.addressof(ns),
-                                       N, H, W, C, C, 3, 3, 1, 1, st) == 0
-        assert ns.value == min(N, slabs or N), ns.value   # one slab per workgroup
-        lib().vlp_conv_wgrad_fold(C, C, 3, 3, ns.value, ws.data_ptr(), g.data_ptr(), st)
-        outs.append(g)
+    # the product gate takes the row-streaming form from 3/4 of the CU count in
+    # images up (bs 256); force it for these small batches
+    prev = ctypes.c_int(0)
+    lib().vlp_set_wgrad_rows_min_images(1, ctypes.addressof(prev))
+    try:
+        for _ in range(2):
+            g = torch.full((C, C, 3, 3), float("nan"), device="cuda")
+            ns = ctypes.c_int(0)
+            assert lib().vlp_conv_wgrad_ws(1, dyd.data_ptr(), xd.data_ptr(), ws.data_ptr(), nws,
+                                           ctypes.addressof(ns), N, H, W, C, C, 3, 3, 1, 1, st) == 0
+            assert ns.value == min(N, slabs or N), ns.value   # one slab per workgroup
+            lib().vlp_conv_wgrad_fold(C, C, 3, 3, ns.value, ws.data_ptr(), g.data_ptr(), st)
+            outs.append(g)
+    finally:
+        lib().vlp_set_wgrad_rows_min_images(prev.value, None)
     torch.cuda.synchronize()
     assert torch.isnan(ws[nws:]).all().item(), "slab writes past the workspace"
     assert torch.equal(outs[0], outs[1])

@@ -1903,9 +1903,14 @@ conv3x3_c64_wgrad_rows_kernel(int N, int H, const bf16* __restrict__ dy, const b
       *reinterpret_cast<v4f*>(out + (size_t)(16 * (2 * ch + a) + i16) * 576 + 16 * (9 * cq + jb) + 4 * g) = acc[a][jb];
 }
 
+// smallest batch (images) for the row-streaming form: one workgroup per image, so
+// a batch well below the CU count leaves most of the chip idle (the per-image
+// time is fixed) where the im2col GEMM spreads the pixels over every CU
+static int g_wgrad_rows_min = -1;   // -1: 3/4 of the device's CUs
 static bool wgrad_rows_ok(const ConvGeom& g) {
+  const int mn = g_wgrad_rows_min >= 0 ? g_wgrad_rows_min : device_cus() * 3 / 4;
   return VLP_WGRAD_ROWS && g.C == 64 && g.Co == 64 && g.KH == 3 && g.KW == 3 && g.S == 1 && g.P == 1 &&
-         g.W == kRcW && g.H >= 1 && (size_t)g.N * g.H * kRcW * 128 < (1ull << 31);
+         g.W == kRcW && g.H >= 1 && g.N >= mn && (size_t)g.N * g.H * kRcW * 128 < (1ull << 31);
 }
 // one slab per workgroup: grid <= the slabs the workspace holds
 static int launch_wgrad_rows(const ConvGeom& g, const void* dy, const void* x, float* ws, int max_ks, int* ks_out,
@@ -2795,6 +2800,12 @@ VLP_EXPORT int vlp_conv_wgrad_ws(int dtype, const void* dy, const void* x, float
   if (!nsplit || (long long)N * H * W * C >= (1ll << 31)) return (int)hipErrorInvalidValue;
   if (dtype == VLP_BF16) return conv_wgrad_ws_t<bf16>(dy, x, split_ws, ws_floats, nsplit, g, st);
   return conv_wgrad_ws_t<float>(dy, x, split_ws, ws_floats, nsplit, g, st);
+}
+
+VLP_EXPORT int vlp_set_wgrad_rows_min_images(int n, int* prev) {
+  if (prev) *prev = g_wgrad_rows_min;
+  g_wgrad_rows_min = n < 0 ? -1 : n;
+  return 0;
 }
 
 VLP_EXPORT int vlp_conv_wgrad_fold(int Co, int C, int KH, int KW, int nsplit, const float* split_ws, float* grad,
