@@ -484,6 +484,41 @@ def test_conv_wgrad_rows_layer1(ops, N, H, slabs):
     assert err < 1e-5, err   # fp32 sums of exact bf16 products: only the summation order differs
 
 
+def test_conv_wgrad_rows_gate_vs_gemm(ops):
+    """The default gate: a batch of at least 3/4 of the CU count in images takes the
+    row-streaming kernel (one slab per workgroup), a forced minimum above the batch
+    takes the im2col GEMM; both fold to the same fp32 weight gradient."""
+    import ctypes
+    from vlp_amd._lib import lib
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    N, H, W, C = max(1, (3 * cus) // 4) + 3, 3, 128, 64
+    torch.manual_seed(12)
+    dyd = torch.randn(N, H, W, C, device="cuda").to(torch.bfloat16)
+    xd = torch.randn(N, H, W, C, device="cuda").to(torch.bfloat16)
+    slab = C * C * 9
+    nws = 4 * N * slab
+    ws = torch.empty(nws, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    res = {}
+    for name, mn in (("rows", -1), ("gemm", 1 << 30)):
+        prev = ctypes.c_int(0)
+        lib().vlp_set_wgrad_rows_min_images(mn, ctypes.addressof(prev))
+        try:
+            g = torch.full((C, C, 3, 3), float("nan"), device="cuda")
+            ns = ctypes.c_int(0)
+            lib().vlp_conv_wgrad_ws(1, dyd.data_ptr(), xd.data_ptr(), ws.data_ptr(), nws, ctypes.addressof(ns),
+                                    N, H, W, C, C, 3, 3, 1, 1, st)
+            lib().vlp_conv_wgrad_fold(C, C, 3, 3, ns.value, ws.data_ptr(), g.data_ptr(), st)
+            torch.cuda.synchronize()
+            res[name] = (g.clone(), ns.value)
+        finally:
+            lib().vlp_set_wgrad_rows_min_images(prev.value, None)
+    assert res["rows"][1] == min(N, cus), res["rows"][1]   # one slab per image workgroup
+    a, b = res["rows"][0], res["gemm"][0]
+    assert torch.isfinite(a).all() and torch.isfinite(b).all()
+    assert (a - b).abs().max().item() <= 1e-5 * b.abs().max().item()
+
+
 @pytest.mark.parametrize("dt", DT)
 @pytest.mark.parametrize("N,H,W,C", [(2, 10, 10, 64), (2, 4, 128, 64), (4, 7, 7, 512), (2, 14, 14, 256),
                                      (2, 8, 64, 128), (2, 16, 16, 512)])
