@@ -544,7 +544,16 @@ def main():
             opt.step()
         return loss
 
-    prefetched_steps(2)   # warm the copy stream and the pinned buffers
+    # warm the copy stream and the pinned buffers: at least W prefetched steps and
+    # 1 s of them (r6: on some boxes the first second of uploads from freshly
+    # pinned pages ran at ~0.8 GB/s while the same process's later prefetched
+    # windows ran at full rate)
+    t_w = time.perf_counter()
+    prefetched_steps(max(2, args.warmup))
+    torch.cuda.synchronize()
+    while time.perf_counter() - t_w < 1.0:
+        prefetched_steps(2)
+        torch.cuda.synchronize()
     el, loss = timed(lambda: prefetched_steps(args.steps))
     rehearsal = None
     if world == 1 and args.dp_rehearsal:
