@@ -151,10 +151,9 @@ _COPY_STREAMS = {}
 
 
 def _copy_stream(device):
-    """One upload stream per device for every prefetcher: a new stream per epoch
-    (per iterator) also moves the process's later streams -- RCCL's among them --
-    to other hardware queues (GPU_MAX_HW_QUEUES is 4): the world-1 RCCL rehearsal
-    in bench.py ran 3.5 % slower after a dozen short prefetch loops."""
+    """One upload stream per device shared by every prefetcher (a new stream per
+    epoch / iterator would keep adding streams onto the process's few hardware
+    queues)."""
     s = _COPY_STREAMS.get(device)
     if s is None:
         s = _COPY_STREAMS[device] = torch.cuda.Stream(device=device)
