@@ -6,7 +6,8 @@ at bs=256/GPU, 512x512, T=40, bf16 (BASELINE.json configs[1]; configs[2] for
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
 
-One process per GPU (RCCL over xGMI for N > 1), W untimed warm-up steps, then
+One process per GPU (RCCL over xGMI for N > 1), W untimed warm-up steps (more,
+untimed, until --warmup-seconds have passed, the same count on every rank), then
 exactly K timed steps bracketed by barrier + synchronize; the max over ranks is
 reported.  `value` times the K steps on a batch resident in HBM when the clock
 starts (the bench contract: the PCIe-inclusive rate is never `value`).
